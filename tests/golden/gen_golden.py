@@ -1,0 +1,478 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE.
+
+Test infrastructure only.  This script imports the read-only reference checkout
+(``/root/reference``, titanium-47/decision-pretrained-transformer) on CPU and
+records inputs + outputs of the hot-path functions as small ``.npz`` files.
+The reference never travels with the repo: only these vectors do.
+
+Randomness is captured, not re-implemented: every ``np.random.choice`` /
+``np.random.normal`` call the reference makes is wrapped; before the real call
+a replica ``RandomState`` is built from the global state and asked for the one
+``random_sample()`` / ``standard_normal()`` draw the call consumes.  After the
+real call the replica and the global state are asserted identical, which proves
+the recorded draw is exactly what the reference used.  This pins the two
+algebraic identities the device path relies on:
+
+* ``np.random.choice(A, p=p) == searchsorted(cumsum(p64)/cumsum(p64)[-1], u, 'right')``
+  (numpy legacy ``RandomState.choice``, numpy 2.2.6 — not vendored in the reference),
+* ``np.random.normal(0, s) == 0.0 + s * g`` with ``g = standard_normal()``.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+The script refuses to run when /root/reference is absent (GPU box).
+"""
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True  # never leave __pycache__ in the reference tree
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _install_stubs():
+    """Minimal stand-ins for modules the reference imports but never computes with.
+
+    gym: only ``gym.Env`` (base class) and ``gym.spaces.Box/Discrete`` (attribute
+    holders) are touched (envs/base_env.py:8, envs/bandit_env.py:37-38,
+    envs/darkroom_env.py:19-21).  IPython: ``embed`` is imported, never called.
+    skimage: ``resize`` is imported at collect_data.py:8 for Miniworld only.
+    """
+    gym = types.ModuleType("gym")
+
+    class Env:  # noqa: D401
+        pass
+
+    class Box:
+        def __init__(self, low=None, high=None, shape=None):
+            self.low, self.high, self.shape = low, high, shape
+
+    class Discrete:
+        def __init__(self, n):
+            self.n = n
+
+    gym.Env = Env
+    gym.spaces = types.SimpleNamespace(Box=Box, Discrete=Discrete)
+    sys.modules["gym"] = gym
+    ipy = types.ModuleType("IPython")
+    ipy.embed = lambda *a, **k: None
+    ipy.get_ipython = lambda: None
+    sys.modules["IPython"] = ipy
+    sk = types.ModuleType("skimage")
+    skt = types.ModuleType("skimage.transform")
+    skt.resize = lambda *a, **k: None
+    sk.transform = skt
+    sys.modules["skimage"] = sk
+    sys.modules["skimage.transform"] = skt
+
+
+class DrawRecorder:
+    """Wraps np.random.choice / np.random.normal and records the consumed draws."""
+
+    def __init__(self, np):
+        self.np = np
+        self.u = []
+        self.g = []
+        self.choice_kind = []
+        self.plain = []
+        self._choice = np.random.choice
+        self._normal = np.random.normal
+
+    def _replica(self):
+        rs = self.np.random.RandomState()
+        rs.set_state(self.np.random.get_state())
+        return rs
+
+    def _same_state(self, rs):
+        a = self.np.random.get_state()
+        b = rs.get_state()
+        return (a[0] == b[0] and (a[1] == b[1]).all() and a[2] == b[2]
+                and a[3] == b[3] and a[4] == b[4])
+
+    def choice(self, a, size=None, replace=True, p=None):
+        np = self.np
+        if p is not None and size is None:
+            rs = self._replica()
+            u = rs.random_sample()
+            out = self._choice(a, size=size, replace=replace, p=p)
+            assert self._same_state(rs), "choice consumed != one uniform"
+            p64 = np.asarray(p, dtype=np.float64)
+            cdf = p64.cumsum()
+            cdf /= cdf[-1]
+            idx = int(cdf.searchsorted(u, side="right"))
+            assert np.asarray(a)[idx] == out, "choice != searchsorted(cdf,u)"
+            self.u.append(u)
+            self.choice_kind.append(1)
+            return out
+        out = self._choice(a, size=size, replace=replace, p=p)
+        self.choice_kind.append(0)
+        self.plain.append(out)
+        return out
+
+    def normal(self, loc=0.0, scale=1.0, size=None):
+        np = self.np
+        if size is None and np.ndim(loc) == 0 and np.ndim(scale) == 0:
+            rs = self._replica()
+            g = rs.standard_normal()
+            out = self._normal(loc, scale)
+            assert self._same_state(rs), "normal consumed != one gaussian"
+            assert out == loc + scale * g, "normal(loc,s) != loc + s*g"
+            self.g.append(g)
+            return out
+        return self._normal(loc, scale, size)
+
+    def __enter__(self):
+        self.np.random.choice = self.choice
+        self.np.random.normal = self.normal
+        return self
+
+    def __exit__(self, *exc):
+        self.np.random.choice = self._choice
+        self.np.random.normal = self._normal
+
+
+def perturbed_state_dict(model, seed, scale=0.05):
+    """Reference init (GPT2 scheme) + seeded N(0,1)*scale perturbation so every
+    parameter (LN gains/biases included) carries signal."""
+    import numpy as np
+    import torch
+    rs = np.random.RandomState(seed)
+    sd = model.state_dict()
+    for k in sorted(sd.keys()):
+        v = sd[k]
+        if k.endswith("wte.weight") or not v.dtype.is_floating_point:
+            continue
+        noise = torch.from_numpy(rs.standard_normal(tuple(v.shape)).astype(np.float32))
+        sd[k] = v + scale * noise
+    model.load_state_dict(sd)
+    return {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()
+            if not k.endswith("wte.weight")}
+
+
+def main():
+    if not os.path.isdir(REF):
+        raise SystemExit("reference checkout not present; fixtures are committed")
+    _install_stubs()
+    import matplotlib
+    matplotlib.use("Agg")
+    sys.path[:0] = [REF, os.path.join(REF, "models")]
+    import numpy as np
+    import torch
+    torch.set_num_threads(8)
+    from net import Transformer  # models/net.py:9
+    from envs import bandit_env, darkroom_env
+    from ctrls.ctrl_bandit import BanditTransformerController
+    from ctrls.ctrl_darkroom import DarkroomTransformerController
+    from evals import eval_bandit, eval_darkroom, eval_linear_bandit
+    import collect_data
+
+    # ---------------------------------------------------------------- F1 bandit transit
+    rs = np.random.RandomState(11)
+    N, A = 64, 5
+    means = rs.uniform(0, 1, (N, A))
+    act = rs.randint(0, A, N)
+    out = {"means": means, "action": act}
+    for var in (0.0, 0.3, 1.0):
+        np.random.seed(100 + int(var * 10))
+        with DrawRecorder(np) as rec:
+            rew = []
+            for i in range(N):
+                env = bandit_env.BanditEnv(means[i], 1, var=var)
+                u = np.zeros(A)
+                u[act[i]] = 1.0
+                env.reset()
+                _, r, done, _ = env.step(u)  # envs/bandit_env.py:66-74
+                assert done
+                rew.append(r)
+        out[f"g_var{var}"] = np.array(rec.g)
+        out[f"reward_var{var}"] = np.array(rew, dtype=np.float64)
+    # linear bandit: means = arms @ theta (envs/bandit_env.py:158-161)
+    arms = np.random.RandomState(1234).normal(size=(20, 2)) / np.sqrt(2)
+    thetas = rs.normal(0, 1, (16, 2)) / np.sqrt(2)
+    lin_means = np.stack([bandit_env.LinearBanditEnv(t, arms, 10, var=0.3).means for t in thetas])
+    out.update(lin_arms=arms, lin_theta=thetas, lin_means=lin_means,
+               lin_opt=np.array([bandit_env.LinearBanditEnv(t, arms, 10).opt_a_index for t in thetas]))
+    # arm value = np.sum(means * onehot) (envs/bandit_env.py:151-153)
+    vec = bandit_env.BanditEnvVec([bandit_env.BanditEnv(m, 1) for m in means])
+    onehot = np.eye(A)[act]
+    out["arm_value"] = vec.get_arm_value(onehot)
+    out["opt_index"] = np.array([e.opt_a_index for e in vec.envs])
+    np.savez_compressed(os.path.join(OUT, "bandit_transit.npz"), **out)
+    print("F1 bandit_transit")
+
+    # ---------------------------------------------------------------- F2 darkroom table
+    dim = 10
+    states = np.array([(x, y) for x in range(dim) for y in range(dim)])
+    nxt = np.zeros((100, 5, 100, 2), np.int8)
+    rew = np.zeros((100, 5, 100), np.int8)
+    opt = np.zeros((100, 100), np.int8)
+    for gi, goal in enumerate(states):
+        env = darkroom_env.DarkroomEnv(dim, goal, 100)
+        for si, s in enumerate(states):
+            opt[gi, si] = np.argmax(env.opt_action(s))
+            for a in range(5):
+                ns, r = env.transit(s, np.eye(5)[a])  # envs/darkroom_env.py:37-55
+                nxt[gi, a, si] = ns
+                rew[gi, a, si] = r
+    pn = np.zeros((120, 5, 100, 2), np.int8)
+    pr = np.zeros((120, 5, 100), np.int8)
+    popt = np.zeros((120, 100), np.int8)
+    perms = np.zeros((120, 5), np.int8)
+    for pi in range(120):
+        env = darkroom_env.DarkroomEnvPermuted(dim, pi, 100)
+        perms[pi] = env.perm
+        for si, s in enumerate(states):
+            popt[pi, si] = np.argmax(env.opt_action(s))
+            for a in range(5):
+                ns, r = env.transit(s, np.eye(5)[a])
+                pn[pi, a, si] = ns
+                pr[pi, a, si] = r
+    np.savez_compressed(os.path.join(OUT, "darkroom_transit.npz"), states=states,
+                        next_state=nxt, reward=rew, opt_action=opt, perms=perms,
+                        perm_next_state=pn, perm_reward=pr, perm_opt_action=popt)
+    print("F2 darkroom_transit")
+
+    # ---------------------------------------------------------------- F3 forward logits
+    def make_model(sd_, ad, H, L=4, seed=0):
+        cfg = dict(horizon=H, state_dim=sd_, action_dim=ad, n_layer=L, n_embd=32,
+                   n_head=4, dropout=0.0, test=True)
+        m = Transformer(cfg)
+        w = perturbed_state_dict(m, seed)
+        m.eval()
+        return m, w, cfg
+
+    def rand_context(rs, n, t, sd_, ad, kind):
+        if kind == "darkroom":
+            cs = rs.randint(0, 10, (n, t, sd_)).astype(np.float64)
+            cn = rs.randint(0, 10, (n, t, sd_)).astype(np.float64)
+            cr = (rs.uniform(size=(n, t, 1)) < 0.1).astype(np.float64)
+            q = rs.randint(0, 10, (n, sd_)).astype(np.float64)
+        else:
+            cs = np.ones((n, t, sd_))
+            cn = np.ones((n, t, sd_))
+            cr = rs.normal(0.5, 0.5, (n, t, 1))
+            q = np.ones((n, sd_))
+        ca = np.eye(ad)[rs.randint(0, ad, (n, t))]
+        return q, cs, ca, cn, cr
+
+    models = {}
+    for name, sd_, ad, H, Ts, kind in (
+            ("bandit5", 1, 5, 500, (1, 2, 8, 101, 501), "bandit"),
+            ("darkroom", 2, 5, 100, (1, 2, 8, 101), "darkroom"),
+            ("linear20", 1, 20, 200, (1, 8, 201), "bandit")):
+        model, w, cfg = make_model(sd_, ad, H, seed={"bandit5": 5, "darkroom": 10, "linear20": 20}[name])
+        models[name] = (model, cfg)
+        out = {f"w/{k}": v for k, v in w.items()}
+        out["cfg"] = np.array([H, sd_, ad, 4, 32])
+        rs = np.random.RandomState(7)
+        for T in Ts:
+            q, cs, ca, cn, cr = rand_context(rs, 16, T - 1, sd_, ad, kind)
+            batch = {
+                "query_states": torch.tensor(q).float(),
+                "zeros": torch.zeros(16, sd_ ** 2 + ad + 1),
+                "context_states": torch.tensor(cs).float(),
+                "context_actions": torch.tensor(ca).float(),
+                "context_next_states": torch.tensor(cn).float(),
+                "context_rewards": torch.tensor(cr).float(),
+            }
+            with torch.no_grad():
+                model.test = True
+                logits = model(batch).numpy()
+                model.test = False
+                allp = model(batch).numpy()  # models/net.py:60 preds[:, 1:]
+                model.test = True
+            out.update({f"T{T}/query": q, f"T{T}/cs": cs, f"T{T}/ca": ca, f"T{T}/cn": cn,
+                        f"T{T}/cr": cr, f"T{T}/logits": logits, f"T{T}/preds_train": allp})
+        np.savez_compressed(os.path.join(OUT, f"forward_{name}.npz"), **out)
+        print("F3 forward", name)
+
+    # ---------------------------------------------------------------- F4 selection
+    out = {}
+    for A_, n in ((5, 512), (20, 256)):
+        rs = np.random.RandomState(3 + A_)
+        logits = (rs.normal(0, 2.0, (n, A_))).astype(np.float32)
+
+        class _Stub(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.config = {"action_dim": A_, "state_dim": 1}
+                self.horizon = 10
+
+            def forward(self, batch):
+                return torch.from_numpy(logits)
+
+        ctrl = BanditTransformerController(_Stub(), sample=True, batch_size=n)
+        ctrl.set_batch({})
+        np.random.seed(2024 + A_)
+        with DrawRecorder(np) as rec:
+            oh = ctrl.act_numpy_vec([np.array([1])] * n)  # ctrls/ctrl_bandit.py:422-444
+        out[f"A{A_}/logits"] = logits
+        out[f"A{A_}/u"] = np.array(rec.u)
+        out[f"A{A_}/sampled"] = oh.argmax(-1)
+        ctrl.sample = False
+        out[f"A{A_}/greedy"] = ctrl.act_numpy_vec([np.array([1])] * n).argmax(-1)
+    np.savez_compressed(os.path.join(OUT, "select.npz"), **out)
+    print("F4 select")
+
+    # ---------------------------------------------------------------- F5 bandit rollouts
+    def bandit_rollout(model, ad, n, H, var, sample, seed, linear=False):
+        rs = np.random.RandomState(seed)
+        if linear:
+            arms = np.random.RandomState(1234).normal(size=(ad, 2)) / np.sqrt(2)
+            thetas = rs.normal(0, 1, (n, 2)) / np.sqrt(2)
+            envs = [bandit_env.LinearBanditEnv(t, arms, H, var=var) for t in thetas]
+            mod = eval_linear_bandit
+        else:
+            means = rs.uniform(0, 1, (n, ad))
+            envs = [bandit_env.BanditEnv(m, H, var=var) for m in means]
+            mod = eval_bandit
+        vec = bandit_env.BanditEnvVec(envs)
+        ctrl = BanditTransformerController(model, sample=sample, batch_size=n)
+        logs = []
+        orig_fwd = model.forward
+
+        def fwd(batch):
+            o = orig_fwd(batch)
+            logs.append(o.detach().numpy().copy())
+            return o
+
+        model.forward = fwd
+        np.random.seed(seed + 1)
+        try:
+            with DrawRecorder(np) as rec, torch.no_grad():
+                cm, meta = mod.deploy_online_vec(vec, ctrl, H, include_meta=True)
+        finally:
+            model.forward = orig_fwd
+        res = {"means": np.stack([e.means for e in envs]), "cum_means": cm,
+               "logits": np.stack(logs), "ctx_actions": meta["context_actions"],
+               "ctx_rewards": meta["context_rewards"][..., 0],
+               "ctx_states": meta["context_states"], "ctx_next_states": meta["context_next_states"],
+               "cfg": np.array([n, H, ad, int(sample)]), "var": np.float64(var)}
+        res["u"] = np.array(rec.u).reshape(H, n) if sample else np.zeros((H, n))
+        res["g"] = np.array(rec.g).reshape(H, n)
+        if linear:
+            res["arms"] = arms
+            res["theta"] = np.stack([e.theta for e in envs])
+        return res
+
+    m5, _ = models["bandit5"]
+    for tag, kw in (("sample", dict(sample=True, var=0.3)), ("greedy", dict(sample=False, var=0.3)),
+                    ("var0", dict(sample=True, var=0.0))):
+        r = bandit_rollout(m5, 5, 8, 40, seed=31, **kw)
+        np.savez_compressed(os.path.join(OUT, f"rollout_bandit_{tag}.npz"), **r)
+    m20, _ = models["linear20"]
+    r = bandit_rollout(m20, 20, 6, 24, 0.3, True, 41, linear=True)
+    np.savez_compressed(os.path.join(OUT, "rollout_linear_sample.npz"), **r)
+    print("F5 bandit rollouts")
+
+    # online regret math on the Opt + Lnr legs (evals/eval_bandit.py:123-178)
+    import scipy.stats
+    r = dict(np.load(os.path.join(OUT, "rollout_bandit_sample.npz")))
+    opt = np.stack([r["means"].max(-1)] * r["cum_means"].shape[0])  # Opt leg: means[opt_a]
+    diff = (opt - r["cum_means"]).T
+    cr = np.cumsum(diff, axis=1)
+    np.savez_compressed(os.path.join(OUT, "regret_math.npz"), lnr=r["cum_means"].T, opt=opt.T,
+                        subopt_mean=np.mean(diff, 0), subopt_sem=scipy.stats.sem(diff, 0),
+                        regret_mean=np.mean(cr, 0), regret_sem=scipy.stats.sem(cr, 0))
+
+    # ---------------------------------------------------------------- offline greedy (var=0 deploy_eval)
+    rs = np.random.RandomState(51)
+    n, h = 8, 50
+    means = rs.uniform(0, 1, (n, 5))
+    envs = [bandit_env.BanditEnv(m, h, var=0.3) for m in means]
+    vec = bandit_env.BanditEnvVec(envs)
+    ca = np.eye(5)[rs.randint(0, 5, (n, h))]
+    cr = (means[np.arange(n)[:, None], ca.argmax(-1)] + 0.3 * rs.normal(size=(n, h)))[..., None]
+    batch = {"context_states": np.ones((n, h, 1)), "context_actions": ca,
+             "context_next_states": np.ones((n, h, 1)), "context_rewards": cr}
+    ctrl = BanditTransformerController(m5, sample=False, batch_size=n)
+    ctrl.set_batch_numpy_vec(batch)
+    with torch.no_grad():
+        _, us, _, rs_ = vec.deploy_eval(ctrl)  # envs/bandit_env.py:114-123 (var forced to 0)
+    np.savez_compressed(os.path.join(OUT, "offline_bandit.npz"), means=means, ctx_actions=ca,
+                        ctx_rewards=cr[..., 0], actions=us.argmax(-1), rewards=rs_)
+    print("F5b offline")
+
+    # ---------------------------------------------------------------- F6 darkroom rollouts
+    mdr, _ = models["darkroom"]
+
+    def darkroom_rollout(n, Heps, H, horizon, sample, seed, permuted=False):
+        rs = np.random.RandomState(seed)
+        if permuted:
+            idx = rs.randint(0, 120, n)
+            envs = [darkroom_env.DarkroomEnvPermuted(10, int(i), horizon) for i in idx]
+        else:
+            goals = rs.randint(0, 10, (n, 2))
+            envs = [darkroom_env.DarkroomEnv(10, g, horizon) for g in goals]
+        vec = darkroom_env.DarkroomEnvVec(envs)
+        ctrl = DarkroomTransformerController(mdr, batch_size=n, sample=sample)
+        logs = []
+        orig_fwd = mdr.forward
+
+        def fwd(batch):
+            o = orig_fwd(batch)
+            logs.append(o.detach().numpy().copy())
+            return o
+
+        mdr.forward = fwd
+        np.random.seed(seed + 1)
+        try:
+            with DrawRecorder(np) as rec, torch.no_grad():
+                ret = eval_darkroom.deploy_online_vec(vec, ctrl, Heps, H, horizon)
+        finally:
+            mdr.forward = orig_fwd
+        res = {"goals": np.stack([e.goal for e in envs]), "returns": ret,
+               "logits": np.stack(logs), "cfg": np.array([n, Heps, H, horizon, int(sample)])}
+        res["u"] = (np.array(rec.u).reshape(Heps, horizon, n) if sample
+                    else np.zeros((Heps, horizon, n)))
+        if permuted:
+            res["perm_index"] = idx
+        return res
+
+    for tag, kw in (("sample", dict(sample=True)), ("greedy", dict(sample=False))):
+        r = darkroom_rollout(6, 5, 20, 10, seed=61, **kw)
+        np.savez_compressed(os.path.join(OUT, f"rollout_darkroom_{tag}.npz"), **r)
+    r = darkroom_rollout(4, 3, 10, 10, True, 71, permuted=True)
+    np.savez_compressed(os.path.join(OUT, "rollout_darkroom_permuted.npz"), **r)
+    print("F6 darkroom rollouts")
+
+    # ---------------------------------------------------------------- F7 rollin (collect_data)
+    np.random.seed(0)
+    out = {}
+    for i in range(6):
+        env = bandit_env.sample(5, 20, 0.3)  # envs/bandit_env.py:10-18
+        rec_vals = {}
+        real_dir = np.random.dirichlet
+
+        def dirichlet(alpha, _r=real_dir):
+            v = _r(alpha)
+            rec_vals["probs"] = v
+            return v
+
+        np.random.dirichlet = dirichlet
+        try:
+            with DrawRecorder(np) as rec:
+                xs, us, xps, rs_ = collect_data.rollin_bandit(env, cov=0.0)
+            # the two no-p choices: cov pick, then the random arm (collect_data.py:30-35)
+            picks = rec.plain
+        finally:
+            np.random.dirichlet = real_dir
+        out[f"{i}/means"] = env.means
+        out[f"{i}/cov"] = np.float64(picks[0])
+        out[f"{i}/dirichlet"] = rec_vals["probs"]
+        out[f"{i}/rand_index"] = np.int64(picks[1])
+        out[f"{i}/u"] = np.array(rec.u)
+        out[f"{i}/g"] = np.array(rec.g)
+        out[f"{i}/xs"], out[f"{i}/us"], out[f"{i}/xps"], out[f"{i}/rs"] = xs, us, xps, rs_
+    # rollin_mdp (uniform): draws are the sampled (state, action) pairs themselves
+    np.random.seed(1)
+    env = darkroom_env.DarkroomEnv(10, np.array([3, 7]), 12)
+    s, a, ns, r = collect_data.rollin_mdp(env, "uniform")  # collect_data.py:83-111
+    out.update({"mdp/states": s, "mdp/actions": a, "mdp/next_states": ns, "mdp/rewards": r,
+                "mdp/goal": env.goal})
+    np.savez_compressed(os.path.join(OUT, "rollin.npz"), **out)
+    print("F7 rollin")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+"""Pin the CPU oracle (oracle/dpt_oracle.py) against vectors recorded from the reference."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import dpt_oracle as O
+
+
+def weights(name):
+    g = golden(f"forward_{name}.npz")
+    w = {k[2:]: v for k, v in g.items() if k.startswith("w/")}
+    return g, O.split_weights(w, int(g["cfg"][3]))
+
+
+def test_bandit_transit_bit_exact():
+    g = golden("bandit_transit.npz")
+    for var in (0.0, 0.3, 1.0):
+        r = O.bandit_reward(g["means"], g["action"], g[f"g_var{var}"], var)
+        assert np.array_equal(r.view(np.int64), g[f"reward_var{var}"].view(np.int64))
+    assert np.array_equal(O.arm_value(g["means"], g["action"]), g["arm_value"])
+    assert np.array_equal(np.argmax(g["means"], 1), g["opt_index"])
+    lm = O.linear_means(g["lin_arms"], g["lin_theta"])
+    assert np.array_equal(lm, g["lin_means"])
+    assert np.array_equal(np.argmax(lm, 1), g["lin_opt"])
+
+
+def test_darkroom_exhaustive_table():
+    g = golden("darkroom_transit.npz")
+    st = g["states"]
+    for gi in range(100):
+        goal = np.broadcast_to(st[gi], st.shape)
+        assert np.array_equal(O.darkroom_opt_action(st, goal), g["opt_action"][gi])
+        for a in range(5):
+            ns, r = O.darkroom_transit(st, np.full(100, a), goal)
+            assert np.array_equal(ns, g["next_state"][gi, a])
+            assert np.array_equal(r, g["reward"][gi, a])
+    perms = O.perm_table()
+    assert np.array_equal(perms, g["perms"])
+    goal = np.full((100, 2), 9)
+    for pi in range(120):
+        perm = np.broadcast_to(perms[pi], (100, 5))
+        assert np.array_equal(O.darkroom_opt_action(st, goal, perm), g["perm_opt_action"][pi])
+        for a in range(5):
+            ns, r = O.darkroom_transit(st, np.full(100, a), goal, perm=perm)
+            assert np.array_equal(ns, g["perm_next_state"][pi, a])
+            assert np.array_equal(r, g["perm_reward"][pi, a])
+
+
+@pytest.mark.parametrize("name", ["bandit5", "darkroom", "linear20"])
+def test_forward_logits_within_1e5(name):
+    g, W = weights(name)
+    Ts = sorted({int(k.split("/")[0][1:]) for k in g if k.startswith("T")})
+    for T in Ts:
+        args = [g[f"T{T}/{k}"] for k in ("query", "cs", "ca", "cn", "cr")]
+        ref = g[f"T{T}/logits"]
+        got = O.transformer_forward(W, *args)
+        tol = 1e-5 * np.maximum(1.0, np.abs(ref))
+        assert (np.abs(got - ref) <= tol).all(), (T, np.abs(got - ref).max())
+        if T > 1:
+            got_all = O.transformer_forward(W, *args, test=False)
+            ref_all = g[f"T{T}/preds_train"]
+            assert np.abs(got_all - ref_all).max() <= 1e-5 * max(1, np.abs(ref_all).max())
+
+
+def test_selection_matches_reference_choice():
+    g = golden("select.npz")
+    for A in (5, 20):
+        lg, u = g[f"A{A}/logits"], g[f"A{A}/u"]
+        assert np.array_equal(O.select_actions(lg, u), g[f"A{A}/sampled"])
+        assert np.array_equal(O.select_actions(lg, sample=False), g[f"A{A}/greedy"])
+
+
+@pytest.mark.parametrize("tag", ["sample", "greedy", "var0"])
+def test_bandit_rollout_matches_reference(tag):
+    g = golden(f"rollout_bandit_{tag}.npz")
+    _, W = weights("bandit5")
+    n, H, A, sample = g["cfg"]
+    out = O.bandit_online_rollout(W, g["means"], int(H), float(g["var"]), g["u"], g["g"], bool(sample))
+    assert np.abs(out["logits"] - g["logits"]).max() <= 1e-5
+    assert np.array_equal(out["actions"], g["ctx_actions"].argmax(-1))
+    assert np.array_equal(out["cum_means"], g["cum_means"])
+    assert np.array_equal(out["rewards"], g["ctx_rewards"])
+
+
+def test_linear_rollout_matches_reference():
+    g = golden("rollout_linear_sample.npz")
+    _, W = weights("linear20")
+    n, H, A, sample = g["cfg"]
+    assert np.array_equal(O.linear_means(g["arms"], g["theta"]), g["means"])
+    out = O.bandit_online_rollout(W, g["means"], int(H), float(g["var"]), g["u"], g["g"], True)
+    assert np.array_equal(out["cum_means"], g["cum_means"])
+    assert np.array_equal(out["rewards"], g["ctx_rewards"])
+
+
+@pytest.mark.parametrize("tag", ["sample", "greedy", "permuted"])
+def test_darkroom_rollout_matches_reference(tag):
+    g = golden(f"rollout_darkroom_{tag}.npz")
+    _, W = weights("darkroom")
+    n, Heps, H, horizon, sample = (int(x) for x in g["cfg"])
+    perm = None
+    if tag == "permuted":
+        perm = O.perm_table()[g["perm_index"]]
+    out = O.darkroom_online_rollout(W, g["goals"], Heps, H, horizon, g["u"], bool(sample), perm)
+    assert np.abs(out["logits"] - g["logits"]).max() <= 1e-5
+    assert np.array_equal(out["returns"], g["returns"])
+
+
+def test_regret_math():
+    g = golden("regret_math.npz")
+    out = O.regret_curves(g["opt"], g["lnr"])
+    for k in ("subopt_mean", "subopt_sem", "regret_mean", "regret_sem"):
+        np.testing.assert_allclose(out[k], g[k], rtol=1e-12, atol=1e-15)
+
+
+def test_rollin_bandit():
+    g = golden("rollin.npz")
+    for i in range(6):
+        xs, us, xps, rs = O.rollin_bandit(g[f"{i}/means"], float(g[f"{i}/cov"]), g[f"{i}/dirichlet"],
+                                          g[f"{i}/rand_index"], g[f"{i}/u"], g[f"{i}/g"], 0.3)
+        assert np.array_equal(us, g[f"{i}/us"])
+        assert np.array_equal(rs, g[f"{i}/rs"])
+        assert np.array_equal(xs, g[f"{i}/xs"]) and np.array_equal(xps, g[f"{i}/xps"])
+    s, a, ns, r = (g[f"mdp/{k}"] for k in ("states", "actions", "next_states", "rewards"))
+    ns2, r2 = O.darkroom_transit(s, a.argmax(-1), np.broadcast_to(g["mdp/goal"], s.shape))
+    assert np.array_equal(ns2, ns) and np.array_equal(r2, r)
