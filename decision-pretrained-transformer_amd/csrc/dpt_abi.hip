@@ -1,0 +1,218 @@
+// extern "C" surface of libdpt_hip.so (declared in include/dpt_hip.h).
+// Validates shapes on the host (a kernel is never launched on an argument the
+// grid arithmetic does not cover), maps failures to DPT_E* codes and keeps a
+// thread-local message for dpt_last_error().
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <string>
+
+#include "dpt_common.h"
+
+namespace dpt {
+
+static thread_local std::string g_last_error;
+
+void set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = std::string("dpt error ") + std::to_string(code) + ": " + buf;
+}
+
+int check_hip(hipError_t e, const char* what) {
+    if (e == hipSuccess) return DPT_OK;
+    set_error(DPT_EHIP, "%s: %s", what, hipGetErrorString(e));
+    return DPT_EHIP;
+}
+
+// declared in the kernel translation units
+ModelView make_view(const float* blob, const dpt_model_desc& d);
+int64_t weights_numel(const dpt_model_desc& d);
+int launch_decode_step(const ModelView&, float*, int, int, int, const float*, float*, hipStream_t);
+int launch_window_decode(const ModelView&, float*, int, int, const float*, const float*, const float*,
+                         const float*, const float*, int, float*, hipStream_t);
+int launch_rollout_bandit(const ModelView&, const dpt_bandit_rollout_args&, hipStream_t);
+int launch_bandit_step(const double*, int, int, const int32_t*, int, double, const double*, uint64_t, uint64_t,
+                       int64_t, double*, double*, hipStream_t);
+int launch_darkroom_step(const int32_t*, const int32_t*, const int32_t*, const int32_t*, int, int, int32_t*,
+                         int32_t*, hipStream_t);
+int launch_darkroom_opt(const int32_t*, const int32_t*, const int32_t*, int, int32_t*, hipStream_t);
+int launch_select(const float*, int, int, int, float, const double*, uint64_t, uint64_t, int64_t, int32_t*,
+                  hipStream_t);
+int launch_draw(int, uint64_t, uint64_t, int64_t, int, uint32_t, double*, hipStream_t);
+
+}  // namespace dpt
+
+using namespace dpt;
+
+struct dpt_model {
+    dpt_model_desc desc;
+    float* blob;
+    ModelView view;
+};
+
+#define REQUIRE(cond, ...)                         \
+    do {                                           \
+        if (!(cond)) {                             \
+            set_error(DPT_EINVAL, __VA_ARGS__);    \
+            return DPT_EINVAL;                     \
+        }                                          \
+    } while (0)
+
+static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static int validate_desc(const dpt_model_desc* d) {
+    REQUIRE(d != nullptr, "null model desc");
+    if (d->n_embd != kE) {
+        set_error(DPT_EUNSUPPORTED, "n_embd=%d: only n_embd=%d is built", d->n_embd, kE);
+        return DPT_EUNSUPPORTED;
+    }
+    REQUIRE(d->n_layer >= 1 && d->n_layer <= 64, "n_layer=%d out of range", d->n_layer);
+    REQUIRE(d->state_dim >= 1 && d->action_dim >= 1 && d->action_dim <= kMaxA, "state_dim=%d action_dim=%d",
+            d->state_dim, d->action_dim);
+    REQUIRE(2 * d->state_dim + d->action_dim + 1 <= kMaxF, "token features exceed %d", kMaxF);
+    REQUIRE(d->n_positions >= 1, "n_positions=%d", d->n_positions);
+    return DPT_OK;
+}
+
+extern "C" {
+
+int dpt_abi_version(void) { return DPT_ABI_VERSION; }
+
+const char* dpt_last_error(void) { return g_last_error.c_str(); }
+
+int dpt_device_count(int* count) {
+    REQUIRE(count != nullptr, "null count");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return DPT_OK;
+}
+
+int dpt_weights_numel(const dpt_model_desc* d, int64_t* numel) {
+    int rc = validate_desc(d);
+    if (rc) return rc;
+    REQUIRE(numel != nullptr, "null numel");
+    *numel = weights_numel(*d);
+    return DPT_OK;
+}
+
+int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** out) {
+    int rc = validate_desc(d);
+    if (rc) return rc;
+    REQUIRE(packed != nullptr && out != nullptr, "null packed/out");
+    const size_t bytes = (size_t)weights_numel(*d) * sizeof(float);
+    float* blob = nullptr;
+    if (hipMalloc(&blob, bytes) != hipSuccess) {
+        set_error(DPT_ENOMEM, "hipMalloc(%zu) for the weight blob failed", bytes);
+        return DPT_ENOMEM;
+    }
+    rc = check_hip(hipMemcpy(blob, packed, bytes, hipMemcpyDeviceToDevice), "weight blob copy");
+    if (rc) {
+        hipFree(blob);
+        return rc;
+    }
+    dpt_model* m = new dpt_model;
+    m->desc = *d;
+    m->blob = blob;
+    m->view = make_view(blob, *d);
+    *out = m;
+    return DPT_OK;
+}
+
+int dpt_model_free(dpt_model* m) {
+    if (!m) return DPT_OK;
+    int rc = check_hip(hipFree(m->blob), "hipFree weight blob");
+    delete m;
+    return rc;
+}
+
+int dpt_kvcache_numel(const dpt_model* m, int32_t N, int32_t max_pos, int64_t* numel) {
+    REQUIRE(m && numel, "null model/numel");
+    REQUIRE(N >= 1 && max_pos >= 1, "N=%d max_pos=%d", N, max_pos);
+    *numel = (int64_t)2 * m->desc.n_layer * N * (int64_t)max_pos * kE;
+    return DPT_OK;
+}
+
+int dpt_forward_window(const dpt_model* m, const float* query, const float* states, const float* actions,
+                       const float* next_states, const float* rewards, int32_t N, int32_t C, int32_t out_mode,
+                       float* out, float* workspace, void* stream) {
+    REQUIRE(m, "null model");
+    REQUIRE(N >= 1 && C >= 0, "N=%d C=%d", N, C);
+    REQUIRE(C + 1 <= m->desc.n_positions, "context length %d + query exceeds n_positions=%d", C,
+            m->desc.n_positions);
+    REQUIRE(out_mode == 0 || (out_mode == 1 && C >= 1), "out_mode=%d with C=%d", out_mode, C);
+    REQUIRE(query && out && workspace, "null query/out/workspace");
+    REQUIRE(C == 0 || (states && actions && next_states && rewards), "null context arrays with C=%d", C);
+    return launch_window_decode(m->view, workspace, N, C, query, states, actions, next_states, rewards, out_mode,
+                                out, S(stream));
+}
+
+int dpt_decode_step(const dpt_model* m, float* kv, int32_t N, int32_t max_pos, int32_t pos, const float* token,
+                    float* logits, void* stream) {
+    REQUIRE(m && kv && token && logits, "null pointer");
+    REQUIRE(N >= 1 && pos >= 0 && pos < max_pos, "N=%d pos=%d max_pos=%d", N, pos, max_pos);
+    REQUIRE(pos < m->desc.n_positions, "pos=%d >= n_positions=%d", pos, m->desc.n_positions);
+    return launch_decode_step(m->view, kv, N, max_pos, pos, token, logits, S(stream));
+}
+
+int dpt_select_action(const float* logits, int32_t N, int32_t A, int32_t sample, float temp,
+                      const double* uniforms, uint64_t seed, uint64_t counter, int64_t first_task,
+                      int32_t* action_out, void* stream) {
+    REQUIRE(logits && action_out, "null pointer");
+    REQUIRE(N >= 1 && A >= 1 && A <= kMaxA, "N=%d A=%d", N, A);
+    REQUIRE(temp > 0.f, "temp=%g", (double)temp);
+    return launch_select(logits, N, A, sample, temp, uniforms, seed, counter, first_task, action_out, S(stream));
+}
+
+int dpt_bandit_step(const double* means, int32_t N, int32_t A, const int32_t* action, int32_t type, double var,
+                    const double* noise, uint64_t seed, uint64_t counter, int64_t first_task, double* reward_out,
+                    double* arm_value_out, void* stream) {
+    REQUIRE(means && action && reward_out, "null pointer");
+    REQUIRE(N >= 1 && A >= 1, "N=%d A=%d", N, A);
+    if (type != DPT_BANDIT_GAUSSIAN && type != DPT_BANDIT_BERNOULLI) {
+        set_error(DPT_EUNSUPPORTED, "bandit type %d", type);
+        return DPT_EUNSUPPORTED;
+    }
+    return launch_bandit_step(means, N, A, action, type, var, noise, seed, counter, first_task, reward_out,
+                              arm_value_out, S(stream));
+}
+
+int dpt_darkroom_step(const int32_t* state, const int32_t* action, const int32_t* goal, const int32_t* perm,
+                      int32_t N, int32_t dim, int32_t* next_state, int32_t* reward, void* stream) {
+    REQUIRE(state && action && goal && next_state && reward, "null pointer");
+    REQUIRE(N >= 1 && dim >= 1, "N=%d dim=%d", N, dim);
+    return launch_darkroom_step(state, action, goal, perm, N, dim, next_state, reward, S(stream));
+}
+
+int dpt_darkroom_opt_action(const int32_t* state, const int32_t* goal, const int32_t* perm, int32_t N,
+                            int32_t* action_out, void* stream) {
+    REQUIRE(state && goal && action_out, "null pointer");
+    REQUIRE(N >= 1, "N=%d", N);
+    return launch_darkroom_opt(state, goal, perm, N, action_out, S(stream));
+}
+
+int dpt_draw(int32_t kind, uint64_t seed, uint64_t counter, int64_t first_task, int32_t N, uint32_t stream_id,
+             double* out, void* stream) {
+    REQUIRE(out && N >= 1 && (kind == 0 || kind == 1), "kind=%d N=%d", kind, N);
+    return launch_draw(kind, seed, counter, first_task, N, stream_id, out, S(stream));
+}
+
+int dpt_rollout_bandit(const dpt_model* m, const dpt_bandit_rollout_args* a, void* stream) {
+    REQUIRE(m && a, "null model/args");
+    REQUIRE(a->N >= 1 && a->H >= 1, "N=%d H=%d", a->N, a->H);
+    REQUIRE(a->A == m->desc.action_dim, "A=%d != model action_dim=%d", a->A, m->desc.action_dim);
+    REQUIRE(m->desc.state_dim == 1, "bandit rollout needs state_dim=1 (got %d)", m->desc.state_dim);
+    REQUIRE(a->H <= m->desc.n_positions, "H=%d exceeds n_positions=%d", a->H, m->desc.n_positions);
+    REQUIRE(a->means && a->kvcache && a->actions_out && a->rewards_out && a->arm_value_out, "null output");
+    if (a->type != DPT_BANDIT_GAUSSIAN && a->type != DPT_BANDIT_BERNOULLI) {
+        set_error(DPT_EUNSUPPORTED, "bandit type %d", a->type);
+        return DPT_EUNSUPPORTED;
+    }
+    return launch_rollout_bandit(m->view, *a, S(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,219 @@
+"""Device runtime of the MI355X DPT hot path: torch tensors in, libdpt_hip.so kernels out.
+
+PyTorch-ROCm is plumbing here (device memory, the current HIP stream); every
+computation below is a hand-written gfx950 kernel behind the C ABI in
+include/dpt_hip.h.  There is deliberately no CPU implementation: calling any
+of these without a GPU raises.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import (BANDIT_BERNOULLI, BANDIT_GAUSSIAN, STREAM_REWARD, STREAM_ROLLIN,  # noqa: F401
+                   STREAM_SELECT, EpisodeEndedError)
+
+E = 32
+
+
+def device():
+    """The device the hot path runs on (``cuda`` == HIP on ROCm)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("the DPT HIP path needs a ROCm GPU (torch.cuda.is_available() is False)")
+    _lib.load()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev(x, dtype, dev=None):
+    dev = dev or device()
+    if isinstance(x, torch.Tensor):
+        return x.to(device=dev, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=dev)
+
+
+def next_seed():
+    """64-bit Philox key drawn from numpy's global RNG (so ``np.random.seed`` governs
+    the run, as it does in the reference: eval.py:64-71, collect_data.py:352)."""
+    return int(np.random.randint(0, 2 ** 62, dtype=np.int64))
+
+
+# ----------------------------------------------------------------------------- weights
+
+def layer_param_names(i):
+    p = f"transformer.h.{i}."
+    return [p + n for n in ("ln_1.weight", "ln_1.bias", "attn.c_attn.weight", "attn.c_attn.bias",
+                            "attn.c_proj.weight", "attn.c_proj.bias", "ln_2.weight", "ln_2.bias",
+                            "mlp.c_fc.weight", "mlp.c_fc.bias", "mlp.c_proj.weight", "mlp.c_proj.bias")]
+
+
+def pack_weights(sd, n_layer):
+    """Flatten a reference ``Transformer.state_dict()`` into the dpt_hip.h blob order.
+
+    nn.Linear weights (embed_transition, pred_actions) are stored [out][in] by
+    torch and transposed here; GPT-2 Conv1D weights are already [in][out].
+    """
+    def t(k):
+        v = sd[k]
+        return v.detach().to("cpu", torch.float32) if isinstance(v, torch.Tensor) else torch.as_tensor(v, dtype=torch.float32)
+
+    parts = [t("embed_transition.weight").t(), t("embed_transition.bias"), t("transformer.wpe.weight")]
+    for i in range(n_layer):
+        parts += [t(k) for k in layer_param_names(i)]
+    parts += [t("transformer.ln_f.weight"), t("transformer.ln_f.bias"),
+              t("pred_actions.weight").t(), t("pred_actions.bias")]
+    return torch.cat([p.contiguous().reshape(-1) for p in parts])
+
+
+class DeviceModel:
+    """Owns one ``dpt_model`` handle (the packed fp32 weights on the GPU)."""
+
+    def __init__(self, state_dict, n_layer, state_dim, action_dim, n_positions, n_embd=E):
+        self.desc = _lib.ModelDesc(n_layer, n_embd, state_dim, action_dim, n_positions)
+        numel = ctypes.c_int64()
+        _lib.call("dpt_weights_numel", ctypes.byref(self.desc), ctypes.byref(numel))
+        blob = pack_weights(state_dict, n_layer)
+        if blob.numel() != numel.value:
+            raise ValueError(f"packed weights {blob.numel()} != expected {numel.value}")
+        dev = device()
+        blob_d = blob.to(dev)
+        h = ctypes.c_void_p()
+        _lib.call("dpt_model_create", ctypes.byref(self.desc), _p(blob_d), ctypes.byref(h))
+        torch.cuda.current_stream().synchronize()
+        self._h = h
+        self.n_layer, self.state_dim, self.action_dim = n_layer, state_dim, action_dim
+        self.n_positions = n_positions
+        self.F = 2 * state_dim + action_dim + 1
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().dpt_model_free(h)
+            except Exception:
+                pass
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def kv_numel(self, N, max_pos):
+        n = ctypes.c_int64()
+        _lib.call("dpt_kvcache_numel", self._h, int(N), int(max_pos), ctypes.byref(n))
+        return n.value
+
+    def forward_window(self, query, cs=None, ca=None, cn=None, cr=None, out_mode=0):
+        """Transformer.forward (models/net.py:41-60) on device. Returns (N,A) or (N,C,A)."""
+        dev = device()
+        q = _dev(query, torch.float32, dev)
+        N = q.shape[0]
+        C = 0 if cs is None else int(cs.shape[1])
+        if C:
+            cs_, ca_, cn_ = (_dev(x, torch.float32, dev) for x in (cs, ca, cn))
+            cr_ = _dev(cr, torch.float32, dev).reshape(N, C)
+        else:
+            cs_ = ca_ = cn_ = cr_ = None
+        out = torch.empty((N, self.action_dim) if out_mode == 0 else (N, C, self.action_dim),
+                          dtype=torch.float32, device=dev)
+        ws = torch.empty(self.kv_numel(N, C + 1), dtype=torch.float32, device=dev)
+        _lib.call("dpt_forward_window", self._h, _p(q), _p(cs_), _p(ca_), _p(cn_), _p(cr_), N, C,
+                  int(out_mode), _p(out), _p(ws), _stream())
+        return out
+
+    def decode_step(self, kv, max_pos, pos, token):
+        token = _dev(token, torch.float32)
+        N = token.shape[0]
+        logits = torch.empty((N, self.action_dim), dtype=torch.float32, device=token.device)
+        _lib.call("dpt_decode_step", self._h, _p(kv), N, int(max_pos), int(pos), _p(token), _p(logits),
+                  _stream())
+        return logits
+
+    def rollout_bandit(self, means, H, var, sample=True, bandit_type=BANDIT_GAUSSIAN, seed=0,
+                       first_task=0, uniforms=None, noise=None, want_logits=False):
+        """Fused online bandit rollout (evals/eval_bandit.py:56-103) on device.
+
+        Returns dict of device tensors: actions (N,H) int32, rewards (N,H) f64,
+        arm_value (N,H) f64 (= cum_means.T), logits (H,N,A) f32 if requested.
+        """
+        dev = device()
+        means_d = _dev(means, torch.float64, dev)
+        N, A = means_d.shape
+        H = int(H)
+        kv = torch.empty(self.kv_numel(N, H), dtype=torch.float32, device=dev)
+        out = dict(actions=torch.empty((N, H), dtype=torch.int32, device=dev),
+                   rewards=torch.empty((N, H), dtype=torch.float64, device=dev),
+                   arm_value=torch.empty((N, H), dtype=torch.float64, device=dev))
+        out["logits"] = (torch.empty((H, N, A), dtype=torch.float32, device=dev) if want_logits else None)
+        u_d = None if uniforms is None else _dev(uniforms, torch.float64, dev)
+        g_d = None if noise is None else _dev(noise, torch.float64, dev)
+        args = _lib.BanditRolloutArgs(
+            N, H, A, int(bandit_type), int(bool(sample)), 0, int(first_task), float(var), int(seed) & (2 ** 64 - 1),
+            _p(means_d).value, None if u_d is None else _p(u_d).value, None if g_d is None else _p(g_d).value,
+            _p(kv).value, _p(out["actions"]).value, _p(out["rewards"]).value, _p(out["arm_value"]).value,
+            None if out["logits"] is None else _p(out["logits"]).value)
+        _lib.call("dpt_rollout_bandit", self._h, ctypes.byref(args), _stream())
+        out["_keep"] = (kv, means_d, u_d, g_d)
+        return out
+
+
+# ----------------------------------------------------------------------------- element-wise ops
+
+def select_action(logits, sample, temp=1.0, uniforms=None, seed=0, counter=0, first_task=0):
+    logits = _dev(logits, torch.float32)
+    N, A = logits.shape
+    u = None if uniforms is None else _dev(uniforms, torch.float64, logits.device)
+    out = torch.empty(N, dtype=torch.int32, device=logits.device)
+    _lib.call("dpt_select_action", _p(logits), N, A, int(bool(sample)), float(temp), _p(u), int(seed),
+              int(counter), int(first_task), _p(out), _stream())
+    return out
+
+
+def bandit_step(means, action, var, bandit_type=BANDIT_GAUSSIAN, noise=None, seed=0, counter=0,
+                first_task=0):
+    means = _dev(means, torch.float64)
+    N, A = means.shape
+    a = _dev(action, torch.int32, means.device)
+    g = None if noise is None else _dev(noise, torch.float64, means.device)
+    r = torch.empty(N, dtype=torch.float64, device=means.device)
+    v = torch.empty(N, dtype=torch.float64, device=means.device)
+    _lib.call("dpt_bandit_step", _p(means), N, A, _p(a), int(bandit_type), float(var), _p(g), int(seed),
+              int(counter), int(first_task), _p(r), _p(v), _stream())
+    return r, v
+
+
+def darkroom_step(state, action, goal, perm=None, dim=10):
+    s = _dev(state, torch.int32)
+    N = s.shape[0]
+    a = _dev(action, torch.int32, s.device)
+    g = _dev(goal, torch.int32, s.device)
+    pm = None if perm is None else _dev(perm, torch.int32, s.device)
+    ns = torch.empty_like(s)
+    r = torch.empty(N, dtype=torch.int32, device=s.device)
+    _lib.call("dpt_darkroom_step", _p(s), _p(a), _p(g), _p(pm), N, int(dim), _p(ns), _p(r), _stream())
+    return ns, r
+
+
+def darkroom_opt_action(state, goal, perm=None):
+    s = _dev(state, torch.int32)
+    g = _dev(goal, torch.int32, s.device)
+    pm = None if perm is None else _dev(perm, torch.int32, s.device)
+    out = torch.empty(s.shape[0], dtype=torch.int32, device=s.device)
+    _lib.call("dpt_darkroom_opt_action", _p(s), _p(g), _p(pm), s.shape[0], _p(out), _stream())
+    return out
+
+
+def draw(kind, seed, counter, first_task, N, stream_id):
+    """The Philox draws the kernels use (kind 0 uniform, 1 normal) -> (N,) float64 device tensor."""
+    out = torch.empty(int(N), dtype=torch.float64, device=device())
+    _lib.call("dpt_draw", int(kind), int(seed), int(counter), int(first_task), int(N), int(stream_id),
+              _p(out), _stream())
+    return out

@@ -1,0 +1,148 @@
+"""DPT policy model — drop-in for the reference models/net.py:9-60 ``Transformer``.
+
+Same constructor config dict, same parameter names (so reference checkpoints
+load with ``load_state_dict`` unchanged), same ``forward(batch) -> logits``
+contract.  The GPT-2 stack is NOT transformers.GPT2Model: parameters live in a
+plain module tree with GPT-2's names, and ``forward`` runs the hand-written
+gfx950 kernels of libdpt_hip.so (dpt_forward_window).  ``n_head`` is accepted
+and ignored exactly as the reference ignores it (net.py:29 forces one head).
+"""
+import math
+import random
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+import dpt_hip
+
+# models/net.py:4 calls transformers.set_seed(0) at import time; keep that side
+# effect so scripts that rely on it (random init without a checkpoint) behave alike.
+random.seed(0)
+np.random.seed(0)
+torch.manual_seed(0)
+
+device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+VOCAB = 50257  # GPT2Config default; wte is unused with inputs_embeds but is part of the state_dict
+
+
+class Conv1D(nn.Module):
+    """GPT-2 Conv1D: y = x @ W + b with W stored [in][out] (transformers pytorch_utils.Conv1D)."""
+
+    def __init__(self, nf, nx):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(nx, nf))
+        self.bias = nn.Parameter(torch.zeros(nf))
+
+
+class _Attn(nn.Module):
+    def __init__(self, E):
+        super().__init__()
+        self.c_attn = Conv1D(3 * E, E)
+        self.c_proj = Conv1D(E, E)
+
+
+class _MLP(nn.Module):
+    def __init__(self, E):
+        super().__init__()
+        self.c_fc = Conv1D(4 * E, E)
+        self.c_proj = Conv1D(E, 4 * E)
+
+
+class _Block(nn.Module):
+    def __init__(self, E):
+        super().__init__()
+        self.ln_1 = nn.LayerNorm(E, eps=1e-5)
+        self.attn = _Attn(E)
+        self.ln_2 = nn.LayerNorm(E, eps=1e-5)
+        self.mlp = _MLP(E)
+
+
+class GPT2Stack(nn.Module):
+    """Parameter container with GPT2Model's names (wte, wpe, h.{i}.*, ln_f)."""
+
+    def __init__(self, n_positions, E, n_layer):
+        super().__init__()
+        self.wte = nn.Embedding(VOCAB, E)
+        self.wpe = nn.Embedding(n_positions, E)
+        self.h = nn.ModuleList([_Block(E) for _ in range(n_layer)])
+        self.ln_f = nn.LayerNorm(E, eps=1e-5)
+
+
+class Transformer(nn.Module):
+    """Transformer class (models/net.py:9-60)."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        self.test = config["test"]
+        self.horizon = self.config["horizon"]
+        self.n_embd = self.config["n_embd"]
+        self.n_layer = self.config["n_layer"]
+        self.n_head = self.config["n_head"]
+        self.state_dim = self.config["state_dim"]
+        self.action_dim = self.config["action_dim"]
+        self.dropout = self.config["dropout"]
+        self.n_positions = 4 * (1 + self.horizon)
+
+        self.transformer = GPT2Stack(self.n_positions, self.n_embd, self.n_layer)
+        self.embed_transition = nn.Linear(2 * self.state_dim + self.action_dim + 1, self.n_embd)
+        self.pred_actions = nn.Linear(self.n_embd, self.action_dim)
+        self._init_gpt2()
+        self._register_load_state_dict_pre_hook(self._drop_legacy_buffers)
+        self._dev_model = None
+        self._dev_sig = None
+
+    # GPT2PreTrainedModel._init_weights: N(0, 0.02) weights, zero biases, LN (1, 0),
+    # c_proj weights N(0, 0.02 / sqrt(2 * n_layer)).
+    def _init_gpt2(self):
+        std = 0.02
+        with torch.no_grad():
+            for mod in self.modules():
+                if isinstance(mod, (nn.Linear, Conv1D)):
+                    mod.weight.normal_(0.0, std)
+                    mod.bias.zero_()
+                elif isinstance(mod, nn.Embedding):
+                    mod.weight.normal_(0.0, std)
+                elif isinstance(mod, nn.LayerNorm):
+                    mod.weight.fill_(1.0)
+                    mod.bias.zero_()
+            for blk in self.transformer.h:
+                blk.attn.c_proj.weight.normal_(0.0, std / math.sqrt(2 * self.n_layer))
+                blk.mlp.c_proj.weight.normal_(0.0, std / math.sqrt(2 * self.n_layer))
+
+    @staticmethod
+    def _drop_legacy_buffers(state_dict, prefix, *args):
+        # transformers 4.5.1 (requirements.txt:1) saved the causal-mask buffers
+        # attn.bias / attn.masked_bias in GPT-2 checkpoints; they carry no weights.
+        for k in list(state_dict.keys()):
+            if k.startswith(prefix) and (k.endswith("attn.masked_bias") or k.endswith("attn.bias")):
+                del state_dict[k]
+
+    # ------------------------------------------------------------------ device weights
+    def device_model(self):
+        """The packed-weight handle on the GPU, rebuilt whenever a parameter changed."""
+        sig = tuple((id(p), p._version, p.data_ptr()) for p in self.parameters())
+        if self._dev_model is None or sig != self._dev_sig:
+            if self.n_embd != dpt_hip.E:
+                raise NotImplementedError(f"n_embd={self.n_embd}: only {dpt_hip.E} is built")
+            self._dev_model = dpt_hip.DeviceModel(self.state_dict(), self.n_layer, self.state_dim,
+                                                  self.action_dim, self.n_positions, self.n_embd)
+            self._dev_sig = sig
+        return self._dev_model
+
+    def forward(self, x):
+        """models/net.py:41-60: pack [query | context] -> embed -> GPT-2 -> head;
+        last position (test) or positions 1.. (train).  Inference only."""
+        dm = self.device_model()
+        query = x["query_states"]
+        cs = x.get("context_states")
+        C = 0 if cs is None else int(cs.shape[1])
+        if C == 0:
+            if not self.test:
+                return torch.zeros((query.shape[0], 0, self.action_dim), device=dpt_hip.device())
+            return dm.forward_window(query)
+        cr = x["context_rewards"]
+        return dm.forward_window(query, cs, x["context_actions"], x["context_next_states"],
+                                 cr.reshape(cr.shape[0], C), out_mode=0 if self.test else 1)

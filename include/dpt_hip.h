@@ -1,0 +1,193 @@
+/*
+ * dpt_hip.h — C ABI of libdpt_hip.so, the MI355X (gfx950) implementation of the
+ * DPT data-generation + in-context-evaluation hot path.
+ *
+ * Reference: titanium-47/decision-pretrained-transformer (pure Python).  The
+ * reference has no FFI; its "plugin API" is three duck-typed Python protocols
+ * (Env, Controller, model.forward).  Every entry point below names the reference
+ * interface it replaces (path:line relative to the reference root).  The Python
+ * shims in decision-pretrained-transformer_amd/ (envs/, ctrls/, evals/, models/)
+ * keep the reference names and call these through ctypes.
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer unless the name ends in _host.
+ *    The caller (torch) allocates every tensor; the library allocates only the
+ *    weight blob owned by an opaque dpt_model handle.
+ *  - All launches are asynchronous on the given stream (hipStream_t passed as
+ *    void* so this header needs no HIP include; NULL = default stream).
+ *  - Return 0 (DPT_OK) or a negative DPT_E* code; dpt_last_error() returns a
+ *    thread-local message for the last failing call on this thread.
+ *  - Layouts are C-contiguous, row-major.  fp64 for everything the reference
+ *    keeps in numpy float64 (means, rewards, arm values, uniforms, normals),
+ *    fp32 for the model (the reference converts contexts with .float()).
+ *  - Randomness: when an optional uniforms/normals pointer is NULL the library
+ *    draws from Philox4x32-10 keyed by `seed` with counter
+ *    (step, global task id, stream, 0); results therefore do not depend on how
+ *    tasks are sharded over GPUs.  Passing explicit draws reproduces a
+ *    reference run draw-for-draw (tests/golden).
+ */
+#ifndef DPT_HIP_H
+#define DPT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPT_ABI_VERSION 1
+
+/* error codes (mapped to the reference's Python exceptions by dpt_hip/_lib.py) */
+#define DPT_OK 0
+#define DPT_EINVAL (-1)          /* bad shape / argument        -> ValueError            */
+#define DPT_EEPISODE_ENDED (-2)  /* step past horizon           -> ValueError("Episode has already ended")
+                                    envs/bandit_env.py:67-68, envs/darkroom_env.py:58-59 */
+#define DPT_EHIP (-3)            /* HIP runtime error           -> RuntimeError          */
+#define DPT_ENOMEM (-4)          /* device allocation failed    -> MemoryError           */
+#define DPT_EUNSUPPORTED (-5)    /* configuration not built     -> NotImplementedError
+                                    (envs/bandit_env.py:16,63 unknown bandit type)      */
+
+/* bandit reward type, envs/bandit_env.py:57-63 / envs/gpu_bandit_env.py:57-62 */
+#define DPT_BANDIT_GAUSSIAN 0
+#define DPT_BANDIT_BERNOULLI 1
+
+/* Philox stream ids (counter word 2) */
+#define DPT_STREAM_SELECT 0
+#define DPT_STREAM_REWARD 1
+#define DPT_STREAM_ROLLIN 2
+
+int dpt_abi_version(void);
+const char* dpt_last_error(void);
+/* number of visible gfx950 devices (0 on a CPU-only host; never faults) */
+int dpt_device_count(int* count_out_host);
+
+/* ------------------------------------------------------------------ model
+ * Replaces models/net.py:9-60 `Transformer` (+ transformers.GPT2Model with
+ * n_head forced to 1, net.py:29).  Only n_embd == 32 (the reference default,
+ * common_args.py:31) is built; n_layer is free.
+ *
+ * Packed fp32 weight blob, in this order (all matrices stored [in][out]):
+ *   emb_w [F][E]  emb_b [E]                 F = 2*state_dim + action_dim + 1
+ *   wpe   [n_positions][E]                  n_positions = 4*(1+horizon) (net.py:26)
+ *   per layer l < n_layer:
+ *     ln1_g[E] ln1_b[E] attn_w[E][3E] attn_b[3E] proj_w[E][E] proj_b[E]
+ *     ln2_g[E] ln2_b[E] fc_w[E][4E] fc_b[4E] mp_w[4E][E] mp_b[E]
+ *   lnf_g[E] lnf_b[E]
+ *   head_w[E][A]  head_b[A]
+ * Conv1D weights are already [in][out]; nn.Linear weights (embed_transition,
+ * pred_actions) are transposed by the packer.
+ */
+typedef struct dpt_model dpt_model;
+
+typedef struct dpt_model_desc {
+    int32_t n_layer;
+    int32_t n_embd;      /* must be 32 */
+    int32_t state_dim;
+    int32_t action_dim;  /* 1..32 */
+    int32_t n_positions; /* rows of wpe */
+    int32_t reserved[3];
+} dpt_model_desc;
+
+/* number of floats in the packed blob for `desc` */
+int dpt_weights_numel(const dpt_model_desc* desc_host, int64_t* numel_out_host);
+/* copies `packed` (device, dpt_weights_numel floats) into a blob owned by the handle */
+int dpt_model_create(const dpt_model_desc* desc_host, const float* packed, dpt_model** out_host);
+int dpt_model_free(dpt_model* model);
+
+/* Full-window forward, replaces Transformer.forward (models/net.py:41-60)
+ * including the token packing (net.py:42-54):
+ *   token 0 = [query, 0_A, 0_sd, 0], token 1+j = [s_j, a_j, s'_j, r_j].
+ * query (N,sd); states/next_states (N,C,sd); actions (N,C,A); rewards (N,C).
+ * C may be 0 (the context pointers may then be NULL).  T = C+1 <= n_positions.
+ * out_mode 0: out (N,A) = preds[:, -1]  (test=True)
+ * out_mode 1: out (N,C,A) = preds[:, 1:] (test=False)                       */
+int dpt_forward_window(const dpt_model* model, const float* query, const float* states,
+                       const float* actions, const float* next_states, const float* rewards,
+                       int32_t N, int32_t C, int32_t out_mode, float* out, float* workspace,
+                       void* stream);
+/* `workspace` holds dpt_kvcache_numel(model, N, C + 1) floats: the window is
+ * evaluated causally, position by position, through a K/V cache (identical to
+ * the full causal recompute; each row attends to rows <= itself).            */
+
+/* ------------------------------------------------------------------ KV-cache decode
+ * Exact incremental form of the growing-window forward used by the bandit
+ * online loop (evals/eval_bandit.py:70-89): the query token is identical at
+ * every step, so positions 0..h-1 are unchanged between steps h-1 and h and
+ * their keys/values can be cached.  Cache layout [2][n_layer][N][max_pos][E].  */
+int dpt_kvcache_numel(const dpt_model* model, int32_t N, int32_t max_pos, int64_t* numel_out_host);
+/* one decode position for all N tasks: token (N,F) packed features of position
+ * `pos` (pos 0 is the query token), appends K/V at `pos`, logits (N,A) of it.  */
+int dpt_decode_step(const dpt_model* model, float* kvcache, int32_t N, int32_t max_pos,
+                    int32_t pos, const float* token, float* logits, void* stream);
+
+/* ------------------------------------------------------------------ action selection
+ * Replaces ctrls/ctrl_bandit.py:435-443 and ctrls/ctrl_darkroom.py:48-62:
+ * sample=1: p = softmax_fp32(logits/temp) (scipy.special.softmax semantics,
+ *   pairwise fp32 sum), i = #{k : cdf64_k <= u} with cdf64 = cumsum(fp64(p)) /
+ *   cdf[-1] — numpy legacy RandomState.choice(A, p=p) given its uniform u.
+ * sample=0: first argmax (np.argmax).
+ * uniforms (N) or NULL -> Philox(seed, (counter, first_task+i, DPT_STREAM_SELECT)). */
+int dpt_select_action(const float* logits, int32_t N, int32_t A, int32_t sample, float temp,
+                      const double* uniforms, uint64_t seed, uint64_t counter, int64_t first_task,
+                      int32_t* action_out, void* stream);
+
+/* ------------------------------------------------------------------ environments
+ * BanditEnvVec.step / GPUBanditEnv.transit (envs/bandit_env.py:56-74,
+ * envs/gpu_bandit_env.py:53-74):
+ *   gaussian : r = means[a] + (0.0 + var*g)   fp64, no contraction (bit-exact to numpy)
+ *   bernoulli: r = (u < means[a]) ? 1 : 0      (torch.bernoulli)
+ * arm_value_out (optional) = means[a]  (get_arm_value, envs/bandit_env.py:151-153).
+ * noise (N) or NULL -> Philox(seed, (counter, first_task+i, DPT_STREAM_REWARD)).   */
+int dpt_bandit_step(const double* means, int32_t N, int32_t A, const int32_t* action,
+                    int32_t type, double var, const double* noise, uint64_t seed,
+                    uint64_t counter, int64_t first_task, double* reward_out,
+                    double* arm_value_out, void* stream);
+
+/* DarkroomEnv(.Permuted).transit (envs/darkroom_env.py:37-55, :100-103): int32
+ * states (N,2), action index (N), goal (N,2), perm (N,5) or NULL.  Bit-exact.   */
+int dpt_darkroom_step(const int32_t* state, const int32_t* action, const int32_t* goal,
+                      const int32_t* perm, int32_t N, int32_t dim, int32_t* next_state,
+                      int32_t* reward, void* stream);
+/* DarkroomEnv.opt_action (envs/darkroom_env.py:69-82, permuted :105-111) */
+int dpt_darkroom_opt_action(const int32_t* state, const int32_t* goal, const int32_t* perm,
+                            int32_t N, int32_t* action_out, void* stream);
+
+/* Materialise the Philox draws the library would use: kind 0 = uniform [0,1),
+ * kind 1 = standard normal; out[i] for global task first_task+i at `counter`. */
+int dpt_draw(int32_t kind, uint64_t seed, uint64_t counter, int64_t first_task, int32_t N,
+             uint32_t stream_id, double* out, void* stream);
+
+/* ------------------------------------------------------------------ fused rollouts
+ * The whole online loop on device, one launch: replaces
+ * evals/eval_bandit.py:56-103 (and the identical evals/eval_linear_bandit.py:54-97)
+ * with BanditTransformerController (ctrls/ctrl_bandit.py:383-444) in the loop.
+ * For h in [0,H): decode position h (query token at h=0, else transition h-1),
+ * select a_h, step the env, append [1, onehot(a_h), 1, float(r_h)].           */
+typedef struct dpt_bandit_rollout_args {
+    int32_t N;            /* tasks on this device                         */
+    int32_t H;            /* horizon (steps = positions)                  */
+    int32_t A;            /* arms == model action_dim                     */
+    int32_t type;         /* DPT_BANDIT_*                                 */
+    int32_t sample;       /* 1: softmax sampling (eval online), 0: argmax */
+    int32_t reserved0;
+    int64_t first_task;   /* global id of task 0 (Philox counter)         */
+    double var;           /* reward noise std (the reference's `var`)     */
+    uint64_t seed;
+    const double* means;  /* (N, A)                                       */
+    const double* uniforms; /* (H, N) or NULL                             */
+    const double* noise;    /* (H, N) or NULL (normals, or bernoulli uniforms) */
+    float* kvcache;         /* dpt_kvcache_numel(model, N, H) floats        */
+    int32_t* actions_out;   /* (N, H)                                       */
+    double* rewards_out;    /* (N, H)                                       */
+    double* arm_value_out;  /* (N, H)  = cum_means.T                         */
+    float* logits_out;      /* (H, N, A) or NULL                             */
+} dpt_bandit_rollout_args;
+
+int dpt_rollout_bandit(const dpt_model* model, const dpt_bandit_rollout_args* args_host,
+                       void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DPT_HIP_H */

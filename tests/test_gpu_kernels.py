@@ -1,0 +1,213 @@
+"""Parity of the HIP kernels (through the C ABI) against reference golden vectors and the oracle.
+
+Bars: bit-exact for env transitions, indices, rewards and arm values; logits
+within 1e-5 * max(1, |x|) (BASELINE.json north_star); sampled actions exact
+wherever the uniform is further than 1e-5 from a cdf edge (flagged otherwise).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import dpt_oracle as O
+import philox_np
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-5
+
+
+def dh():
+    import dpt_hip
+    dpt_hip.device()
+    return dpt_hip
+
+
+def model_from_golden(name):
+    import dpt_hip
+    g = golden(f"forward_{name}.npz")
+    w = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w/")}
+    H, sd, A, L, E = (int(x) for x in g["cfg"])
+    m = dpt_hip.DeviceModel(w, L, sd, A, 4 * (1 + H))
+    W = O.split_weights({k: v.numpy() for k, v in w.items()}, L)
+    return g, m, W
+
+
+def assert_logits(got, ref):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(got - ref)
+    assert (err <= LOGIT_TOL * np.maximum(1.0, np.abs(ref))).all(), err.max()
+
+
+def test_bandit_step_bit_exact():
+    d = dh()
+    g = golden("bandit_transit.npz")
+    for var in (0.0, 0.3, 1.0):
+        r, v = d.bandit_step(g["means"], g["action"], var, noise=g[f"g_var{var}"])
+        assert np.array_equal(r.cpu().numpy().view(np.int64), g[f"reward_var{var}"].view(np.int64))
+        assert np.array_equal(v.cpu().numpy(), g["arm_value"])
+
+
+def test_bandit_step_bernoulli_and_philox():
+    d = dh()
+    rs = np.random.RandomState(0)
+    means = rs.uniform(0, 1, (1000, 5))
+    a = rs.randint(0, 5, 1000)
+    u = rs.uniform(size=1000)
+    r, _ = d.bandit_step(means, a, 0.0, d.BANDIT_BERNOULLI, noise=u)
+    assert np.array_equal(r.cpu().numpy(), O.bernoulli_reward(means, a, u))
+    # Philox path: rewards equal the oracle fed with the draws the library reports
+    seed, step = 1234567, 17
+    r, _ = d.bandit_step(means, a, 0.3, seed=seed, counter=step, first_task=100)
+    gdraw = d.draw(1, seed, step, 100, 1000, d.STREAM_REWARD).cpu().numpy()
+    assert np.array_equal(r.cpu().numpy(), O.bandit_reward(means, a, gdraw, 0.3))
+    np.testing.assert_allclose(gdraw, philox_np.normal(seed, step, np.arange(100, 1100), d.STREAM_REWARD),
+                               rtol=1e-12, atol=1e-12)
+    udraw = d.draw(0, seed, step, 5, 1000, d.STREAM_SELECT).cpu().numpy()
+    assert np.array_equal(udraw, philox_np.uniform(seed, step, np.arange(5, 1005), d.STREAM_SELECT))
+    assert 0.45 < udraw.mean() < 0.55 and abs(gdraw.mean()) < 0.1 and 0.9 < gdraw.std() < 1.1
+
+
+def test_darkroom_exhaustive():
+    d = dh()
+    g = golden("darkroom_transit.npz")
+    st = np.tile(g["states"], (100 * 5, 1))
+    goals = np.repeat(g["states"], 100, axis=0)
+    goals5 = np.repeat(goals[None], 5, 0).reshape(-1, 2)
+    acts = np.repeat(np.arange(5), 100 * 100)
+    # order (a, goal, state)
+    ns, r = d.darkroom_step(st, acts, goals5)
+    ref_ns = g["next_state"].transpose(1, 0, 2, 3).reshape(-1, 2)
+    ref_r = g["reward"].transpose(1, 0, 2).reshape(-1)
+    assert np.array_equal(ns.cpu().numpy(), ref_ns)
+    assert np.array_equal(r.cpu().numpy(), ref_r)
+    opt = d.darkroom_opt_action(np.tile(g["states"], (100, 1)), goals)
+    assert np.array_equal(opt.cpu().numpy(), g["opt_action"].reshape(-1))
+    # permuted: goal fixed at (9, 9)
+    perms = g["perms"].astype(np.int32)
+    st = np.tile(g["states"], (120 * 5, 1))
+    pidx = np.repeat(np.tile(np.arange(120), 5), 100)
+    acts = np.repeat(np.arange(5), 120 * 100)
+    goal = np.full((len(st), 2), 9)
+    ns, r = d.darkroom_step(st, acts, goal, perm=perms[pidx])
+    assert np.array_equal(ns.cpu().numpy(), g["perm_next_state"].transpose(1, 0, 2, 3).reshape(-1, 2))
+    assert np.array_equal(r.cpu().numpy(), g["perm_reward"].transpose(1, 0, 2).reshape(-1))
+    st1 = np.tile(g["states"], (120, 1))
+    opt = d.darkroom_opt_action(st1, np.full((len(st1), 2), 9), perm=perms[np.repeat(np.arange(120), 100)])
+    assert np.array_equal(opt.cpu().numpy(), g["perm_opt_action"].reshape(-1))
+
+
+def test_select_action_matches_reference():
+    d = dh()
+    g = golden("select.npz")
+    for A in (5, 20):
+        lg, u = g[f"A{A}/logits"], g[f"A{A}/u"]
+        got = d.select_action(lg, True, uniforms=u).cpu().numpy()
+        margin = O.boundary_margin(O.softmax_f32(lg), u)
+        ok = margin > 1e-5
+        assert np.array_equal(got[ok], g[f"A{A}/sampled"][ok]), np.nonzero(got != g[f"A{A}/sampled"])
+        assert np.array_equal(d.select_action(lg, False).cpu().numpy(), g[f"A{A}/greedy"])
+    # temperature path (ctrl_darkroom.py:51 divides by temp)
+    lg = g["A5/logits"]
+    u = g["A5/u"]
+    got = d.select_action(lg, True, temp=0.5, uniforms=u).cpu().numpy()
+    ref = O.select_actions(lg, u, True, temp=0.5)
+    ok = O.boundary_margin(O.softmax_f32(lg, 0.5), u) > 1e-5
+    assert np.array_equal(got[ok], ref[ok])
+
+
+@pytest.mark.parametrize("name", ["bandit5", "darkroom", "linear20"])
+def test_forward_window_logits(name):
+    g, m, W = model_from_golden(name)
+    Ts = sorted({int(k.split("/")[0][1:]) for k in g if k.startswith("T")})
+    for T in Ts:
+        q, cs, ca, cn, cr = (g[f"T{T}/{k}"] for k in ("query", "cs", "ca", "cn", "cr"))
+        C = T - 1
+        args = (q,) if C == 0 else (q, cs, ca, cn, cr)
+        out = m.forward_window(*args).cpu().numpy()
+        assert_logits(out, g[f"T{T}/logits"])
+        if C >= 1:
+            allp = m.forward_window(q, cs, ca, cn, cr, out_mode=1).cpu().numpy()
+            assert_logits(allp, g[f"T{T}/preds_train"])
+
+
+def test_decode_steps_equal_window():
+    import dpt_hip
+    g, m, W = model_from_golden("bandit5")
+    q, cs, ca, cn, cr = (g[f"T101/{k}"] for k in ("query", "cs", "ca", "cn", "cr"))
+    N, C = cs.shape[:2]
+    seq = O.pack_tokens(q, cs, ca, cn, cr, 5, 1).astype(np.float32)
+    kv = torch.empty(m.kv_numel(N, C + 1), dtype=torch.float32, device=dpt_hip.device())
+    for p in range(C + 1):
+        lg = m.decode_step(kv, C + 1, p, seq[:, p]).cpu().numpy()
+    win = m.forward_window(q, cs, ca, cn, cr).cpu().numpy()
+    assert np.array_equal(lg, win)
+    assert_logits(lg, g["T101/logits"])
+
+
+@pytest.mark.parametrize("tag", ["sample", "greedy", "var0"])
+def test_rollout_bandit_matches_reference(tag):
+    r = golden(f"rollout_bandit_{tag}.npz")
+    _, m, W = model_from_golden("bandit5")
+    n, H, A, sample = (int(x) for x in r["cfg"])
+    out = m.rollout_bandit(r["means"], H, float(r["var"]), bool(sample), uniforms=r["u"] if sample else None,
+                           noise=r["g"], want_logits=True)
+    assert_logits(out["logits"].cpu().numpy(), r["logits"])
+    assert np.array_equal(out["actions"].cpu().numpy(), r["ctx_actions"].argmax(-1))
+    assert np.array_equal(out["rewards"].cpu().numpy(), r["ctx_rewards"])
+    assert np.array_equal(out["arm_value"].cpu().numpy().T, r["cum_means"])
+
+
+def test_rollout_linear_matches_reference():
+    r = golden("rollout_linear_sample.npz")
+    _, m, W = model_from_golden("linear20")
+    n, H, A, sample = (int(x) for x in r["cfg"])
+    out = m.rollout_bandit(r["means"], H, float(r["var"]), True, uniforms=r["u"], noise=r["g"],
+                           want_logits=True)
+    assert_logits(out["logits"].cpu().numpy(), r["logits"])
+    assert np.array_equal(out["arm_value"].cpu().numpy().T, r["cum_means"])
+
+
+def test_rollout_philox_vs_oracle_and_sharding():
+    """Philox draws: the device rollout equals the oracle fed the same draws, and
+    splitting the tasks over 'ranks' (first_task offsets) changes nothing."""
+    d = dh()
+    _, m, W = model_from_golden("bandit5")
+    rs = np.random.RandomState(5)
+    N, H, seed = 24, 20, 987654321
+    means = rs.uniform(0, 1, (N, 5))
+    full = m.rollout_bandit(means, H, 0.3, True, seed=seed)
+    u = np.stack([philox_np.uniform(seed, h, np.arange(N), d.STREAM_SELECT) for h in range(H)])
+    g = np.stack([d.draw(1, seed, h, 0, N, d.STREAM_REWARD).cpu().numpy() for h in range(H)])
+    ref = O.bandit_online_rollout(W, means, H, 0.3, u, g, True)
+    acts = full["actions"].cpu().numpy()
+    assert np.array_equal(acts, ref["actions"])
+    assert np.array_equal(full["arm_value"].cpu().numpy().T, ref["cum_means"])
+    a = m.rollout_bandit(means[:10], H, 0.3, True, seed=seed, first_task=0)
+    b = m.rollout_bandit(means[10:], H, 0.3, True, seed=seed, first_task=10)
+    assert np.array_equal(np.concatenate([a["actions"].cpu().numpy(), b["actions"].cpu().numpy()]), acts)
+    assert np.array_equal(np.concatenate([a["rewards"].cpu().numpy(), b["rewards"].cpu().numpy()]),
+                          full["rewards"].cpu().numpy())
+
+
+def test_rollout_large_properties():
+    """Full-size invariants at N=4096 (config 2 width) on a shorter horizon:
+    determinism, arm_value == means[action], rewards == means[a] + var*g."""
+    d = dh()
+    _, m, _ = model_from_golden("bandit5")
+    rs = np.random.RandomState(1)
+    N, H = 4096, 48
+    means = rs.uniform(0, 1, (N, 5))
+    o1 = m.rollout_bandit(means, H, 0.3, True, seed=42)
+    o2 = m.rollout_bandit(means, H, 0.3, True, seed=42)
+    a = o1["actions"].cpu().numpy()
+    assert np.array_equal(a, o2["actions"].cpu().numpy())
+    assert a.min() >= 0 and a.max() < 5
+    av = o1["arm_value"].cpu().numpy()
+    assert np.array_equal(av, means[np.arange(N)[:, None], a])
+    g = np.stack([d.draw(1, 42, h, 0, N, d.STREAM_REWARD).cpu().numpy() for h in range(H)], 1)
+    assert np.array_equal(o1["rewards"].cpu().numpy(), av + (0.0 + 0.3 * g))
+    # partial tile (N not a multiple of 16) behaves like the full run on its prefix
+    o3 = m.rollout_bandit(means[:1000], H, 0.3, True, seed=42)
+    assert np.array_equal(o3["actions"].cpu().numpy(), a[:1000])
