@@ -59,13 +59,13 @@ def cpu_baseline(sd, means, H, var, n_layer, A):
     blob = dpt_hip.pack_weights(sd, n_layer).numpy()
     npos = 4 * (1 + H)
     rs = np.random.RandomState(7)
-    n_rec = 16
+    n_rec = 128  # ~10-20 s of CPU work on a 16-thread share
     u = rs.uniform(size=(H, n_rec))
     g = rs.normal(size=(H, n_rec))
     t0 = time.perf_counter()
     c_oracle.bandit_rollout(blob, n_layer, A, npos, means[:n_rec], H, var, u, g, True, True, threads)
     t_rec = time.perf_counter() - t0
-    n_kv = 256
+    n_kv = 2048
     u = rs.uniform(size=(H, n_kv))
     g = rs.normal(size=(H, n_kv))
     t0 = time.perf_counter()
