@@ -43,6 +43,12 @@ int launch_darkroom_opt(const int32_t*, const int32_t*, const int32_t*, int, int
 int launch_select(const float*, int, int, int, float, const double*, uint64_t, uint64_t, int64_t, int32_t*,
                   hipStream_t);
 int launch_draw(int, uint64_t, uint64_t, int64_t, int, uint32_t, double*, hipStream_t);
+int launch_rollin_bandit(const double*, const double*, int, int, int, int, double, const double*, const double*,
+                         uint64_t, int64_t, int32_t*, double*, hipStream_t);
+int launch_rollin_darkroom(const int32_t*, const int32_t*, int, int, int, int, const int32_t*, const int32_t*,
+                           uint64_t, int64_t, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*,
+                           hipStream_t);
+int launch_rollout_policy(const dpt_policy_rollout_args&, hipStream_t);
 
 }  // namespace dpt
 
@@ -112,7 +118,7 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
     }
     rc = check_hip(hipMemcpy(blob, packed, bytes, hipMemcpyDeviceToDevice), "weight blob copy");
     if (rc) {
-        hipFree(blob);
+        (void)hipFree(blob);
         return rc;
     }
     dpt_model* m = new dpt_model;
@@ -173,7 +179,8 @@ int dpt_bandit_step(const double* means, int32_t N, int32_t A, const int32_t* ac
                     double* arm_value_out, void* stream) {
     REQUIRE(means && action && reward_out, "null pointer");
     REQUIRE(N >= 1 && A >= 1, "N=%d A=%d", N, A);
-    if (type != DPT_BANDIT_GAUSSIAN && type != DPT_BANDIT_BERNOULLI) {
+    const int base = type & ~DPT_BANDIT_F32;
+    if (base != DPT_BANDIT_GAUSSIAN && base != DPT_BANDIT_BERNOULLI) {
         set_error(DPT_EUNSUPPORTED, "bandit type %d", type);
         return DPT_EUNSUPPORTED;
     }
@@ -199,6 +206,58 @@ int dpt_draw(int32_t kind, uint64_t seed, uint64_t counter, int64_t first_task, 
              double* out, void* stream) {
     REQUIRE(out && N >= 1 && (kind == 0 || kind == 1), "kind=%d N=%d", kind, N);
     return launch_draw(kind, seed, counter, first_task, N, stream_id, out, S(stream));
+}
+
+int dpt_rollin_bandit(const double* means, const double* probs, int32_t N, int32_t A, int32_t H, int32_t type,
+                      double var, const double* uniforms, const double* noise, uint64_t seed, int64_t first_task,
+                      int32_t* actions_out, double* rewards_out, void* stream) {
+    REQUIRE(means && probs && actions_out && rewards_out, "null pointer");
+    REQUIRE(N >= 1 && A >= 1 && H >= 1, "N=%d A=%d H=%d", N, A, H);
+    if (type != DPT_BANDIT_GAUSSIAN && type != DPT_BANDIT_BERNOULLI) {
+        set_error(DPT_EUNSUPPORTED, "bandit type %d", type);
+        return DPT_EUNSUPPORTED;
+    }
+    return launch_rollin_bandit(means, probs, N, A, H, type, var, uniforms, noise, seed, first_task, actions_out,
+                                rewards_out, S(stream));
+}
+
+int dpt_rollin_darkroom(const int32_t* goal, const int32_t* perm, int32_t N, int32_t H, int32_t dim, int32_t mode,
+                        const int32_t* states_in, const int32_t* actions_in, uint64_t seed, int64_t first_task,
+                        int32_t* states_out, int32_t* actions_out, int32_t* next_states_out, int32_t* rewards_out,
+                        int32_t* query_out, int32_t* opt_action_out, void* stream) {
+    REQUIRE(goal && states_out && actions_out && next_states_out && rewards_out, "null pointer");
+    REQUIRE(N >= 1 && H >= 1 && dim >= 1, "N=%d H=%d dim=%d", N, H, dim);
+    if (mode != 0 && mode != 1) {
+        set_error(DPT_EUNSUPPORTED, "rollin mode %d (0 uniform, 1 expert)", mode);
+        return DPT_EUNSUPPORTED;
+    }
+    REQUIRE((states_in == nullptr) == (actions_in == nullptr), "inject states and actions together");
+    REQUIRE(mode == 0 || states_in == nullptr, "injected draws only in uniform mode");
+    return launch_rollin_darkroom(goal, perm, N, H, dim, mode, states_in, actions_in, seed, first_task, states_out,
+                                  actions_out, next_states_out, rewards_out, query_out, opt_action_out, S(stream));
+}
+
+int dpt_policy_workspace_numel(int32_t N, int32_t A, int32_t H, int64_t* numel) {
+    REQUIRE(numel && N >= 1 && A >= 1 && H >= 1, "N=%d A=%d H=%d", N, A, H);
+    *numel = (int64_t)A * H * N;
+    return DPT_OK;
+}
+
+int dpt_rollout_policy(const dpt_policy_rollout_args* a, void* stream) {
+    REQUIRE(a, "null args");
+    REQUIRE(a->N >= 1 && a->H >= 1 && a->A >= 1 && a->A <= kMaxA, "N=%d H=%d A=%d", a->N, a->H, a->A);
+    REQUIRE(a->C >= 0 && a->C + a->H <= 2048, "C+H=%d > 2048 (pairwise-sum depth)", a->C + a->H);
+    REQUIRE(a->C == 0 || (a->ctx_actions && a->ctx_rewards), "null prefix context with C=%d", a->C);
+    REQUIRE(a->means && a->actions_out && a->rewards_out && a->arm_value_out, "null pointer");
+    REQUIRE(a->policy >= DPT_POLICY_OPT && a->policy <= DPT_POLICY_LINUCB, "policy=%d", a->policy);
+    REQUIRE(a->policy == DPT_POLICY_OPT || a->policy == DPT_POLICY_LINUCB || a->workspace,
+            "policy %d needs the per-arm workspace", a->policy);
+    REQUIRE(a->policy != DPT_POLICY_LINUCB || (a->arms && a->lin_d >= 1 && a->lin_d <= 2), "LinUCB needs arms, d<=2");
+    if (a->type != DPT_BANDIT_GAUSSIAN && a->type != DPT_BANDIT_BERNOULLI) {
+        set_error(DPT_EUNSUPPORTED, "bandit type %d", a->type);
+        return DPT_EUNSUPPORTED;
+    }
+    return launch_rollout_policy(*a, S(stream));
 }
 
 int dpt_rollout_bandit(const dpt_model* m, const dpt_bandit_rollout_args* a, void* stream) {

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (BANDIT_BERNOULLI, BANDIT_GAUSSIAN, STREAM_REWARD, STREAM_ROLLIN,  # noqa: F401
+from ._lib import (BANDIT_BERNOULLI, BANDIT_F32, BANDIT_GAUSSIAN, STREAM_REWARD, STREAM_ROLLIN,  # noqa: F401
                    STREAM_SELECT, EpisodeEndedError)
 
 E = 32
@@ -216,4 +216,84 @@ def draw(kind, seed, counter, first_task, N, stream_id):
     out = torch.empty(int(N), dtype=torch.float64, device=device())
     _lib.call("dpt_draw", int(kind), int(seed), int(counter), int(first_task), int(N), int(stream_id),
               _p(out), _stream())
+    return out
+
+
+# ----------------------------------------------------------------------------- data generation
+
+def rollin_bandit(means, probs, H, var, bandit_type=BANDIT_GAUSSIAN, uniforms=None, noise=None, seed=0,
+                  first_task=0):
+    """collect_data.py:23-53 for all tasks at once -> (actions (N,H) int32, rewards (N,H) f64) on device."""
+    means = _dev(means, torch.float64)
+    N, A = means.shape
+    probs = _dev(probs, torch.float64, means.device)
+    u = None if uniforms is None else _dev(uniforms, torch.float64, means.device)
+    g = None if noise is None else _dev(noise, torch.float64, means.device)
+    acts = torch.empty((N, int(H)), dtype=torch.int32, device=means.device)
+    rews = torch.empty((N, int(H)), dtype=torch.float64, device=means.device)
+    _lib.call("dpt_rollin_bandit", _p(means), _p(probs), N, A, int(H), int(bandit_type), float(var), _p(u), _p(g),
+              int(seed), int(first_task), _p(acts), _p(rews), _stream())
+    return acts, rews
+
+
+def rollin_darkroom(goals, H, dim=10, perm=None, mode=0, states=None, actions=None, seed=0, first_task=0):
+    """collect_data.py:83-111 (+ query / expert label, :199-201) for all tasks at once (device tensors)."""
+    goals = _dev(goals, torch.int32)
+    N = goals.shape[0]
+    dev = goals.device
+    pm = None if perm is None else _dev(perm, torch.int32, dev)
+    si = None if states is None else _dev(states, torch.int32, dev)
+    ai = None if actions is None else _dev(actions, torch.int32, dev)
+    out = dict(states=torch.empty((N, int(H), 2), dtype=torch.int32, device=dev),
+               actions=torch.empty((N, int(H)), dtype=torch.int32, device=dev),
+               next_states=torch.empty((N, int(H), 2), dtype=torch.int32, device=dev),
+               rewards=torch.empty((N, int(H)), dtype=torch.int32, device=dev),
+               query=torch.empty((N, 2), dtype=torch.int32, device=dev),
+               opt_action=torch.empty(N, dtype=torch.int32, device=dev))
+    _lib.call("dpt_rollin_darkroom", _p(goals), _p(pm), N, int(H), int(dim), int(mode), _p(si), _p(ai), int(seed),
+              int(first_task), _p(out["states"]), _p(out["actions"]), _p(out["next_states"]), _p(out["rewards"]),
+              _p(out["query"]), _p(out["opt_action"]), _stream())
+    return out
+
+
+# ----------------------------------------------------------------------------- classical baselines
+
+from ._lib import (POLICY_EMP, POLICY_LCB, POLICY_LINUCB, POLICY_OPT, POLICY_THOMPSON,  # noqa: E402,F401
+                   POLICY_UCB)
+
+
+def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=True, sample=True, c=1.0,
+                   ts_std=0.1, ts_prior_mean=0.5, ts_prior_var=1 / 12.0, arms=None, seed=0, first_task=0,
+                   noise=None, policy_noise=None, ctx_actions=None, ctx_rewards=None):
+    """Fused classical-policy rollout (dpt_rollout_policy); optional prefix context (N, C)."""
+    dev = device()
+    means_d = _dev(means, torch.float64, dev)
+    N, A = means_d.shape
+    H = int(H)
+    C = 0 if ctx_actions is None else int(np.asarray(ctx_actions).shape[1]) if not isinstance(
+        ctx_actions, torch.Tensor) else int(ctx_actions.shape[1])
+    keep = [means_d]
+
+    def opt(x, dt):
+        if x is None:
+            return None
+        t = _dev(x, dt, dev)
+        keep.append(t)
+        return _p(t).value
+
+    n = ctypes.c_int64()
+    _lib.call("dpt_policy_workspace_numel", N, A, C + H, ctypes.byref(n))
+    ws = torch.empty(n.value, dtype=torch.float64, device=dev)
+    out = dict(actions=torch.empty((N, H), dtype=torch.int32, device=dev),
+               rewards=torch.empty((N, H), dtype=torch.float64, device=dev),
+               arm_value=torch.empty((N, H), dtype=torch.float64, device=dev))
+    d = 0 if arms is None else int(np.asarray(arms).shape[1])
+    args = _lib.PolicyRolloutArgs(
+        N, H, A, int(policy), int(bool(online)), int(bandit_type), int(bool(sample)), d, int(first_task), float(var),
+        float(c), float(ts_std), float(ts_prior_mean), float(ts_prior_var), int(seed) & (2 ** 64 - 1),
+        _p(means_d).value, opt(arms, torch.float64), opt(noise, torch.float64), opt(policy_noise, torch.float64),
+        _p(ws).value, _p(out["actions"]).value, _p(out["rewards"]).value, _p(out["arm_value"]).value, C, 0,
+        opt(ctx_actions, torch.int32), opt(ctx_rewards, torch.float64))
+    _lib.call("dpt_rollout_policy", ctypes.byref(args), _stream())
+    out["_keep"] = (keep, ws)
     return out

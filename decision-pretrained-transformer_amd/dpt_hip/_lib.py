@@ -23,6 +23,7 @@ DPT_EUNSUPPORTED = -5
 
 BANDIT_GAUSSIAN = 0
 BANDIT_BERNOULLI = 1
+BANDIT_F32 = 16
 STREAM_SELECT = 0
 STREAM_REWARD = 1
 STREAM_ROLLIN = 2
@@ -70,6 +71,10 @@ SIGNATURES = {
     "dpt_darkroom_opt_action": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p]),
     "dpt_draw": (_i32, [_i32, _u64, _u64, _i64, _i32, _u32, _c_void_p, _c_void_p]),
     "dpt_rollout_bandit": (_i32, [_c_void_p, ctypes.POINTER(BanditRolloutArgs), _c_void_p]),
+    "dpt_rollin_bandit": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _f64, _c_void_p, _c_void_p, _u64,
+                                 _i64, _c_void_p, _c_void_p, _c_void_p]),
+    "dpt_rollin_darkroom": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p, _u64, _i64,
+                                   _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
 }
 
 _lock = threading.Lock()
@@ -119,3 +124,22 @@ def check(rc):
 
 def call(name, *args):
     check(getattr(load(), name)(*args))
+
+
+POLICY_OPT, POLICY_EMP, POLICY_UCB, POLICY_THOMPSON, POLICY_LCB, POLICY_LINUCB = range(6)
+
+
+class PolicyRolloutArgs(ctypes.Structure):
+    _fields_ = [("N", _i32), ("H", _i32), ("A", _i32), ("policy", _i32), ("online", _i32), ("type", _i32),
+                ("sample", _i32), ("lin_d", _i32), ("first_task", _i64), ("var", _f64), ("c", _f64),
+                ("ts_std", _f64), ("ts_prior_mean", _f64), ("ts_prior_var", _f64), ("seed", _u64),
+                ("means", _c_void_p), ("arms", _c_void_p), ("noise", _c_void_p), ("policy_noise", _c_void_p),
+                ("workspace", _c_void_p), ("actions_out", _c_void_p), ("rewards_out", _c_void_p),
+                ("arm_value_out", _c_void_p), ("C", _i32), ("reserved0", _i32), ("ctx_actions", _c_void_p),
+                ("ctx_rewards", _c_void_p)]
+
+
+SIGNATURES.update({
+    "dpt_policy_workspace_numel": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_i64)]),
+    "dpt_rollout_policy": (_i32, [ctypes.POINTER(PolicyRolloutArgs), _c_void_p]),
+})

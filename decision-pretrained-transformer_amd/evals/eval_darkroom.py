@@ -1,0 +1,157 @@
+"""DarkRoom evaluation — drop-in for the reference evals/eval_darkroom.py.
+
+``deploy_online_vec`` (evals/eval_darkroom.py:20-84): with the DPT controller
+over this package's ``Transformer`` and a ``DarkroomEnvVec`` the loop never
+leaves the device — per step one window forward (gfx950 kernel) over the fixed
+in-context episodes with the current state as query, device sampling, the
+integer grid step kernel, and an on-device append into the episode buffers;
+returns are summed on device and copied once at the end.  Other controllers
+run the reference's episode loop (envs step on the device).
+"""
+import numpy as np
+import torch
+
+import dpt_hip
+from ctrls.ctrl_darkroom import DarkroomOptPolicy, DarkroomTransformerController
+from envs.darkroom_env import DarkroomEnv, DarkroomEnvPermuted, DarkroomEnvVec
+from utils import convert_to_tensor
+
+device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+
+def _device_ok(vec_env, controller):
+    from models.net import Transformer
+    return (isinstance(controller, DarkroomTransformerController) and isinstance(vec_env, DarkroomEnvVec)
+            and isinstance(controller.model, Transformer) and controller.batch_size == vec_env.num_envs)
+
+
+def _episode_device(dm, ctrl, vec_env, ctx, horizon):
+    """One DarkroomEnvVec.deploy_eval episode on device: returns (states, actions, next, rewards)."""
+    dev = dpt_hip.device()
+    N = vec_env.num_envs
+    state = torch.zeros((N, 2), dtype=torch.int32, device=dev)   # DarkroomEnv.reset -> (0, 0)
+    es = torch.empty((N, horizon, 2), dtype=torch.int32, device=dev)
+    ea = torch.empty((N, horizon), dtype=torch.int64, device=dev)
+    er = torch.empty((N, horizon), dtype=torch.int32, device=dev)
+    goals, perms, dim = vec_env.goals_device, vec_env.perms_device, vec_env.dim
+    for t in range(horizon):
+        logits = dm.forward_window(state.float(), *ctx)
+        a = ctrl.select(logits)
+        es[:, t] = state
+        ea[:, t] = a
+        state, r = dpt_hip.darkroom_step(state, a, goals, perms, dim)
+        er[:, t] = r
+    ns = torch.cat([es[:, 1:], state[:, None]], dim=1)
+    return es, ea, ns, er
+
+
+def deploy_online_vec(vec_env, controller, Heps, H, horizon):
+    assert H % horizon == 0
+    ctx_rollouts = H // horizon
+    num_envs = vec_env.num_envs
+    dev = dpt_hip.device()
+    sd, ad = vec_env.state_dim, vec_env.action_dim
+    cs = torch.zeros((num_envs, ctx_rollouts, horizon, sd), device=dev)
+    ca = torch.zeros((num_envs, ctx_rollouts, horizon, ad), device=dev)
+    cn = torch.zeros((num_envs, ctx_rollouts, horizon, sd), device=dev)
+    cr = torch.zeros((num_envs, ctx_rollouts, horizon, 1), device=dev)
+    fast = _device_ok(vec_env, controller)
+    dm = controller.model.device_model() if fast else None
+    cum_means = []
+    for ep in range(Heps):
+        if ep < ctx_rollouts:
+            ctx = [x[:, :ep].reshape(num_envs, -1, x.shape[-1]) for x in (cs, ca, cn, cr)]
+        else:  # the last ctx_rollouts episodes (shift-append, eval_darkroom.py:75-82)
+            ctx = [x.reshape(num_envs, -1, x.shape[-1]) for x in (cs, ca, cn, cr)]
+        if fast:
+            c = () if ctx[0].shape[1] == 0 else (ctx[0], ctx[1], ctx[2], ctx[3][..., 0])
+            es, ea, ens, er = _episode_device(dm, controller, vec_env, c, horizon)
+            new = (es.float(), torch.nn.functional.one_hot(ea, ad).float(), ens.float(), er.float()[..., None])
+            cum_means.append(er.sum(-1))
+        else:
+            batch = {"context_states": ctx[0], "context_actions": ctx[1], "context_next_states": ctx[2],
+                     "context_rewards": ctx[3]}
+            controller.set_batch(batch)
+            s, a, n, r = vec_env.deploy_eval(controller)
+            cum_means.append(torch.as_tensor(np.sum(r, axis=-1), device=dev))
+            new = (convert_to_tensor(s), convert_to_tensor(a), convert_to_tensor(n), convert_to_tensor(r[:, :, None]))
+        if ep < ctx_rollouts:
+            for buf, v in zip((cs, ca, cn, cr), new):
+                buf[:, ep] = v
+        else:
+            cs, ca, cn, cr = (torch.cat((buf[:, 1:], v[:, None]), dim=1) for buf, v in zip((cs, ca, cn, cr), new))
+    return torch.stack(cum_means, dim=1).cpu().numpy()
+
+
+def online(eval_trajs, model, Heps, H, n_eval, dim, horizon, permuted=False):
+    """evals/eval_darkroom.py:87-121."""
+    import matplotlib.pyplot as plt
+    import scipy.stats
+    assert H % horizon == 0
+    envs = []
+    for i in range(n_eval):
+        traj = eval_trajs[i]
+        envs.append(DarkroomEnvPermuted(dim, traj["perm_index"], horizon) if permuted
+                    else DarkroomEnv(dim, traj["goal"], horizon))
+    lnr = DarkroomTransformerController(model, batch_size=n_eval, sample=True)
+    vec_env = DarkroomEnvVec(envs)
+    all_means_lnr = np.array(deploy_online_vec(vec_env, lnr, Heps, H, horizon))
+    means_lnr = np.mean(all_means_lnr, axis=0)
+    sems_lnr = scipy.stats.sem(all_means_lnr, axis=0)
+    for i in range(n_eval):
+        plt.plot(all_means_lnr[i], color="blue", alpha=0.2)
+    plt.plot(means_lnr, label="Learner")
+    plt.fill_between(np.arange(Heps), means_lnr - sems_lnr, means_lnr + sems_lnr, alpha=0.2)
+    plt.legend()
+    plt.xlabel("Episodes")
+    plt.ylabel("Average Return")
+    plt.title(f"Online Evaluation on {n_eval} Envs")
+    return all_means_lnr
+
+
+def offline(eval_trajs, model, n_eval, H, dim, permuted=False):
+    """evals/eval_darkroom.py:124-189: expert vs DPT (sampled and greedy) on fixed contexts."""
+    import matplotlib.pyplot as plt
+    envs = []
+    for i in range(n_eval):
+        traj = eval_trajs[i]
+        envs.append(DarkroomEnvPermuted(dim, traj["perm_index"], H) if permuted else DarkroomEnv(dim, traj["goal"], H))
+    trajs = eval_trajs[:n_eval]
+    vec_env = DarkroomEnvVec(envs)
+    opt = _OptVec(envs)
+    _, _, _, rs_opt = vec_env.deploy_eval(opt)
+    batch = {"context_states": convert_to_tensor([t["context_states"] for t in trajs]),
+             "context_actions": convert_to_tensor([t["context_actions"] for t in trajs]),
+             "context_next_states": convert_to_tensor([t["context_next_states"] for t in trajs]),
+             "context_rewards": convert_to_tensor([t["context_rewards"][:, None] for t in trajs])}
+    res = {"Opt": np.sum(rs_opt, axis=-1)}
+    for name, sample in (("Learner", True), ("Learner (greedy)", False)):
+        ctrl = DarkroomTransformerController(model, batch_size=n_eval, sample=sample)
+        ctrl.set_batch(dict(batch))
+        dm = model.device_model()
+        c = (batch["context_states"], batch["context_actions"], batch["context_next_states"],
+             batch["context_rewards"][..., 0])
+        _, _, _, er = _episode_device(dm, ctrl, vec_env, c, H)
+        res[name] = er.sum(-1).cpu().numpy()
+    means = {k: np.mean(v) for k, v in res.items()}
+    colors = plt.cm.viridis(np.linspace(0, 1, len(means)))
+    plt.bar(means.keys(), means.values(), color=colors)
+    plt.ylabel("Average Return")
+    plt.title(f"Average Return on {n_eval} Trajectories")
+    return res
+
+
+class _OptVec:
+    """Vectorised DarkroomOptPolicy over a DarkroomEnvVec (one device kernel per step)."""
+
+    def __init__(self, envs):
+        self.envs = envs
+        self.vec = DarkroomEnvVec(envs)
+
+    def act(self, states):
+        st = np.stack([np.asarray(s, np.int32) for s in states])
+        a = dpt_hip.darkroom_opt_action(st, self.vec.goals_device, self.vec.perms_device).cpu().numpy()
+        return np.eye(5)[a]
+
+
+__all__ = ["deploy_online_vec", "online", "offline", "DarkroomOptPolicy"]

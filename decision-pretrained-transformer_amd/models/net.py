@@ -117,7 +117,7 @@ class Transformer(nn.Module):
         # transformers 4.5.1 (requirements.txt:1) saved the causal-mask buffers
         # attn.bias / attn.masked_bias in GPT-2 checkpoints; they carry no weights.
         for k in list(state_dict.keys()):
-            if k.startswith(prefix) and (k.endswith("attn.masked_bias") or k.endswith("attn.bias")):
+            if k.startswith(prefix) and (k.endswith(".attn.masked_bias") or k.endswith(".attn.bias")):
                 del state_dict[k]
 
     # ------------------------------------------------------------------ device weights

@@ -50,11 +50,15 @@ extern "C" {
 /* bandit reward type, envs/bandit_env.py:57-63 / envs/gpu_bandit_env.py:57-62 */
 #define DPT_BANDIT_GAUSSIAN 0
 #define DPT_BANDIT_BERNOULLI 1
+/* OR-ed into `type`: fp32 arithmetic, r = float(m) + float(g) * float(var) (two
+ * roundings), the torch semantics of GPUBanditEnv.transit (gpu_bandit_env.py:58-59) */
+#define DPT_BANDIT_F32 16
 
 /* Philox stream ids (counter word 2) */
 #define DPT_STREAM_SELECT 0
 #define DPT_STREAM_REWARD 1
 #define DPT_STREAM_ROLLIN 2
+#define DPT_STREAM_POLICY 16 /* + arm index: baseline-policy draws (Thompson posterior samples) */
 
 int dpt_abi_version(void);
 const char* dpt_last_error(void);
@@ -157,6 +161,30 @@ int dpt_darkroom_opt_action(const int32_t* state, const int32_t* goal, const int
 int dpt_draw(int32_t kind, uint64_t seed, uint64_t counter, int64_t first_task, int32_t N,
              uint32_t stream_id, double* out, void* stream);
 
+/* ------------------------------------------------------------------ data generation
+ * collect_data.py:23-53 rollin_bandit (+ generate_bandit_histories :158-182,
+ * :221-225): for every task i and step h, i.i.d. arm ~ choice(A, probs[i])
+ * (cdf/searchsorted semantics on the given fp64 behaviour policy, which the
+ * host draws as (1-cov)*Dirichlet(1) + cov*e_rand, collect_data.py:30-36) and
+ * r = means[i][arm] + (0.0 + var*g) (or Bernoulli).  uniforms/noise (H,N) or
+ * NULL -> Philox streams DPT_STREAM_ROLLIN / DPT_STREAM_REWARD.
+ * Outputs actions (N,H) int32, rewards (N,H) fp64.                         */
+int dpt_rollin_bandit(const double* means, const double* probs, int32_t N, int32_t A, int32_t H,
+                      int32_t type, double var, const double* uniforms, const double* noise,
+                      uint64_t seed, int64_t first_task, int32_t* actions_out, double* rewards_out,
+                      void* stream);
+
+/* collect_data.py:83-111 rollin_mdp + :189-218: mode 0 'uniform' (i.i.d. state
+ * ~ U{0..dim-1}^2 and action ~ U{0..4} per step; states_in (N,H,2) /
+ * actions_in (N,H) inject them), mode 1 'expert' (greedy walk from (0,0)).
+ * Outputs (N,H,2)/(N,H) int32; query_out (N,2) ~ U and opt_action_out (N) =
+ * its expert label (optional).                                              */
+int dpt_rollin_darkroom(const int32_t* goal, const int32_t* perm, int32_t N, int32_t H, int32_t dim,
+                        int32_t mode, const int32_t* states_in, const int32_t* actions_in,
+                        uint64_t seed, int64_t first_task, int32_t* states_out,
+                        int32_t* actions_out, int32_t* next_states_out, int32_t* rewards_out,
+                        int32_t* query_out, int32_t* opt_action_out, void* stream);
+
 /* ------------------------------------------------------------------ fused rollouts
  * The whole online loop on device, one launch: replaces
  * evals/eval_bandit.py:56-103 (and the identical evals/eval_linear_bandit.py:54-97)
@@ -185,6 +213,51 @@ typedef struct dpt_bandit_rollout_args {
 
 int dpt_rollout_bandit(const dpt_model* model, const dpt_bandit_rollout_args* args_host,
                        void* stream);
+
+/* The classical comparison policies of the same online loop, fused with the env
+ * (one lane per task, all H steps): replaces deploy_online_vec with
+ *   DPT_POLICY_OPT      OptPolicy            ctrls/ctrl_bandit.py:22-38
+ *   DPT_POLICY_EMP      EmpMeanPolicy        :57-118  (online flag: play unseen arms first)
+ *   DPT_POLICY_UCB      UCBPolicy(c)         :318-380
+ *   DPT_POLICY_THOMPSON ThompsonSampling     :122-251 (std, prior_mean, prior_var; sample 0 = 100-draw vote)
+ *   DPT_POLICY_LCB      PessMeanPolicy(c)    :255-314
+ *   DPT_POLICY_LINUCB   LinUCBPolicy(c)      :447-528 (arms (A, lin_d), lin_d <= 2)
+ * Per-arm statistics are recomputed each step from the per-arm reward lists in
+ * numpy's fp64 pairwise-summation order, as the reference does, so action
+ * indices match it bit for bit given the same draws.  policy_noise: Thompson
+ * (H,N,A) posterior normals; LinUCB (N) uniforms for the empty-context arm.  */
+#define DPT_POLICY_OPT 0
+#define DPT_POLICY_EMP 1
+#define DPT_POLICY_UCB 2
+#define DPT_POLICY_THOMPSON 3
+#define DPT_POLICY_LCB 4
+#define DPT_POLICY_LINUCB 5
+
+typedef struct dpt_policy_rollout_args {
+    int32_t N, H, A, policy;
+    int32_t online, type, sample, lin_d;
+    int64_t first_task;
+    double var;          /* env reward noise std */
+    double c;            /* UCB / LCB / LinUCB constant */
+    double ts_std, ts_prior_mean, ts_prior_var;
+    uint64_t seed;
+    const double* means;        /* (N, A) */
+    const double* arms;         /* (A, lin_d) or NULL */
+    const double* noise;        /* (H, N) or NULL */
+    const double* policy_noise; /* see above, or NULL */
+    double* workspace;          /* dpt_policy_workspace_numel(N, A, C + H) doubles */
+    int32_t* actions_out;       /* (N, H) */
+    double* rewards_out;        /* (N, H) */
+    double* arm_value_out;      /* (N, H) */
+    /* optional prefix context (set_batch_numpy_vec): C transitions per task,
+     * replayed into the statistics before step 0 (offline eval: C = h, H = 1) */
+    int32_t C, reserved0;
+    const int32_t* ctx_actions; /* (N, C) arm indices */
+    const double* ctx_rewards;  /* (N, C) */
+} dpt_policy_rollout_args;
+
+int dpt_policy_workspace_numel(int32_t N, int32_t A, int32_t H, int64_t* numel_out_host);
+int dpt_rollout_policy(const dpt_policy_rollout_args* args_host, void* stream);
 
 #ifdef __cplusplus
 }

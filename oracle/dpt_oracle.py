@@ -342,3 +342,82 @@ def rollin_bandit(means, cov, dirichlet, rand_index, u, g, var):
     us = np.eye(A)[idx]
     rs = means[idx] + (0.0 + var * np.asarray(g, np.float64))
     return np.ones((len(u), 1)), us, np.ones((len(u), 1)), rs
+
+
+# ----------------------------------------------------------------------------- classical baselines
+
+
+def policy_action(policy, acts_ctx, rews_ctx, A, online=True, c=1.0, ts=None, ts_g=None, arms=None,
+                  first_u_idx=None):
+    """One decision of a classical controller from its context (fp64 numpy, the reference's
+    arithmetic).  acts_ctx (N, h) int, rews_ctx (N, h) float64.
+
+    emp: ctrls/ctrl_bandit.py:89-118; ucb :348-380; lcb :286-314; thompson :184-236
+    (sample=True, posterior normals ts_g (N, A)); linucb :488-528 (first_u_idx (N) for h=0).
+    """
+    N, h = acts_ctx.shape
+    if policy == "linucb":
+        if h < 1:
+            return np.asarray(first_u_idx)
+        out = np.zeros(N, np.int64)
+        for i in range(N):
+            X = arms[acts_ctx[i]]
+            cov = np.eye(arms.shape[1]) + X.T @ X
+            cinv = np.linalg.inv(cov)
+            theta = (cinv @ X.T @ rews_ctx[i][:, None]).flatten()
+            best, bi = -np.inf, None
+            for k, arm in enumerate(arms):
+                v = theta @ arm + c * np.sqrt(arm @ cinv @ arm)
+                if v > best:
+                    best, bi = v, k
+            out[i] = bi
+        return out
+    b = np.zeros((N, A))
+    counts = np.zeros((N, A))
+    for i in range(N):
+        for k in range(A):
+            r = rews_ctx[i][acts_ctx[i] == k]
+            b[i, k] = np.sum(r)
+            counts[i, k] = len(r)
+    if policy == "thompson":
+        var, pm, pv = ts["std"] ** 2, ts["prior_mean"], ts["prior_var"]
+        means = np.ones((N, A)) * pm
+        variances = np.ones((N, A)) * pv
+        arm_means = np.zeros((N, A))
+        for i in range(N):
+            for k in range(A):
+                if counts[i, k] > 0:
+                    arm_means[i, k] = np.mean(rews_ctx[i][acts_ctx[i] == k])
+        with np.errstate(divide="ignore", invalid="ignore"):
+            w = var / (var + counts * pv)
+            new_mean = w * pm + (1 - w) * arm_means
+            new_var = 1 / (1 / pv + counts / var)
+        mask = counts > 0
+        means[mask] = new_mean[mask]
+        variances[mask] = new_var[mask]
+        return np.argmax(means + np.sqrt(variances) * ts_g, axis=-1)
+    b_mean = b / np.maximum(1, counts)
+    if policy in ("ucb", "lcb"):
+        bons = c / np.maximum(1, np.sqrt(counts))
+        b_mean = b_mean + bons if policy == "ucb" else b_mean - bons
+    i = np.argmax(b_mean, axis=-1)
+    if policy == "ucb" or (policy == "emp" and online):
+        j = np.argmin(counts, axis=-1)
+        mask = counts[np.arange(N), j] == 0
+        i[mask] = j[mask]
+    return i
+
+
+def bandit_policy_rollout(policy, means, H, var, g, **kw):
+    """evals/eval_bandit.py:56-103 with a classical controller; draws injected.
+    kw: online, c, ts (dict std/prior_mean/prior_var), ts_g (H, N, A), arms, first_u_idx."""
+    means = np.asarray(means, np.float64)
+    N, A = means.shape
+    acts = np.zeros((N, H), np.int64)
+    rews = np.zeros((N, H))
+    ts_g = kw.pop("ts_g", None)
+    for h in range(H):
+        a = policy_action(policy, acts[:, :h], rews[:, :h], A, ts_g=None if ts_g is None else ts_g[h], **kw)
+        acts[:, h] = a
+        rews[:, h] = bandit_reward(means, a, g[h], var)
+    return dict(actions=acts, rewards=rews, cum_means=np.stack([arm_value(means, acts[:, h]) for h in range(H)]))

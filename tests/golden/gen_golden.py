@@ -75,6 +75,7 @@ class DrawRecorder:
         self.g = []
         self.choice_kind = []
         self.plain = []
+        self.garr = []
         self._choice = np.random.choice
         self._normal = np.random.normal
 
@@ -119,6 +120,14 @@ class DrawRecorder:
             assert out == loc + scale * g, "normal(loc,s) != loc + s*g"
             self.g.append(g)
             return out
+        if size is None:  # array loc/scale (Thompson posterior draw, ctrl_bandit.py:232)
+            rs = self._replica()
+            g = rs.standard_normal(np.broadcast(loc, scale).shape)
+            out = self._normal(loc, scale)
+            assert self._same_state(rs), "array normal consumed != standard_normal(shape)"
+            assert np.array_equal(out, loc + scale * g), "normal(loc,s) != loc + s*g (array)"
+            self.garr.append(g)
+            return out
         return self._normal(loc, scale, size)
 
     def __enter__(self):
@@ -149,10 +158,109 @@ def perturbed_state_dict(model, seed, scale=0.05):
             if not k.endswith("wte.weight")}
 
 
+def baselines():
+    """F8: the classical policies of eval_bandit.online / offline, through the reference loop."""
+    import numpy as np
+    from envs import bandit_env
+    from ctrls import ctrl_bandit as cb
+    from evals import eval_bandit, eval_linear_bandit
+
+    def run(mod, envs, ctrl, H, seed):
+        vec = bandit_env.BanditEnvVec(envs)
+        np.random.seed(seed)
+        with DrawRecorder(np) as rec:
+            cm, meta = mod.deploy_online_vec(vec, ctrl, H, include_meta=True)
+        return cm, meta, rec
+
+    out = {}
+    rs = np.random.RandomState(81)
+    N, H, A, var = 200, 24, 5, 0.3  # UCBPolicy.act_numpy_vec only works for 200 tasks (ctrl_bandit.py:374)
+    means = rs.uniform(0, 1, (N, A))
+    out["means"] = means
+    for name, mk in (("emp", lambda e: cb.EmpMeanPolicy(e[0], online=True, batch_size=N)),
+                     ("ucb", lambda e: cb.UCBPolicy(e[0], const=1.0, batch_size=N)),
+                     ("thomp", lambda e: cb.ThompsonSamplingPolicy(e[0], std=var, sample=True, prior_mean=0.5,
+                                                                     prior_var=1 / 12.0, warm_start=False,
+                                                                     batch_size=N))):
+        envs = [bandit_env.BanditEnv(m, H, var=var) for m in means]
+        cm, meta, rec = run(eval_bandit, envs, mk(envs), H, 90 + len(name))
+        out[f"{name}/cum_means"] = cm
+        out[f"{name}/actions"] = meta["context_actions"].argmax(-1)
+        out[f"{name}/rewards"] = meta["context_rewards"][..., 0]
+        out[f"{name}/g"] = np.array(rec.g).reshape(H, N)
+        if rec.garr:
+            out[f"{name}/policy_g"] = np.stack(rec.garr)  # (H, N, A)
+    # offline decisions on a fixed context (var forced to 0 by deploy_eval)
+    h = 30
+    ca = np.eye(A)[rs.randint(0, A, (N, h))]
+    cr = (means[np.arange(N)[:, None], ca.argmax(-1)] + 0.3 * rs.normal(size=(N, h)))[..., None]
+    batch = {"context_states": np.ones((N, h, 1)), "context_actions": ca, "context_next_states": np.ones((N, h, 1)),
+             "context_rewards": cr}
+    out.update({"off/ctx_actions": ca.argmax(-1), "off/ctx_rewards": cr[..., 0]})
+    envs = [bandit_env.BanditEnv(m, h, var=var) for m in means]
+    vec = bandit_env.BanditEnvVec(envs)
+    for name, pol in (("emp", cb.EmpMeanPolicy(envs[0], online=False, batch_size=N)),
+                      ("lcb", cb.PessMeanPolicy(envs[0], const=.8, batch_size=N))):
+        pol.set_batch_numpy_vec(batch)
+        _, us, _, rsum = vec.deploy_eval(pol)
+        out[f"off/{name}/actions"] = us.argmax(-1)
+        out[f"off/{name}/rewards"] = rsum
+    # LinUCB on linear bandits (eval_linear_bandit.online leg)
+    arms = np.random.RandomState(1234).normal(size=(10, 2)) / np.sqrt(2)
+    thetas = rs.normal(0, 1, (N, 2)) / np.sqrt(2)
+    lenvs = [bandit_env.LinearBanditEnv(t, arms, 16, var=var) for t in thetas]
+    cm, meta, rec = run(eval_linear_bandit, lenvs, cb.LinUCBPolicy(lenvs[0], const=1.0, batch_size=N), 16, 77)
+    out.update({"lin/means": np.stack([e.means for e in lenvs]), "lin/arms": arms, "lin/cum_means": cm,
+                "lin/actions": meta["context_actions"].argmax(-1), "lin/g": np.array(rec.g).reshape(16, N),
+                "lin/first_action": np.asarray(rec.plain[0])})
+    np.savez_compressed(os.path.join(OUT, "baselines.npz"), **out)
+    print("F8 baselines")
+
+
+def host_surface():
+    """F9: filenames (utils.py:14-190) and argparse defaults (common_args.py:2-59) -> JSON."""
+    import argparse
+    import json
+    import utils
+    import common_args
+    cases = []
+    cfgs = [dict(n_hists=1, n_samples=1, horizon=500, dim=5, var=0.3, cov=0.0, lin_d=2, rollin_type="uniform"),
+            dict(n_hists=3, n_samples=2, horizon=100, dim=10, var=0.0, cov=0.5, lin_d=3, rollin_type="uniform")]
+    for cfg in cfgs:
+        for mode in (0, 1, 2):
+            cases.append(["build_bandit_data_filename", ["bandit", 100000, cfg, mode],
+                          utils.build_bandit_data_filename("bandit", 100000, cfg, mode)])
+            cases.append(["build_linear_bandit_data_filename", ["linear_bandit", 1000, cfg, mode],
+                          utils.build_linear_bandit_data_filename("linear_bandit", 1000, cfg, mode)])
+            cases.append(["build_darkroom_data_filename", ["darkroom_heldout", 100, cfg, mode],
+                          utils.build_darkroom_data_filename("darkroom_heldout", 100, cfg, mode)])
+    mcfg = dict(shuffle=True, lr=0.0001, dropout=0, n_embd=32, n_layer=4, n_head=4, n_envs=100000, n_hists=1,
+                n_samples=1, var=0.3, cov=0.0, horizon=500, dim=5, seed=1, lin_d=2)
+    for fn, env in (("build_bandit_model_filename", "bandit"), ("build_linear_bandit_model_filename", "linear_bandit"),
+                    ("build_darkroom_model_filename", "darkroom_heldout")):
+        cases.append([fn, [env, mcfg], getattr(utils, fn)(env, mcfg)])
+    p = argparse.ArgumentParser()
+    common_args.add_dataset_args(p)
+    common_args.add_model_args(p)
+    common_args.add_train_args(p)
+    common_args.add_eval_args(p)
+    defaults = vars(p.parse_args(["--env", "bandit"]))
+    json.dump({"filenames": cases, "defaults": defaults}, open(os.path.join(OUT, "host_surface.json"), "w"),
+              indent=1, sort_keys=True)
+    print("F9 host_surface")
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit("reference checkout not present; fixtures are committed")
     _install_stubs()
+    if len(sys.argv) > 1:  # regenerate only the named groups, e.g. `gen_golden.py baselines`
+        import matplotlib
+        matplotlib.use("Agg")
+        sys.path[:0] = [REF, os.path.join(REF, "models")]
+        for name in sys.argv[1:]:
+            globals()[name]()
+        return
     import matplotlib
     matplotlib.use("Agg")
     sys.path[:0] = [REF, os.path.join(REF, "models")]

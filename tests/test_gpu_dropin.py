@@ -1,0 +1,245 @@
+"""The reference-named drop-in layer (envs/, ctrls/, evals/, models/, collect_data) on the GPU,
+against golden vectors recorded from the reference and the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import dpt_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_model(name):
+    """models.net.Transformer loaded (strict) from a reference state_dict fixture."""
+    from models.net import Transformer
+    g = golden(f"forward_{name}.npz")
+    H, sd, A, L, E = (int(x) for x in g["cfg"])
+    m = Transformer(dict(horizon=H, state_dim=sd, action_dim=A, n_layer=L, n_embd=E, n_head=4, dropout=0.0,
+                         test=True))
+    state = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w/")}
+    state["transformer.wte.weight"] = m.transformer.wte.weight.detach().clone()
+    state["transformer.h.0.attn.bias"] = torch.ones(1)  # transformers 4.5.1 legacy buffer: dropped on load
+    m.load_state_dict(state)
+    return g, m
+
+
+def test_transformer_forward_drop_in():
+    g, m = ref_model("darkroom")
+    for T in (1, 8, 101):
+        b = {"query_states": torch.from_numpy(g[f"T{T}/query"]).float(),
+             "zeros": torch.zeros(16, 2 ** 2 + 5 + 1)}
+        if T > 1:
+            b.update(context_states=torch.from_numpy(g[f"T{T}/cs"]).float(),
+                     context_actions=torch.from_numpy(g[f"T{T}/ca"]).float(),
+                     context_next_states=torch.from_numpy(g[f"T{T}/cn"]).float(),
+                     context_rewards=torch.from_numpy(g[f"T{T}/cr"]).float())
+        else:
+            b.update(context_states=torch.zeros(16, 0, 2), context_actions=torch.zeros(16, 0, 5),
+                     context_next_states=torch.zeros(16, 0, 2), context_rewards=torch.zeros(16, 0, 1))
+        out = m(b).cpu().numpy()
+        ref = g[f"T{T}/logits"]
+        assert (np.abs(out - ref) <= 1e-5 * np.maximum(1, np.abs(ref))).all()
+    # parameter change -> device weights repacked
+    with torch.no_grad():
+        m.pred_actions.bias += 1.0
+    out2 = m(b).cpu().numpy()
+    assert np.allclose(out2, out + 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("tag", ["sample", "greedy"])
+def test_eval_bandit_deploy_online_vec(tag):
+    from ctrls.ctrl_bandit import BanditTransformerController
+    from envs.bandit_env import BanditEnv, BanditEnvVec
+    from evals import eval_bandit
+    r = golden(f"rollout_bandit_{tag}.npz")
+    _, m = ref_model("bandit5")
+    n, H, A, sample = (int(x) for x in r["cfg"])
+    envs = [BanditEnv(mu, H, var=float(r["var"])) for mu in r["means"]]
+    vec = BanditEnvVec(envs)
+    ctrl = BanditTransformerController(m, sample=bool(sample), batch_size=n)
+    cm, meta = eval_bandit.deploy_online_vec(vec, ctrl, H, include_meta=True, uniforms=r["u"] if sample else None,
+                                             noise=r["g"])
+    assert np.array_equal(cm, r["cum_means"])
+    for k, ref in (("context_actions", r["ctx_actions"]), ("context_states", r["ctx_states"]),
+                   ("context_next_states", r["ctx_next_states"])):
+        assert np.array_equal(meta[k], ref), k
+    assert np.array_equal(meta["context_rewards"][..., 0], r["ctx_rewards"])
+
+
+def test_generic_loop_equals_fused():
+    """The reference per-step loop (controller stepped through envs on device) and the fused
+    kernel give the same trajectory for the same injected draws."""
+    from ctrls.ctrl_bandit import BanditTransformerController
+    from envs.bandit_env import BanditEnv, BanditEnvVec
+    from evals import eval_bandit
+    r = golden("rollout_bandit_greedy.npz")
+    _, m = ref_model("bandit5")
+    n, H = 8, 12
+    envs = [BanditEnv(mu, H, var=0.0) for mu in r["means"]]
+    vec = BanditEnvVec(envs)
+
+    cm_f = eval_bandit.deploy_online_vec(vec, BanditTransformerController(m, sample=False, batch_size=n), H)
+    cm_g = eval_bandit.deploy_online_vec(vec, BanditTransformerController(m, sample=False, batch_size=n), H,
+                                         fused=False)
+    assert np.array_equal(cm_f, cm_g)
+    # classical policies: per-step prefix-context kernel calls == fused kernel (var=0: no env noise)
+    from ctrls.ctrl_bandit import EmpMeanPolicy, UCBPolicy
+    for mk in (lambda: EmpMeanPolicy(envs[0], online=True, batch_size=n), lambda: UCBPolicy(envs[0], batch_size=n)):
+        a = eval_bandit.deploy_online_vec(vec, mk(), H)
+        b = eval_bandit.deploy_online_vec(vec, mk(), H, fused=False)
+        assert np.array_equal(a, b)
+
+
+def test_offline_greedy_matches_reference():
+    from ctrls.ctrl_bandit import BanditTransformerController
+    from envs.bandit_env import BanditEnv, BanditEnvVec
+    r = golden("offline_bandit.npz")
+    _, m = ref_model("bandit5")
+    n, h = r["ctx_actions"].shape[:2]
+    envs = [BanditEnv(mu, h, var=0.3) for mu in r["means"]]
+    vec = BanditEnvVec(envs)
+    ctrl = BanditTransformerController(m, sample=False, batch_size=n)
+    ctrl.set_batch_numpy_vec({"context_states": np.ones((n, h, 1)), "context_actions": r["ctx_actions"],
+                              "context_next_states": np.ones((n, h, 1)), "context_rewards": r["ctx_rewards"][..., None]})
+    _, us, _, rs = vec.deploy_eval(ctrl)
+    assert np.array_equal(us.argmax(-1), r["actions"])
+    assert np.array_equal(rs, r["rewards"])  # var forced to 0: rewards = means[a] exactly
+
+
+@pytest.mark.parametrize("name", ["emp", "ucb", "thomp"])
+def test_baseline_policy_kernel(name):
+    import dpt_hip
+    g = golden("baselines.npz")
+    code = {"emp": dpt_hip.POLICY_EMP, "ucb": dpt_hip.POLICY_UCB, "thomp": dpt_hip.POLICY_THOMPSON}[name]
+    kw = dict(online=True, c=1.0, ts_std=0.3, ts_prior_mean=0.5, ts_prior_var=1 / 12.0)
+    H = g[f"{name}/g"].shape[0]
+    out = dpt_hip.rollout_policy(code, g["means"], H, 0.3, noise=g[f"{name}/g"],
+                                 policy_noise=g.get(f"{name}/policy_g"), **kw)
+    assert np.array_equal(out["actions"].cpu().numpy(), g[f"{name}/actions"])
+    assert np.array_equal(out["rewards"].cpu().numpy(), g[f"{name}/rewards"])
+    assert np.array_equal(out["arm_value"].cpu().numpy().T, g[f"{name}/cum_means"])
+
+
+def test_baseline_offline_prefix_and_linucb():
+    import dpt_hip
+    g = golden("baselines.npz")
+    ca, cr = g["off/ctx_actions"], g["off/ctx_rewards"]
+    for name, code, c in (("emp", dpt_hip.POLICY_EMP, 1.0), ("lcb", dpt_hip.POLICY_LCB, 0.8)):
+        out = dpt_hip.rollout_policy(code, g["means"], 1, 0.0, online=False, c=c, ctx_actions=ca, ctx_rewards=cr)
+        assert np.array_equal(out["actions"][:, 0].cpu().numpy(), g[f"off/{name}/actions"])
+    A = g["lin/arms"].shape[0]
+    u = (g["lin/first_action"] + 0.5) / A
+    H = g["lin/g"].shape[0]
+    out = dpt_hip.rollout_policy(dpt_hip.POLICY_LINUCB, g["lin/means"], H, 0.3, c=1.0, arms=g["lin/arms"],
+                                 noise=g["lin/g"], policy_noise=u)
+    acts = out["actions"].cpu().numpy()
+    # LinUCB: closed-form 2x2 inverse vs LAPACK -> indices equal up to near-ties
+    agree = (acts == g["lin/actions"]).mean()
+    assert agree >= 0.99, agree
+    assert np.array_equal(acts[:, 0], g["lin/first_action"])
+
+
+def test_online_and_offline_eval_run():
+    import matplotlib
+    matplotlib.use("Agg")
+    from evals import eval_bandit
+    _, m = ref_model("bandit5")
+    rs = np.random.RandomState(3)
+    trajs = [{"means": rs.uniform(0, 1, 5), "context_states": np.ones((30, 1)),
+              "context_actions": np.eye(5)[rs.randint(0, 5, 30)], "context_next_states": np.ones((30, 1)),
+              "context_rewards": rs.normal(0.5, 0.3, 30)} for _ in range(16)]
+    np.random.seed(0)
+    all_means, st = eval_bandit.online(trajs, m, n_eval=16, horizon=30, var=0.3, bandit_type="uniform")
+    assert set(all_means) == {"opt", "Lnr", "Emp", "UCB1.0", "Thomp"}
+    assert all(v.shape == (16, 30) for v in all_means.values())
+    assert (st["regret_means"]["opt"] == 0).all()
+    base = eval_bandit.offline(trajs, m, n_eval=16, horizon=30, var=0.3, bandit_type="uniform")
+    assert set(base) == {"opt", "lnr", "emp", "thmp", "lcb"}
+    assert (base["opt"] >= base["lnr"] - 1e-12).all()
+
+
+def test_eval_darkroom_device_loop_matches_reference():
+    from ctrls.ctrl_darkroom import DarkroomTransformerController
+    from envs.darkroom_env import DarkroomEnv, DarkroomEnvPermuted, DarkroomEnvVec
+    from evals import eval_darkroom
+    _, m = ref_model("darkroom")
+    for tag in ("sample", "greedy", "permuted"):
+        r = golden(f"rollout_darkroom_{tag}.npz")
+        n, Heps, H, horizon, sample = (int(x) for x in r["cfg"])
+        if tag == "permuted":
+            envs = [DarkroomEnvPermuted(10, int(i), horizon) for i in r["perm_index"]]
+        else:
+            envs = [DarkroomEnv(10, g_, horizon) for g_ in r["goals"]]
+        ctrl = DarkroomTransformerController(m, batch_size=n, sample=bool(sample))
+        u = r["u"].reshape(-1, n)
+        ctrl.uniforms = lambda k: u[k]
+        ret = eval_darkroom.deploy_online_vec(DarkroomEnvVec(envs), ctrl, Heps, H, horizon)
+        assert np.array_equal(ret, r["returns"]), tag
+
+
+def test_rollin_kernels_match_oracle():
+    import dpt_hip
+    g = golden("rollin.npz")
+    for i in range(6):
+        means, cov, dr = g[f"{i}/means"], float(g[f"{i}/cov"]), g[f"{i}/dirichlet"]
+        p = (1 - cov) * dr + cov * np.eye(5)[int(g[f"{i}/rand_index"])]
+        u, gg = g[f"{i}/u"], g[f"{i}/g"]
+        acts, rews = dpt_hip.rollin_bandit(means[None], p[None], len(u), 0.3, uniforms=u[:, None], noise=gg[:, None])
+        assert np.array_equal(np.eye(5)[acts.cpu().numpy()[0]], g[f"{i}/us"])
+        assert np.array_equal(rews.cpu().numpy()[0], g[f"{i}/rs"])
+    s, a = g["mdp/states"], g["mdp/actions"].argmax(-1)
+    o = dpt_hip.rollin_darkroom(g["mdp/goal"][None], len(a), 10, states=s[None], actions=a[None])
+    assert np.array_equal(o["next_states"].cpu().numpy()[0], g["mdp/next_states"])
+    assert np.array_equal(o["rewards"].cpu().numpy()[0], g["mdp/rewards"])
+    # expert rollin walks to the goal: reward 1 from arrival on
+    goals = np.array([[3, 7], [9, 9], [0, 0]])
+    o = dpt_hip.rollin_darkroom(goals, 25, 10, mode=1)
+    rw = o["rewards"].cpu().numpy()
+    assert (rw[:, -1] == 1).all() and (rw[2] == 1).all()
+
+
+def test_collect_data_generators_format():
+    import collect_data
+    from envs import bandit_env
+    np.random.seed(0)
+    trajs = collect_data.generate_bandit_histories(64, 5, 20, 0.3, n_hists=2, n_samples=2, cov=0.0, type="uniform")
+    assert len(trajs) == 64 * 4
+    t = trajs[0]
+    assert set(t) == {"query_state", "optimal_action", "context_states", "context_actions", "context_next_states",
+                      "context_rewards", "means"}
+    assert t["context_actions"].shape == (20, 5) and t["context_actions"].dtype == np.float64
+    assert t["context_states"].shape == (20, 1) and t["context_rewards"].shape == (20,)
+    a = t["context_actions"].argmax(-1)
+    noise = t["context_rewards"] - t["means"][a]
+    assert np.abs(noise).max() < 0.3 * 6
+    goals = np.array([[1, 2], [3, 4], [9, 9]])
+    dtr = collect_data.generate_darkroom_histories(goals, 10, 30, n_hists=1, n_samples=3, rollin_type="uniform")
+    assert len(dtr) == 9
+    for t in dtr:
+        ns, r = O.darkroom_transit(t["context_states"], t["context_actions"].argmax(-1),
+                                   np.broadcast_to(t["goal"], (30, 2)))
+        assert np.array_equal(ns, t["context_next_states"]) and np.array_equal(r, t["context_rewards"])
+        q = t["query_state"][None]
+        assert t["optimal_action"].argmax() == O.darkroom_opt_action(q, t["goal"][None])[0]
+    lin = collect_data.generate_linear_bandit_histories(8, 10, 2, 12, 0.3, n_hists=1, n_samples=1, cov=0.0,
+                                                        data_type="thompson")
+    assert len(lin) == 8 and lin[0]["context_actions"].shape == (12, 10)
+    assert isinstance(bandit_env.LinearBanditEnv(lin[0]["theta"], lin[0]["arms"], 12).means, np.ndarray)
+
+
+def test_gpu_bandit_env():
+    from envs.gpu_bandit_env import GPUBanditEnv
+    torch.manual_seed(0)
+    env = GPUBanditEnv(5, 64, 3, var=0.3)
+    env.reset()
+    us = torch.nn.functional.one_hot(torch.randint(0, 5, (64,)), 5).float().cuda()
+    _, r, done, _ = env.step(us)
+    assert r.dtype == torch.float32 and r.shape == (64,) and not bool(done.any())
+    env.step(us)
+    _, _, done, _ = env.step(us)
+    assert bool(done.all())
+    with pytest.raises(ValueError):
+        env.step(us)
+    m = env.means[torch.arange(64), us.argmax(1)]
+    assert float((r - m).abs().max()) < 0.3 * 6

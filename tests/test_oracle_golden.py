@@ -123,3 +123,29 @@ def test_rollin_bandit():
     s, a, ns, r = (g[f"mdp/{k}"] for k in ("states", "actions", "next_states", "rewards"))
     ns2, r2 = O.darkroom_transit(s, a.argmax(-1), np.broadcast_to(g["mdp/goal"], s.shape))
     assert np.array_equal(ns2, ns) and np.array_equal(r2, r)
+
+
+@pytest.mark.parametrize("name", ["emp", "ucb", "thomp"])
+def test_baseline_rollouts(name):
+    g = golden("baselines.npz")
+    kw = dict(emp=dict(policy="emp", online=True), ucb=dict(policy="ucb", c=1.0),
+              thomp=dict(policy="thompson", ts=dict(std=0.3, prior_mean=0.5, prior_var=1 / 12.0)))[name]
+    if name == "thomp":
+        kw["ts_g"] = g["thomp/policy_g"]
+    H = g[f"{name}/g"].shape[0]
+    out = O.bandit_policy_rollout(kw.pop("policy"), g["means"], H, 0.3, g[f"{name}/g"], **kw)
+    assert np.array_equal(out["actions"], g[f"{name}/actions"])
+    assert np.array_equal(out["rewards"], g[f"{name}/rewards"])
+    assert np.array_equal(out["cum_means"], g[f"{name}/cum_means"])
+
+
+def test_baseline_offline_and_linucb():
+    g = golden("baselines.npz")
+    ca, cr = g["off/ctx_actions"], g["off/ctx_rewards"]
+    assert np.array_equal(O.policy_action("emp", ca, cr, 5, online=False), g["off/emp/actions"])
+    assert np.array_equal(O.policy_action("lcb", ca, cr, 5, c=0.8), g["off/lcb/actions"])
+    H = g["lin/g"].shape[0]
+    out = O.bandit_policy_rollout("linucb", g["lin/means"], H, 0.3, g["lin/g"], c=1.0, arms=g["lin/arms"],
+                                  first_u_idx=g["lin/first_action"])
+    assert np.array_equal(out["actions"], g["lin/actions"])
+    assert np.array_equal(out["cum_means"], g["lin/cum_means"])
