@@ -3,9 +3,13 @@
 One "step" = one full online rollout (evals/eval_bandit.py:56-103 with the DPT
 controller sampling, ctrls/ctrl_bandit.py:422-444) of N_local = 4096 tasks x
 H = 500 env steps on each GPU (BASELINE.json configs[1]; weak scaling over
-GPUs, tasks sharded by global id, Philox keyed by global task id), followed by
+GPUs: contiguous task blocks, Philox keyed by global task id), followed by
 the RCCL all-gather of the per-task arm-value curves (the regret inputs).
 Inputs (weights, means) are resident in HBM before the timed region.
+
+Other workloads (not the headline line): --workload linear (config 4 shard:
+20-arm linear bandit, H=1000, 4096 tasks/GPU), --workload darkroom (config 3:
+DarkRoom 10x10, H=100, Heps=40, 4096 tasks/GPU).
 
 Prints ONE JSON line on rank 0.  Launch: python bench.py [--gpus N --steps K --warmup W]
 (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...).
@@ -22,7 +26,8 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "decision-pretrained-transformer_amd"), ROOT]
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: FP32 matrix 157.3 TFLOP/s (spec)
 
 
 def synthetic_state_dict(n_layer, state_dim, action_dim, horizon, seed=0):
@@ -39,7 +44,7 @@ def synthetic_state_dict(n_layer, state_dim, action_dim, horizon, seed=0):
         if k.endswith("wte.weight"):
             continue
         sd[k] = v + 0.05 * torch.from_numpy(rs.standard_normal(tuple(v.shape)).astype(np.float32))
-    return sd
+    return sd, m
 
 
 def algorithmic_bytes(N, H, n_layer, E=32):
@@ -52,36 +57,45 @@ def algorithmic_bytes(N, H, n_layer, E=32):
     return N * per_task
 
 
-def cpu_baseline(sd, means, H, var, n_layer, A):
+def window_flops(T, n_layer, F, A, E=32):
+    """FLOPs of one causal window forward over T tokens (embed, L blocks, ln_f, head):
+    per block 2*T*E*(3E + E + 4E + 4E) dense + 2 * 2*E * T(T+1)/2 attention."""
+    dense = 2 * T * E * (3 * E + E + 4 * E + 4 * E)
+    attn = 2 * 2 * E * T * (T + 1) // 2
+    return n_layer * (dense + attn) + 2 * T * F * E + 2 * E * A
+
+
+def cpu_info():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(sd, means, H, var, n_layer, A, n_rec=128, n_kv=2048):
+    """The C oracle (oracle/dpt_oracle.c) on this host's cores: reference algorithm
+    (whole window re-forwarded each step) on a bounded task sample, and the same
+    arithmetic with an exact K/V cache."""
     from oracle import c_oracle
     import dpt_hip
     threads = max(1, min(16, os.cpu_count() or 1))
     blob = dpt_hip.pack_weights(sd, n_layer).numpy()
     npos = 4 * (1 + H)
     rs = np.random.RandomState(7)
-    n_rec = 128  # ~10-20 s of CPU work on a 16-thread share
-    u = rs.uniform(size=(H, n_rec))
-    g = rs.normal(size=(H, n_rec))
+    u, g = rs.uniform(size=(H, n_rec)), rs.normal(size=(H, n_rec))
     t0 = time.perf_counter()
     c_oracle.bandit_rollout(blob, n_layer, A, npos, means[:n_rec], H, var, u, g, True, True, threads)
     t_rec = time.perf_counter() - t0
-    n_kv = 2048
-    u = rs.uniform(size=(H, n_kv))
-    g = rs.normal(size=(H, n_kv))
+    u, g = rs.uniform(size=(H, n_kv)), rs.normal(size=(H, n_kv))
     t0 = time.perf_counter()
     c_oracle.bandit_rollout(blob, n_layer, A, npos, means[:n_kv], H, var, u, g, True, False, threads)
     t_kv = time.perf_counter() - t0
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
     return ({"value": n_rec * H / t_rec, "unit": "env-steps/s", "cores": threads, "kind": "port",
              "sample": f"{n_rec} tasks x H={H} full online rollout, reference algorithm (whole window "
-                       f"re-forwarded every step, evals/eval_bandit.py:56-103), fp32 C + OpenMP, {cpu}",
+                       f"re-forwarded every step, evals/eval_bandit.py:56-103), fp32 C + OpenMP, {cpu_info()}",
              "seconds": t_rec},
             {"value": n_kv * H / t_kv, "unit": "env-steps/s", "cores": threads, "kind": "port-kvcache",
              "sample": f"{n_kv} tasks x H={H}, same C oracle with an exact K/V cache", "seconds": t_kv})
@@ -92,9 +106,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=("bandit", "linear", "darkroom"), default="bandit")
     ap.add_argument("--tasks", type=int, default=4096, help="tasks per GPU")
-    ap.add_argument("--H", type=int, default=500)
-    ap.add_argument("--arms", type=int, default=5)
+    ap.add_argument("--H", type=int, default=None)
     ap.add_argument("--var", type=float, default=0.3)
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -109,20 +123,59 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import dpt_hip
+    from dpt_hip.distributed import gather_rows, shard
 
-    N, H, A, L = args.tasks, args.H, args.arms, args.layers
-    sd = synthetic_state_dict(L, 1, A, H, seed=0)
-    model = dpt_hip.DeviceModel(sd, L, 1, A, 4 * (1 + H))
-    means_all = np.random.RandomState(1).uniform(0, 1, (N * world, A))
-    first = rank * N
-    means = torch.from_numpy(means_all[first:first + N]).cuda()
-    gather = torch.empty((world * N, H), dtype=torch.float64, device="cuda") if world > 1 else None
+    N, L, wl = args.tasks, args.layers, args.workload
+    n_total = N * world
+    first, count = shard(n_total, world, rank)
+    extra = {}
+    if wl in ("bandit", "linear"):
+        A, H = (5, args.H or 500) if wl == "bandit" else (20, args.H or 1000)
+        sd, _ = synthetic_state_dict(L, 1, A, H, seed=0)
+        model = dpt_hip.DeviceModel(sd, L, 1, A, 4 * (1 + H))
+        if wl == "bandit":
+            means_all = np.random.RandomState(1).uniform(0, 1, (n_total, A))
+        else:  # collect_data.py:230-231 arms; theta ~ N(0,1)/sqrt(d)
+            arms = np.random.RandomState(1234).normal(size=(A, 2)) / np.sqrt(2)
+            thetas = np.random.RandomState(2).normal(0, 1, (n_total, 2)) / np.sqrt(2)
+            means_all = np.stack([arms @ t for t in thetas])
+        means = torch.from_numpy(means_all[first:first + count]).cuda()
 
-    def one(step_idx):
-        out = model.rollout_bandit(means, H, args.var, True, seed=1000 + step_idx, first_task=first)
-        if dist is not None:
-            dist.all_gather_into_tensor(gather, out["arm_value"])
-        return out
+        def one(step_idx):
+            out = model.rollout_bandit(means, H, args.var, True, seed=1000 + step_idx, first_task=first)
+            if dist is not None:
+                gather_rows(out["arm_value"], n_total)
+            return out
+
+        env_steps_per_step = n_total * H
+        workload = (f"{A}-arm {'Gaussian' if wl == 'bandit' else 'linear (d=2)'} bandit online eval, DPT sampling "
+                    f"policy in the loop, H={H}, {N} tasks/GPU, var={args.var}, L={L} E=32 1 head")
+        cfg = {"tasks_per_gpu": N, "horizon": H, "arms": A}
+    else:
+        from ctrls.ctrl_darkroom import DarkroomTransformerController
+        from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec
+        from evals import eval_darkroom
+        H, Heps = args.H or 100, 40
+        sd, tmodel = synthetic_state_dict(L, 2, 5, H, seed=0)
+        tmodel.load_state_dict({**sd, "transformer.wte.weight": tmodel.transformer.wte.weight}, strict=True)
+        tmodel.cuda()
+        goals = np.array([(j, i) for j in range(10) for i in range(10)])
+        np.random.RandomState(0).shuffle(goals)   # collect_data.py:408-409 order, cycled to N
+        goals_all = goals[np.arange(n_total) % 100]
+        envs = [DarkroomEnv(10, g, H) for g in goals_all[first:first + count]]
+        vec = DarkroomEnvVec(envs)
+
+        def one(step_idx):
+            np.random.seed(step_idx)
+            ctrl = DarkroomTransformerController(tmodel, batch_size=count, sample=True)
+            ret = eval_darkroom.deploy_online_vec(vec, ctrl, Heps, H, H)
+            if dist is not None:
+                gather_rows(torch.from_numpy(ret).cuda(), n_total)
+            return ret
+
+        env_steps_per_step = n_total * Heps * H
+        workload = f"DarkRoom 10x10 online eval, DPT sampling policy, H=horizon={H}, Heps={Heps}, {N} tasks/GPU"
+        cfg = {"tasks_per_gpu": N, "horizon": H, "episodes": Heps}
 
     for w in range(args.warmup):
         one(w)
@@ -134,10 +187,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record()
-        out = model.rollout_bandit(means, H, args.var, True, seed=2000 + k, first_task=first)
+        one(100 + k)
         ev[k][1].record()
-        if dist is not None:
-            dist.all_gather_into_tensor(gather, out["arm_value"])
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -145,24 +196,33 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        km = torch.tensor([kern_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kern_ms = float(km.item())
+        elapsed, kern_ms = float(t[0]), float(t[1])
 
-    env_steps = world * N * H * args.steps
-    value = env_steps / elapsed
-    abytes = algorithmic_bytes(N, H, L)
-    achieved = abytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_rollout_bandit.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    value = env_steps_per_step * args.steps / elapsed
+    if wl in ("bandit", "linear"):
+        # the timed span per step is the rollout launch (+ the gather for N>1): for N=1 the
+        # events bracket exactly the one rollout_bandit_kernel launch on the current stream
+        abytes = algorithmic_bytes(count, H, L)
+        achieved = abytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_rollout_bandit.json")
+        if wl == "bandit" and os.path.exists(pmc):
+            p = json.load(open(pmc))
+            if p.get("algorithmic_bytes_per_launch") == abytes:
+                traffic = p.get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "rollout_bandit_kernel",
+                "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": abytes}
+    else:
+        F = 2 * 2 + 5 + 1
+        flops = count * H * (window_flops(1, L, F, 5) + (Heps - 1) * window_flops(1 + H, L, F, 5))
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                "frac": achieved / FP32_MFMA_PEAK_TF, "traffic": None,
+                "kernel": "window_decode_kernel (whole step: all launches of one online eval)",
+                "kernel_ms": kern_ms, "algorithmic_flops_per_step": flops}
     line = {
         "metric": "env-steps/sec/GPU (DPT policy in loop), 5-arm bandit H=500, 1/2/4/8 MI355X",
         "value": value,
@@ -175,18 +235,15 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32 (model) / f64 (env, rewards)",
-        "data": "synthetic: seeded GPT-2-init weights (+0.05 N(0,1)), means ~ RandomState(1).U(0,1)",
-        "config": {"workload": f"{A}-arm Gaussian bandit online eval, DPT sampling policy in the loop, "
-                               f"H={H}, {N} tasks/GPU, var={args.var}, L={L} E=32 1 head",
-                   "tasks_per_gpu": N, "horizon": H, "arms": A, "parallelism": f"task-sharded x{world}",
-                   "env_steps_per_step": world * N * H},
+        "data": "synthetic: seeded GPT-2-init weights (+0.05 N(0,1)); tasks per SURVEY.md §8(d)",
+        "config": dict(workload=workload, parallelism=f"task-sharded x{world}",
+                       env_steps_per_step=env_steps_per_step, **cfg),
         "per_gpu_value": value / world,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "rollout_bandit_kernel", "kernel_ms": kern_ms,
-                     "algorithmic_bytes_per_launch": abytes},
+        "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if wl != "bandit":
+        line["metric"] = f"env-steps/sec ({wl} workload; headline metric is --workload bandit)"
+    if rank == 0 and world == 1 and wl == "bandit" and not args.no_cpu_baseline:
         base, kv = cpu_baseline(sd, means_all, H, args.var, L, A)
         line["cpu_baseline"] = base
         line["cpu_baseline_kvcache"] = kv

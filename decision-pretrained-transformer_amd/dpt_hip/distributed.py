@@ -1,0 +1,44 @@
+"""Task sharding over GPUs.
+
+Tasks never interact, so the rollout itself has no collective: each rank runs
+its contiguous block of tasks (Philox keyed by the GLOBAL task id, so results
+do not depend on the number of ranks) and the per-task curves are gathered
+once with ``all_gather_into_tensor`` (RCCL over xGMI with the ``nccl``
+backend; ``gloo`` in CPU tests).  Uneven blocks are padded to the largest.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard(n_total, world, rank):
+    """Contiguous block of tasks for ``rank``: (first_task, count)."""
+    base, rem = divmod(n_total, world)
+    first = rank * base + min(rank, rem)
+    return first, base + (1 if rank < rem else 0)
+
+
+def gather_rows(local, n_total, group=None):
+    """All-gather per-task rows (count, ...) from every rank into (n_total, ...) on every rank."""
+    world = dist.get_world_size(group)
+    counts = [shard(n_total, world, r)[1] for r in range(world)]
+    width = max(counts)
+    pad = torch.zeros((width,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    out = torch.empty((world * width,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "gloo":
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, pad, group=group)
+        out = torch.cat(parts)
+    else:
+        dist.all_gather_into_tensor(out, pad, group=group)
+    return torch.cat([out[r * width: r * width + counts[r]] for r in range(world)])
+
+
+def sharded_online(rollout_fn, means_all, group=None):
+    """Run ``rollout_fn(means_local, first_task) -> dict with 'arm_value' (count, H)`` on this
+    rank's block and gather the (N_total, H) arm-value curves (the regret inputs) everywhere."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    n_total = means_all.shape[0]
+    first, count = shard(n_total, world, rank)
+    out = rollout_fn(means_all[first:first + count], first)
+    return gather_rows(out["arm_value"], n_total, group), out
