@@ -49,6 +49,7 @@ int launch_rollin_darkroom(const int32_t*, const int32_t*, int, int, int, int, c
                            uint64_t, int64_t, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*,
                            hipStream_t);
 int launch_rollout_policy(const dpt_policy_rollout_args&, hipStream_t);
+int set_decode_tile(int);
 
 }  // namespace dpt
 
@@ -89,6 +90,15 @@ extern "C" {
 int dpt_abi_version(void) { return DPT_ABI_VERSION; }
 
 const char* dpt_last_error(void) { return g_last_error.c_str(); }
+
+int dpt_tuning_set(int32_t key, int64_t value) {
+    if (key == DPT_TUNE_DECODE_TILE) {
+        REQUIRE(set_decode_tile((int)value) == DPT_OK, "decode tile %lld: 8 or 16", (long long)value);
+        return DPT_OK;
+    }
+    set_error(DPT_EINVAL, "unknown tuning key %d", key);
+    return DPT_EINVAL;
+}
 
 int dpt_device_count(int* count) {
     REQUIRE(count != nullptr, "null count");

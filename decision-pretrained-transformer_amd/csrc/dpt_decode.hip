@@ -6,79 +6,141 @@
 // causal SDPA, one head -> c_proj -> residual -> ln_2 -> c_fc -> gelu_new ->
 // c_proj -> residual) and ln_f.
 //
-// Work decomposition (one workgroup = one tile of kTile = 16 tasks, 16 waves):
-//  * dense projections (embed excluded): f32 MFMA 16x16x4, tasks are the M
-//    rows, weights [in][out] are the B operand streamed from L2, one 16-column
-//    tile per wave; every weight element is read once per workgroup per step;
+// Work decomposition (one workgroup = one tile of TILE = 8 or 16 tasks, TILE waves;
+// TILE = 8 puts two workgroups on a CU so one streams K/V while the other computes):
+//  * dense projections: f32 MFMA 16x16x4, tasks are the M rows, weights
+//    [in][out] are the B operand streamed from L2 (every weight element is
+//    read once per workgroup per step); c_fc is computed transposed so its
+//    accumulator feeds mlp.c_proj as the A operand with no LDS round trip;
 //  * attention: one wave per task streams that task's K/V rows for positions
 //    0..pos-1 from HBM (8 positions x 128 B per float4 wave-load = 1 KiB
 //    coalesced), online softmax per lane-group of 8, combined across the 8
 //    groups by a 3-step butterfly; the new position's K/V come from LDS;
 //  * LayerNorm / gelu / residual: one half-wave per task in LDS.
-// The rollout kernel keeps a tile resident for all H steps (tasks never
-// interact, so no inter-workgroup synchronisation exists anywhere).
-#include <stdarg.h>
-#include <stdio.h>
-
-#include <string>
-
+// Small parameters (embedding, LayerNorm, biases, head) and the tile's bandit
+// means live in LDS for the whole launch.  Phases inside one position are
+// separated by LDS-only barriers (lgkmcnt + s_barrier: the K/V stores of the
+// step stay in flight); one full __syncthreads per position orders those
+// stores before the next position reads them.  The rollout kernel keeps a
+// tile resident for all H steps (tasks never interact, so no inter-workgroup
+// synchronisation exists anywhere).
 #include "dpt_common.h"
+
+// DPT_STAMPS (diagnostic build only, libdpt_hip_stamps.so): s_memtime after
+// every barrier of decode_position, accumulated per phase by workgroup 0
+// thread 0 into g_stamps; never part of the shipped library.
+#ifdef DPT_STAMPS
+__device__ unsigned long long g_stamps[64];
+__device__ unsigned long long g_stamp_last;
+#define DPT_STAMP(k)                                                          \
+    do {                                                                      \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                            \
+            unsigned long long t_ = __builtin_amdgcn_s_memtime();             \
+            if (g_stamp_last) g_stamps[(k)] += t_ - g_stamp_last;             \
+            g_stamp_last = t_;                                                \
+        }                                                                     \
+    } while (0)
+#else
+#define DPT_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
 
 namespace dpt {
 
-constexpr int kTile = 16;
-constexpr int kThreads = 1024;            // 16 waves
+constexpr int kM = 16;                    // MFMA rows = task slots in LDS (TILE <= 16 are live)
 constexpr int kLdE = kE + 2;              // padded LDS row strides (conflict-free A reads)
-constexpr int kLdFF = kFF + 2;
 constexpr int kRows = 4;                  // K/V rows (of 8 positions) in flight per wave
+constexpr int kChunks = kFF / 16;         // hidden-unit chunks of the fused c_fc -> mlp.c_proj
 
-struct DecodeSmem {
-    float x[kTile][kE];          // residual stream of the current position
-    float xn[kTile][kLdE];       // LayerNorm output (MFMA A operand)
-    float q[kTile][kE];
-    float kcur[kTile][kE];
-    float vcur[kTile][kE];
-    float o[kTile][kLdE];        // attention output (A operand of c_proj)
-    float h[kTile][kLdFF];       // MLP hidden (A operand of mlp.c_proj)
-    float part[4][kTile][kE];    // split-K partials of mlp.c_proj
-    float logits[kTile][kMaxA];
-    float tok[kTile][kMaxF];     // packed token features of the current position
-    int action[kTile];
-};
-
-__device__ inline floatx4 mfma_tile(const float* A, int lda, const float* __restrict__ B, int ldb,
-                                     int K, int lane) {
-    // C[16x16] = A[16 x K] (LDS) * B[K x 16] (global, column offset folded into B).
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    const int i = lane & 15, kq = lane >> 4;
-    float b[32];
-#pragma unroll 8
-    for (int s = 0; s < K / 4; ++s) b[s] = __ldg(B + (size_t)(4 * s + kq) * ldb + i);
-#pragma unroll 8
-    for (int s = 0; s < K / 4; ++s) {
-        float a = A[i * lda + 4 * s + kq];
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[s], acc, 0, 0, 0);
-    }
-    return acc;
+// barrier for LDS hand-offs only: does not wait for outstanding global stores
+__device__ inline void bar_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// LayerNorm of the tile's residual rows: one half-wave (32 lanes) per task.
-__device__ inline void layer_norm_tile(DecodeSmem& S, const float* __restrict__ g,
-                                       const float* __restrict__ b, int tid) {
-    if (tid < kTile * kE) {
-        const int t = tid >> 5, j = tid & 31;
-        float v = S.x[t][j];
-        float s = v;
-#pragma unroll
-        for (int off = 16; off >= 1; off >>= 1) s += __shfl_xor(s, off, 32);
-        const float mean = s * (1.0f / kE);
-        const float d = v - mean;
-        float s2 = d * d;
-#pragma unroll
-        for (int off = 16; off >= 1; off >>= 1) s2 += __shfl_xor(s2, off, 32);
-        const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
-        S.xn[t][j] = fmaf(d * rstd, g[j], b[j]);
+struct Smem {
+    float x[kM][kE];             // residual stream of the current position
+    float xn[kM][kLdE];          // LayerNorm output (MFMA operand)
+    float q[kM][kE];
+    float kcur[kM][kE];
+    float vcur[kM][kE];
+    float o[kM][kLdE];           // attention output (A operand of c_proj)
+    float part[kChunks][kM][kE]; // mlp.c_proj partial sums, one per 16-unit hidden chunk
+    float logits[kM][kMaxA];
+    float tok[kM][kMaxF];        // packed token features of the current position
+    double draw_u[kM];           // this step's selection uniform (rollout)
+    double draw_g[kM];           // this step's reward normal / Bernoulli uniform (rollout)
+    double means[kM][kMaxA];     // the tile's arm means (rollout)
+};
+static_assert(sizeof(Smem) % 16 == 0, "parameter block must start 16-B aligned");
+
+// Small parameters copied to LDS once per launch (offsets in floats).
+struct PLay {
+    static constexpr int ln1_g = 0, ln1_b = 32, attn_b = 64, proj_b = 160, ln2_g = 192, ln2_b = 224,
+                         fc_b = 256, mp_b = 384, size = 416;
+};
+struct ParamLDS {
+    int emb_w, emb_b, layers, lnf_g, lnf_b, head_w, head_b, total;
+    __host__ __device__ static ParamLDS make(int F, int L, int A) {
+        ParamLDS p;
+        int o = 0;
+        p.emb_w = o; o += F * kE;
+        p.emb_b = o; o += kE;
+        p.layers = o; o += L * PLay::size;
+        p.lnf_g = o; o += kE;
+        p.lnf_b = o; o += kE;
+        p.head_w = o; o += kE * A;
+        p.head_b = o; o += A;
+        p.total = (o + 3) & ~3;
+        return p;
     }
+};
+
+__host__ inline size_t decode_smem_bytes(const ModelView& M) {
+    return sizeof(Smem) + sizeof(float) * (size_t)ParamLDS::make(M.F, M.n_layer, M.A).total;
+}
+
+template <int NT>
+__device__ inline void load_params(float* P, const ParamLDS& pl, const ModelView& M) {
+    const int tid = threadIdx.x;
+    for (int i = tid; i < M.F * kE; i += NT) P[pl.emb_w + i] = M.emb_w[i];
+    for (int i = tid; i < kE; i += NT) {
+        P[pl.emb_b + i] = M.emb_b[i];
+        P[pl.lnf_g + i] = M.lnf_g[i];
+        P[pl.lnf_b + i] = M.lnf_b[i];
+    }
+    for (int i = tid; i < M.n_layer * PLay::size; i += NT) {
+        const int l = i / PLay::size, k = i % PLay::size;
+        const float* W = M.layers + (size_t)l * LayerOff::size;
+        float v;
+        if (k < PLay::ln1_b) v = W[LayerOff::ln1_g + k];
+        else if (k < PLay::attn_b) v = W[LayerOff::ln1_b + k - PLay::ln1_b];
+        else if (k < PLay::proj_b) v = W[LayerOff::attn_b + k - PLay::attn_b];
+        else if (k < PLay::ln2_g) v = W[LayerOff::proj_b + k - PLay::proj_b];
+        else if (k < PLay::ln2_b) v = W[LayerOff::ln2_g + k - PLay::ln2_g];
+        else if (k < PLay::fc_b) v = W[LayerOff::ln2_b + k - PLay::ln2_b];
+        else if (k < PLay::mp_b) v = W[LayerOff::fc_b + k - PLay::fc_b];
+        else v = W[LayerOff::mp_b + k - PLay::mp_b];
+        P[pl.layers + i] = v;
+    }
+    for (int i = tid; i < kE * M.A; i += NT) P[pl.head_w + i] = M.head_w[i];
+    for (int i = tid; i < M.A; i += NT) P[pl.head_b + i] = M.head_b[i];
+}
+
+// LayerNorm of one 32-wide row held by the 32 lanes of a half-wave.
+__device__ inline float ln_halfwave(float v, float g, float b) {
+    float s = v;
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) s += __shfl_xor(s, off, 32);
+    const float mean = s * (1.0f / kE);
+    const float d = v - mean;
+    float s2 = d * d;
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) s2 += __shfl_xor(s2, off, 32);
+    const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
+    return fmaf(d * rstd, g, b);
 }
 
 __device__ inline float gelu_new(float x) {
@@ -188,194 +250,302 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
     }
 }
 
-// One decode position for the tile: S.tok -> ... -> S.logits.  K/V of `pos`
-// are appended to the cache.  kv: [2][L][N][max_pos][E].
-__device__ void decode_position(DecodeSmem& S, const ModelView& M, float* __restrict__ kv, int N,
-                                int max_pos, int tile0, int pos) {
+// Per-step Philox draws of a rollout, computed off the critical path by an
+// otherwise idle wave (during the c_proj phase of block 0).
+struct DrawJob {
+    uint64_t seed;
+    int64_t first_task;
+    const double* uniforms;  // (H, N) or null
+    const double* noise;     // (H, N) or null
+    int N, step, sample, bernoulli;
+};
+
+template <int TILE>
+__device__ inline void zero_smem(Smem& S) {
+    float* p = reinterpret_cast<float*>(&S);
+    for (int i = threadIdx.x; i < (int)(sizeof(Smem) / sizeof(float)); i += TILE * kWave) p[i] = 0.f;
+}
+
+// One decode position for a tile of TILE tasks: S.tok -> S.logits, appending
+// K/V of `pos` to the cache kv[2][L][N][max_pos][E].  Per layer:
+//   c_attn (MFMA) | attention (wave per task) | c_proj + residual + ln_2 (one wave,
+//   in registers) | c_fc -> gelu -> mlp.c_proj (fused, 8 waves, split-K) |
+//   split-K reduce + residual + next LayerNorm (half-wave per task)
+// `wpe_j` is wpe[pos][tid & 31] (prefetched by the caller); P is the LDS
+// parameter block.
+template <int TILE>
+__device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, const ModelView& M,
+                                float* __restrict__ kv, int N, int max_pos, int tile0, int pos, float wpe_j,
+                                const DrawJob* dj) {
+    constexpr int kProjWave = TILE - 1;  // a wave with no c_attn tile (TILE >= 8)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t lstride = (size_t)N * max_pos * kE;            // one layer of K (or V)
     const size_t vhalf = (size_t)M.n_layer * lstride;
+    const int i16 = lane & 15, kq = lane >> 4;
 
-    // embed_transition + wpe (net.py:52-53; GPT2Model inputs_embeds + position_embeds)
-    if (tid < kTile * kE) {
+    // embed_transition + wpe (net.py:52-53; GPT2Model inputs_embeds + position_embeds) + ln_1 of block 0
+    if (tid < TILE * 32) {
         const int t = tid >> 5, j = tid & 31;
         float acc = 0.f;
-        for (int f = 0; f < M.F; ++f) acc = fmaf(S.tok[t][f], M.emb_w[f * kE + j], acc);
-        S.x[t][j] = (acc + M.emb_b[j]) + M.wpe[(size_t)pos * kE + j];
+        for (int f = 0; f < M.F; ++f) acc = fmaf(S.tok[t][f], P[pl.emb_w + f * kE + j], acc);
+        const float x = (acc + P[pl.emb_b + j]) + wpe_j;
+        S.x[t][j] = x;
+        S.xn[t][j] = ln_halfwave(x, P[pl.layers + PLay::ln1_g + j], P[pl.layers + PLay::ln1_b + j]);
     }
-    __syncthreads();
+    bar_lds();
+    DPT_STAMP(0);
 
     for (int li = 0; li < M.n_layer; ++li) {
         const float* W = M.layers + (size_t)li * LayerOff::size;
-        layer_norm_tile(S, W + LayerOff::ln1_g, W + LayerOff::ln1_b, tid);
-        __syncthreads();
+        const float* PL = P + pl.layers + li * PLay::size;
         // c_attn: [16 x 32] x [32 x 96] -> q | k | v, one 16-column tile per wave
         if (wave < 6) {
-            floatx4 acc = mfma_tile(&S.xn[0][0], kLdE, W + LayerOff::attn_w + wave * 16, 3 * kE, kE, lane);
-            const int col = wave * 16 + (lane & 15);
-            const float bias = W[LayerOff::attn_b + col];
+            const float* B = W + LayerOff::attn_w + wave * 16;
+            float w[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) w[s] = __ldg(B + (size_t)(4 * s + kq) * 3 * kE + i16);
+            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(S.xn[i16][4 * s + kq], w[s], acc, 0, 0, 0);
+            const int col = wave * 16 + i16;
+            const float bias = PL[PLay::attn_b + col];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int t = (lane >> 4) * 4 + r;
+                const int t = kq * 4 + r;
                 const float v = acc[r] + bias;
                 const int task = tile0 + t;
-                if (col < kE) {
-                    S.q[t][col] = v;
-                } else if (col < 2 * kE) {
-                    S.kcur[t][col - kE] = v;
-                    if (task < N) kv[li * lstride + ((size_t)task * max_pos + pos) * kE + col - kE] = v;
-                } else {
-                    S.vcur[t][col - 2 * kE] = v;
-                    if (task < N)
-                        kv[vhalf + li * lstride + ((size_t)task * max_pos + pos) * kE + col - 2 * kE] = v;
+                if (t < TILE) {
+                    if (col < kE) {
+                        S.q[t][col] = v;
+                    } else if (col < 2 * kE) {
+                        S.kcur[t][col - kE] = v;
+                        if (task < N) kv[li * lstride + ((size_t)task * max_pos + pos) * kE + col - kE] = v;
+                    } else {
+                        S.vcur[t][col - 2 * kE] = v;
+                        if (task < N)
+                            kv[vhalf + li * lstride + ((size_t)task * max_pos + pos) * kE + col - 2 * kE] = v;
+                    }
                 }
             }
         }
-        __syncthreads();
+        bar_lds();
+        DPT_STAMP(1);
         // causal self-attention, one wave per task
-        {
-            const int t = wave;
-            const int task = tile0 + t;
+        if (wave < TILE) {
+            const int task = tile0 + wave;
             if (task < N) {
                 const float* kc = kv + li * lstride + (size_t)task * max_pos * kE;
                 const float* vc = kv + vhalf + li * lstride + (size_t)task * max_pos * kE;
-                attend_one(kc, vc, pos, S.q[t], S.kcur[t], S.vcur[t], S.o[t], lane);
+                attend_one(kc, vc, pos, S.q[wave], S.kcur[wave], S.vcur[wave], S.o[wave], lane);
             }
         }
-        __syncthreads();
-        // c_proj + residual
-        if (wave < 2) {
-            floatx4 acc = mfma_tile(&S.o[0][0], kLdE, W + LayerOff::proj_w + wave * 16, kE, kE, lane);
-            const int col = wave * 16 + (lane & 15);
-            const float bias = W[LayerOff::proj_b + col];
+        bar_lds();
+        DPT_STAMP(2);
+        // c_proj + residual + ln_2, one wave: both 16-column tiles, rows reduced over 16 lanes
+        if (wave == kProjWave) {
+            const float* B = W + LayerOff::proj_w;
+            float w0[8], w1[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                w0[s] = __ldg(B + (size_t)(4 * s + kq) * kE + i16);
+                w1[s] = __ldg(B + (size_t)(4 * s + kq) * kE + 16 + i16);
+            }
+            floatx4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const float a = S.o[i16][4 * s + kq];
+                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w0[s], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w1[s], a1, 0, 0, 0);
+            }
+            const int c0 = i16, c1 = 16 + i16;
+            const float b0 = PL[PLay::proj_b + c0], b1 = PL[PLay::proj_b + c1];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int t = (lane >> 4) * 4 + r;
-                S.x[t][col] = (acc[r] + bias) + S.x[t][col];
+                const int t = kq * 4 + r;
+                const float x0 = (a0[r] + b0) + S.x[t][c0];
+                const float x1 = (a1[r] + b1) + S.x[t][c1];
+                float s = x0 + x1;
+#pragma unroll
+                for (int off = 1; off <= 8; off <<= 1) s += __shfl_xor(s, off);
+                const float mean = s * (1.0f / kE);
+                const float d0 = x0 - mean, d1 = x1 - mean;
+                float s2 = d0 * d0 + d1 * d1;
+#pragma unroll
+                for (int off = 1; off <= 8; off <<= 1) s2 += __shfl_xor(s2, off);
+                const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
+                if (t < TILE) {
+                    S.x[t][c0] = x0;
+                    S.x[t][c1] = x1;
+                    S.xn[t][c0] = fmaf(d0 * rstd, PL[PLay::ln2_g + c0], PL[PLay::ln2_b + c0]);
+                    S.xn[t][c1] = fmaf(d1 * rstd, PL[PLay::ln2_g + c1], PL[PLay::ln2_b + c1]);
+                }
+            }
+        } else if (li == 0 && dj && wave == 0 && lane < TILE) {
+            // this step's draws (select uniform, reward normal / Bernoulli uniform)
+            const int task = tile0 + lane;
+            if (task < dj->N) {
+                const int64_t gtask = dj->first_task + task;
+                if (dj->sample)
+                    S.draw_u[lane] = dj->uniforms ? dj->uniforms[(size_t)dj->step * dj->N + task]
+                                                  : philox_uniform(dj->seed, dj->step, gtask, DPT_STREAM_SELECT);
+                S.draw_g[lane] = dj->noise ? dj->noise[(size_t)dj->step * dj->N + task]
+                                 : dj->bernoulli ? philox_uniform(dj->seed, dj->step, gtask, DPT_STREAM_REWARD)
+                                                 : philox_normal(dj->seed, dj->step, gtask, DPT_STREAM_REWARD);
             }
         }
-        __syncthreads();
-        layer_norm_tile(S, W + LayerOff::ln2_g, W + LayerOff::ln2_b, tid);
-        __syncthreads();
-        // c_fc + gelu_new
-        if (wave < 8) {
-            floatx4 acc = mfma_tile(&S.xn[0][0], kLdE, W + LayerOff::fc_w + wave * 16, kFF, kE, lane);
-            const int col = wave * 16 + (lane & 15);
-            const float bias = W[LayerOff::fc_b + col];
+        bar_lds();
+        DPT_STAMP(3);
+        // c_fc (computed transposed: hidden units on the MFMA rows) -> gelu_new -> mlp.c_proj
+        // partial over this wave's 16 hidden units; the accumulator is the A operand
+        // of the second product directly (k order permuted, matched on the B side).
+        if (wave < kChunks) {
+            const float* W1 = W + LayerOff::fc_w + wave * 16;                          // [E][FF]
+            const float* W2 = W + LayerOff::mp_w + (size_t)(wave * 16 + kq * 4) * kE;  // this lane group's rows
+            float w1[8], w2a[4], w2b[4];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) w1[s] = __ldg(W1 + (size_t)(4 * s + kq) * kFF + i16);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                w2a[s] = __ldg(W2 + (size_t)s * kE + i16);
+                w2b[s] = __ldg(W2 + (size_t)s * kE + 16 + i16);
+            }
+            floatx4 ht = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                ht = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[s], S.xn[i16][4 * s + kq], ht, 0, 0, 0);
+            // ht[r] = h^T[unit 16*wave + 4*kq + r][task i16]
+            floatx4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const float hv = gelu_new(ht[s] + PL[PLay::fc_b + wave * 16 + kq * 4 + s]);
+                p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2a[s], p0, 0, 0, 0);
+                p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2b[s], p1, 0, 0, 0);
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int t = (lane >> 4) * 4 + r;
-                S.h[t][col] = gelu_new(acc[r] + bias);
+                S.part[wave][kq * 4 + r][i16] = p0[r];
+                S.part[wave][kq * 4 + r][16 + i16] = p1[r];
             }
         }
-        __syncthreads();
-        // mlp.c_proj: K = 128 split four ways over waves, partials reduced in order
-        if (wave < 8) {
-            const int ct = wave & 1, kc4 = wave >> 1;
-            floatx4 acc = mfma_tile(&S.h[0][kc4 * 32], kLdFF,
-                                    W + LayerOff::mp_w + (size_t)kc4 * 32 * kE + ct * 16, kE, 32, lane);
-            const int col = ct * 16 + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) S.part[kc4][(lane >> 4) * 4 + r][col] = acc[r];
-        }
-        __syncthreads();
-        if (tid < kTile * kE) {
+        bar_lds();
+        DPT_STAMP(4);
+        // reduce the 8 partials in a fixed tree + bias + residual, then the next LayerNorm
+        if (tid < TILE * 32) {
             const int t = tid >> 5, j = tid & 31;
-            const float ff = ((S.part[0][t][j] + S.part[1][t][j]) + (S.part[2][t][j] + S.part[3][t][j]));
-            S.x[t][j] = S.x[t][j] + (ff + W[LayerOff::mp_b + j]);
+            const float ff = ((S.part[0][t][j] + S.part[1][t][j]) + (S.part[2][t][j] + S.part[3][t][j])) +
+                             ((S.part[4][t][j] + S.part[5][t][j]) + (S.part[6][t][j] + S.part[7][t][j]));
+            const float x = S.x[t][j] + (ff + PL[PLay::mp_b + j]);
+            S.x[t][j] = x;
+            const bool last = li + 1 == M.n_layer;
+            const float g = last ? P[pl.lnf_g + j] : PL[PLay::size + PLay::ln1_g + j];
+            const float b = last ? P[pl.lnf_b + j] : PL[PLay::size + PLay::ln1_b + j];
+            S.xn[t][j] = ln_halfwave(x, g, b);
         }
-        __syncthreads();
+        bar_lds();
+        DPT_STAMP(5);
     }
-    layer_norm_tile(S, M.lnf_g, M.lnf_b, tid);
-    __syncthreads();
-    // pred_actions head: [16 x 32] x [32 x A]
+    // pred_actions head: [16 x 32] x [32 x A] (weights in LDS)
     const int ntile = (M.A + 15) >> 4;
     if (wave < ntile) {
-        // head_w is [E][A]; columns beyond A read a clamped column and are discarded
-        const int i = lane & 15, kq = lane >> 4;
-        const int col = wave * 16 + i;
-        const int colc = col < M.A ? col : M.A - 1;
+        const int col = wave * 16 + i16;
+        const int colc = col < M.A ? col : M.A - 1;  // columns beyond A are computed and discarded
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < kE / 4; ++s) {
-            float a = S.xn[i][4 * s + kq];
-            float b = M.head_w[(4 * s + kq) * M.A + colc];
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-        }
+        for (int s = 0; s < kE / 4; ++s)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(S.xn[i16][4 * s + kq], P[pl.head_w + (4 * s + kq) * M.A + colc],
+                                                       acc, 0, 0, 0);
         if (col < M.A) {
-            const float bias = M.head_b[col];
+            const float bias = P[pl.head_b + col];
 #pragma unroll
             for (int r = 0; r < 4; ++r) S.logits[kq * 4 + r][col] = acc[r] + bias;
         }
     }
-    __syncthreads();
+    bar_lds();
+    DPT_STAMP(6);
 }
+
+// dynamic LDS: Smem followed by the parameter block
+#define DPT_SMEM_SETUP(TILE_)                                                   \
+    extern __shared__ __align__(16) unsigned char smem_raw[];                   \
+    Smem& S = *reinterpret_cast<Smem*>(smem_raw);                               \
+    float* P = reinterpret_cast<float*>(smem_raw + sizeof(Smem));               \
+    const ParamLDS pl = ParamLDS::make(M.F, M.n_layer, M.A);                    \
+    zero_smem<TILE_>(S);                                                        \
+    load_params<TILE_ * 64>(P, pl, M);                                          \
+    __syncthreads();
 
 // ----------------------------------------------------------------------------- kernels
 
 // One decode position for all tasks; tokens (N, F) given.
-__global__ __launch_bounds__(kThreads) void decode_step_kernel(ModelView M, float* kv, int N, int max_pos,
-                                                               int pos, const float* __restrict__ token,
-                                                               float* __restrict__ logits) {
-    __shared__ DecodeSmem S;
-    const int tile0 = blockIdx.x * kTile;
+template <int TILE>
+__global__ __launch_bounds__(TILE * 64, 4) void decode_step_kernel(ModelView M, float* kv, int N, int max_pos,
+                                                                   int pos, const float* __restrict__ token,
+                                                                   float* __restrict__ logits) {
+    DPT_SMEM_SETUP(TILE)
+    const int tile0 = blockIdx.x * TILE;
     const int tid = threadIdx.x;
-    for (int i = tid; i < kTile * kMaxF; i += kThreads) {
+    for (int i = tid; i < TILE * kMaxF; i += TILE * 64) {
         const int t = i / kMaxF, f = i % kMaxF;
         S.tok[t][f] = (tile0 + t < N && f < M.F) ? token[(size_t)(tile0 + t) * M.F + f] : 0.f;
     }
+    const float wpe_j = M.wpe[(size_t)pos * kE + (tid & 31)];
     __syncthreads();
-    decode_position(S, M, kv, N, max_pos, tile0, pos);
-    for (int i = tid; i < kTile * M.A; i += kThreads) {
+    decode_position<TILE>(S, P, pl, M, kv, N, max_pos, tile0, pos, wpe_j, nullptr);
+    for (int i = tid; i < TILE * M.A; i += TILE * 64) {
         const int t = i / M.A, a = i % M.A;
         if (tile0 + t < N) logits[(size_t)(tile0 + t) * M.A + a] = S.logits[t][a];
     }
 }
 
 // Teacher-forced window forward (= Transformer.forward over query + C context
-// rows): positions 0..C decoded in order through the workspace cache.
-__global__ __launch_bounds__(kThreads) void window_decode_kernel(
+// rows): positions 0..C decoded in order through the workspace cache; the next
+// position's token features and wpe row are prefetched into registers.
+template <int TILE>
+__global__ __launch_bounds__(TILE * 64, 4) void window_decode_kernel(
     ModelView M, float* kv, int N, int C, const float* __restrict__ query, const float* __restrict__ cs,
     const float* __restrict__ ca, const float* __restrict__ cn, const float* __restrict__ cr, int out_mode,
     float* __restrict__ out) {
-    __shared__ DecodeSmem S;
-    const int tile0 = blockIdx.x * kTile;
+    DPT_SMEM_SETUP(TILE)
+    const int tile0 = blockIdx.x * TILE;
     const int tid = threadIdx.x;
     const int sd = M.sd, A = M.A;
     const int T = C + 1;
+    // this thread's token element: t = tid / kMaxF, f = tid % kMaxF (TILE * kMaxF == TILE * 64 threads)
+    const int tt = tid / kMaxF, ff = tid % kMaxF;
+    const int ttask = tile0 + tt;
+    auto token_elem = [&](int pos) -> float {
+        if (ttask >= N || ff >= M.F) return 0.f;
+        if (pos == 0) return (ff < sd) ? query[(size_t)ttask * sd + ff] : 0.f;
+        const size_t row = (size_t)ttask * C + (pos - 1);
+        if (ff < sd) return cs[row * sd + ff];
+        if (ff < sd + A) return ca[row * A + (ff - sd)];
+        if (ff < 2 * sd + A) return cn[row * sd + (ff - sd - A)];
+        return cr[row];
+    };
+    float tok_next = token_elem(0);
+    float wpe_next = M.wpe[tid & 31];
     for (int pos = 0; pos < T; ++pos) {
-        // token packing (models/net.py:42-51)
-        for (int i = tid; i < kTile * kMaxF; i += kThreads) {
-            const int t = i / kMaxF, f = i % kMaxF;
-            const int task = tile0 + t;
-            float v = 0.f;
-            if (task < N && f < M.F) {
-                if (pos == 0) {
-                    v = (f < sd) ? query[(size_t)task * sd + f] : 0.f;
-                } else {
-                    const size_t row = (size_t)task * C + (pos - 1);
-                    if (f < sd) v = cs[row * sd + f];
-                    else if (f < sd + A) v = ca[row * A + (f - sd)];
-                    else if (f < 2 * sd + A) v = cn[row * sd + (f - sd - A)];
-                    else v = cr[row];
-                }
-            }
-            S.tok[t][f] = v;
+        S.tok[tt][ff] = tok_next;  // packing (models/net.py:42-51)
+        const float wpe_j = wpe_next;
+        if (pos + 1 < T) {
+            tok_next = token_elem(pos + 1);
+            wpe_next = M.wpe[(size_t)(pos + 1) * kE + (tid & 31)];
         }
-        __syncthreads();
-        decode_position(S, M, kv, N, T, tile0, pos);
+        bar_lds();
+        decode_position<TILE>(S, P, pl, M, kv, N, T, tile0, pos, wpe_j, nullptr);
         if (out_mode == 0 && pos == C) {
-            for (int i = tid; i < kTile * A; i += kThreads) {
+            for (int i = tid; i < TILE * A; i += TILE * 64) {
                 const int t = i / A, a = i % A;
                 if (tile0 + t < N) out[(size_t)(tile0 + t) * A + a] = S.logits[t][a];
             }
         } else if (out_mode == 1 && pos >= 1) {
-            for (int i = tid; i < kTile * A; i += kThreads) {
+            for (int i = tid; i < TILE * A; i += TILE * 64) {
                 const int t = i / A, a = i % A;
                 if (tile0 + t < N) out[((size_t)(tile0 + t) * C + (pos - 1)) * A + a] = S.logits[t][a];
             }
         }
-        __syncthreads();
+        __syncthreads();  // K/V stores of `pos` visible before position pos+1 reads them
     }
 }
 
@@ -396,44 +566,38 @@ struct BanditRolloutParams {
 
 // The bandit online loop (evals/eval_bandit.py:70-89) for one tile of tasks,
 // all H steps: decode -> select -> env step -> append transition.
-__global__ __launch_bounds__(kThreads) void rollout_bandit_kernel(ModelView M, BanditRolloutParams P) {
-    __shared__ DecodeSmem S;
-    const int tile0 = blockIdx.x * kTile;
+template <int TILE>
+__global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView M, BanditRolloutParams Pr) {
+    DPT_SMEM_SETUP(TILE)
+    const int tile0 = blockIdx.x * TILE;
     const int tid = threadIdx.x;
-    const int A = P.A;
-    // position 0: the query token [state=1, 0_A, 0, 0] (BanditEnv.state = [1], ctrl_bandit.py:426)
-    for (int i = tid; i < kTile * kMaxF; i += kThreads) {
-        const int t = i / kMaxF, f = i % kMaxF;
-        S.tok[t][f] = (f == 0) ? 1.f : 0.f;
+    const int A = Pr.A;
+    for (int i = tid; i < TILE * A; i += TILE * 64) {
+        const int t = i / A, k = i % A;
+        S.means[t][k] = (tile0 + t < Pr.N) ? Pr.means[(size_t)(tile0 + t) * A + k] : 0.0;
     }
+    // position 0: the query token [state=1, 0_A, 0, 0] (BanditEnv.state = [1], ctrl_bandit.py:426)
+    if (tid < TILE) S.tok[tid][0] = 1.f;
+    DrawJob dj{Pr.seed, Pr.first_task, Pr.uniforms, Pr.noise, Pr.N, 0, Pr.sample, Pr.type == DPT_BANDIT_BERNOULLI};
+    float wpe_next = M.wpe[tid & 31];
     __syncthreads();
-    for (int h = 0; h < P.H; ++h) {
-        decode_position(S, M, P.kv, P.N, P.H, tile0, h);
-        if (tid < kTile) {
+    for (int h = 0; h < Pr.H; ++h) {
+        const float wpe_j = wpe_next;
+        if (h + 1 < Pr.H) wpe_next = M.wpe[(size_t)(h + 1) * kE + (tid & 31)];
+        dj.step = h;
+        decode_position<TILE>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, &dj);
+        if (tid < TILE) {
             const int t = tid, task = tile0 + t;
-            if (task < P.N) {
-                const int64_t gtask = P.first_task + task;
-                double u = 0.0;
-                if (P.sample)
-                    u = P.uniforms ? P.uniforms[(size_t)h * P.N + task]
-                                   : philox_uniform(P.seed, h, gtask, DPT_STREAM_SELECT);
-                const int a = select_from_logits(S.logits[t], A, P.sample, 1.0f, u);
-                const double mean = P.means[(size_t)task * A + a];
-                double r;
-                if (P.type == DPT_BANDIT_BERNOULLI) {
-                    const double ur = P.noise ? P.noise[(size_t)h * P.N + task]
-                                              : philox_uniform(P.seed, h, gtask, DPT_STREAM_REWARD);
-                    r = (ur < mean) ? 1.0 : 0.0;
-                } else {
-                    const double g = P.noise ? P.noise[(size_t)h * P.N + task]
-                                             : philox_normal(P.seed, h, gtask, DPT_STREAM_REWARD);
-                    r = gaussian_reward(mean, P.var, g);
-                }
-                P.actions_out[(size_t)task * P.H + h] = a;
-                P.rewards_out[(size_t)task * P.H + h] = r;
-                P.arm_value_out[(size_t)task * P.H + h] = mean;
-                if (P.logits_out)
-                    for (int k = 0; k < A; ++k) P.logits_out[((size_t)h * P.N + task) * A + k] = S.logits[t][k];
+            if (task < Pr.N) {
+                const int a = select_from_logits(S.logits[t], A, Pr.sample, 1.0f, S.draw_u[t]);
+                const double mean = S.means[t][a];
+                const double r = (Pr.type == DPT_BANDIT_BERNOULLI) ? ((S.draw_g[t] < mean) ? 1.0 : 0.0)
+                                                                  : gaussian_reward(mean, Pr.var, S.draw_g[t]);
+                Pr.actions_out[(size_t)task * Pr.H + h] = a;
+                Pr.rewards_out[(size_t)task * Pr.H + h] = r;
+                Pr.arm_value_out[(size_t)task * Pr.H + h] = mean;
+                if (Pr.logits_out)
+                    for (int k = 0; k < A; ++k) Pr.logits_out[((size_t)h * Pr.N + task) * A + k] = S.logits[t][k];
                 // next token = transition h: [s=1, onehot(a), s'=1, float(r)] (eval_bandit.py:83-86)
                 S.tok[t][0] = 1.f;
                 for (int k = 0; k < A; ++k) S.tok[t][1 + k] = (k == a) ? 1.f : 0.f;
@@ -441,7 +605,8 @@ __global__ __launch_bounds__(kThreads) void rollout_bandit_kernel(ModelView M, B
                 S.tok[t][2 + A] = (float)r;
             }
         }
-        __syncthreads();
+        __syncthreads();  // K/V stores of step h visible before step h+1 reads them
+        DPT_STAMP(7);
     }
 }
 
@@ -473,31 +638,92 @@ int64_t weights_numel(const dpt_model_desc& d) {
            (int64_t)kE * d.action_dim + d.action_dim;
 }
 
+#ifdef DPT_STAMPS
+extern "C" int dpt_debug_stamps(unsigned long long* out, int n, int reset) {
+    if (reset) {
+        unsigned long long z[64] = {0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_last), z, sizeof(unsigned long long));
+        return 0;
+    }
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (n < 64 ? n : 64));
+}
+#endif
+
+static int g_decode_tile = 16;  // tuning knob (dpt_tuning_set(DPT_TUNE_DECODE_TILE, 8|16))
+
+int set_decode_tile(int t) {
+    if (t != 8 && t != 16) return DPT_EINVAL;
+    g_decode_tile = t;
+    return DPT_OK;
+}
+
+// the dynamic-LDS size must fit one CU
+static int check_smem(const ModelView& M, size_t* bytes) {
+    *bytes = decode_smem_bytes(M);
+    if (*bytes > 160 * 1024) {
+        set_error(DPT_EUNSUPPORTED, "decode LDS %zu B > 160 KiB (n_layer=%d, action_dim=%d)", *bytes, M.n_layer, M.A);
+        return DPT_EUNSUPPORTED;
+    }
+    return DPT_OK;
+}
+
+template <int TILE>
+static dim3 tiles(int n) { return dim3((n + TILE - 1) / TILE); }
+
+// dynamic LDS beyond the default 64 KiB must be opted into per kernel
+template <class K>
+static void allow_smem(K kernel, size_t bytes) {
+    if (bytes > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)bytes);
+}
+
 int launch_decode_step(const ModelView& M, float* kv, int N, int max_pos, int pos, const float* token,
                        float* logits, hipStream_t st) {
-    dim3 grid((N + kTile - 1) / kTile);
-    hipLaunchKernelGGL(decode_step_kernel, grid, dim3(kThreads), 0, st, M, kv, N, max_pos, pos, token, logits);
+    size_t sm;
+    if (int rc = check_smem(M, &sm)) return rc;
+    allow_smem(decode_step_kernel<8>, sm);
+    allow_smem(decode_step_kernel<16>, sm);
+    if (g_decode_tile == 8)
+        hipLaunchKernelGGL(decode_step_kernel<8>, tiles<8>(N), dim3(512), sm, st, M, kv, N, max_pos, pos, token, logits);
+    else
+        hipLaunchKernelGGL(decode_step_kernel<16>, tiles<16>(N), dim3(1024), sm, st, M, kv, N, max_pos, pos, token,
+                           logits);
     return check_hip(hipGetLastError(), "decode_step_kernel launch");
 }
 
 int launch_window_decode(const ModelView& M, float* kv, int N, int C, const float* q, const float* cs,
                          const float* ca, const float* cn, const float* cr, int out_mode, float* out,
                          hipStream_t st) {
-    dim3 grid((N + kTile - 1) / kTile);
-    hipLaunchKernelGGL(window_decode_kernel, grid, dim3(kThreads), 0, st, M, kv, N, C, q, cs, ca, cn, cr,
-                       out_mode, out);
+    size_t sm;
+    if (int rc = check_smem(M, &sm)) return rc;
+    allow_smem(window_decode_kernel<8>, sm);
+    allow_smem(window_decode_kernel<16>, sm);
+    if (g_decode_tile == 8)
+        hipLaunchKernelGGL(window_decode_kernel<8>, tiles<8>(N), dim3(512), sm, st, M, kv, N, C, q, cs, ca, cn, cr,
+                           out_mode, out);
+    else
+        hipLaunchKernelGGL(window_decode_kernel<16>, tiles<16>(N), dim3(1024), sm, st, M, kv, N, C, q, cs, ca, cn,
+                           cr, out_mode, out);
     return check_hip(hipGetLastError(), "window_decode_kernel launch");
 }
 
 int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, hipStream_t st) {
+    size_t sm;
+    if (int rc = check_smem(M, &sm)) return rc;
     BanditRolloutParams P;
     P.N = a.N; P.H = a.H; P.A = a.A; P.type = a.type; P.sample = a.sample;
     P.first_task = a.first_task; P.var = a.var; P.seed = a.seed;
     P.means = a.means; P.uniforms = a.uniforms; P.noise = a.noise; P.kv = a.kvcache;
     P.actions_out = a.actions_out; P.rewards_out = a.rewards_out; P.arm_value_out = a.arm_value_out;
     P.logits_out = a.logits_out;
-    dim3 grid((a.N + kTile - 1) / kTile);
-    hipLaunchKernelGGL(rollout_bandit_kernel, grid, dim3(kThreads), 0, st, M, P);
+    allow_smem(rollout_bandit_kernel<8>, sm);
+    allow_smem(rollout_bandit_kernel<16>, sm);
+    if (g_decode_tile == 8)
+        hipLaunchKernelGGL(rollout_bandit_kernel<8>, tiles<8>(a.N), dim3(512), sm, st, M, P);
+    else
+        hipLaunchKernelGGL(rollout_bandit_kernel<16>, tiles<16>(a.N), dim3(1024), sm, st, M, P);
     return check_hip(hipGetLastError(), "rollout_bandit_kernel launch");
 }
 

@@ -297,3 +297,8 @@ def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=Tr
     _lib.call("dpt_rollout_policy", ctypes.byref(args), _stream())
     out["_keep"] = (keep, ws)
     return out
+
+
+def set_decode_tile(tile):
+    """Tasks per workgroup of the decode kernels (8: two workgroups per CU; 16: one)."""
+    _lib.call("dpt_tuning_set", _lib.TUNE_DECODE_TILE, int(tile))

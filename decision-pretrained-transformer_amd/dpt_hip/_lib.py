@@ -143,3 +143,6 @@ SIGNATURES.update({
     "dpt_policy_workspace_numel": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_i64)]),
     "dpt_rollout_policy": (_i32, [ctypes.POINTER(PolicyRolloutArgs), _c_void_p]),
 })
+
+TUNE_DECODE_TILE = 1
+SIGNATURES["dpt_tuning_set"] = (_i32, [_i32, _i64])

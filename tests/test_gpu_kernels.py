@@ -211,3 +211,26 @@ def test_rollout_large_properties():
     # partial tile (N not a multiple of 16) behaves like the full run on its prefix
     o3 = m.rollout_bandit(means[:1000], H, 0.3, True, seed=42)
     assert np.array_equal(o3["actions"].cpu().numpy(), a[:1000])
+
+
+def test_decode_tiles_bit_identical():
+    """TILE 8 (two workgroups per CU) and TILE 16 give bit-identical rollouts and windows."""
+    import dpt_hip
+    _, m, _ = model_from_golden("bandit5")
+    rs = np.random.RandomState(9)
+    means = rs.uniform(0, 1, (100, 5))
+    outs = []
+    g, mw, _ = model_from_golden("darkroom")
+    q, cs, ca, cn, cr = (g[f"T101/{k}"] for k in ("query", "cs", "ca", "cn", "cr"))
+    try:
+        for tile in (16, 8):
+            dpt_hip.set_decode_tile(tile)
+            o = m.rollout_bandit(means, 40, 0.3, True, seed=5, want_logits=True)
+            w = mw.forward_window(q, cs, ca, cn, cr, out_mode=1)
+            outs.append([o["actions"].cpu().numpy(), o["rewards"].cpu().numpy(), o["logits"].cpu().numpy(),
+                         w.cpu().numpy()])
+    finally:
+        dpt_hip.set_decode_tile(16)
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    assert_logits(outs[1][3], g["T101/preds_train"])
