@@ -221,7 +221,7 @@ def main():
         achieved = flops / (kern_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                 "frac": achieved / FP32_MFMA_PEAK_TF, "traffic": None,
-                "kernel": "window_decode_kernel (whole step: all launches of one online eval)",
+                "kernel": "rollout_darkroom_kernel (one launch = one whole online eval)",
                 "kernel_ms": kern_ms, "algorithmic_flops_per_step": flops}
     line = {
         "metric": "env-steps/sec/GPU (DPT policy in loop), 5-arm bandit H=500, 1/2/4/8 MI355X",

@@ -49,6 +49,10 @@ int launch_rollin_darkroom(const int32_t*, const int32_t*, int, int, int, int, c
                            uint64_t, int64_t, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*,
                            hipStream_t);
 int launch_rollout_policy(const dpt_policy_rollout_args&, hipStream_t);
+int launch_pack_fragments(const ModelView&, float*, hipStream_t);
+int64_t fragments_numel(int n_layer);
+int launch_rollout_darkroom(const ModelView&, const float*, const dpt_darkroom_rollout_args&, hipStream_t);
+int darkroom_max_window();
 int set_decode_tile(int);
 
 }  // namespace dpt
@@ -58,6 +62,7 @@ using namespace dpt;
 struct dpt_model {
     dpt_model_desc desc;
     float* blob;
+    float* frag;  // the blocks' weights in MFMA fragment order (dpt_darkroom.hip FragOff)
     ModelView view;
 };
 
@@ -131,10 +136,26 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
         (void)hipFree(blob);
         return rc;
     }
+    const ModelView view = make_view(blob, *d);
+    float* frag = nullptr;
+    const size_t frag_bytes = (size_t)fragments_numel(d->n_layer) * sizeof(float);
+    if (hipMalloc(&frag, frag_bytes) != hipSuccess) {
+        (void)hipFree(blob);
+        set_error(DPT_ENOMEM, "hipMalloc(%zu) for the fragment-packed weights failed", frag_bytes);
+        return DPT_ENOMEM;
+    }
+    rc = launch_pack_fragments(view, frag, nullptr);
+    if (!rc) rc = check_hip(hipDeviceSynchronize(), "fragment packing");
+    if (rc) {
+        (void)hipFree(blob);
+        (void)hipFree(frag);
+        return rc;
+    }
     dpt_model* m = new dpt_model;
     m->desc = *d;
     m->blob = blob;
-    m->view = make_view(blob, *d);
+    m->frag = frag;
+    m->view = view;
     *out = m;
     return DPT_OK;
 }
@@ -142,7 +163,9 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
 int dpt_model_free(dpt_model* m) {
     if (!m) return DPT_OK;
     int rc = check_hip(hipFree(m->blob), "hipFree weight blob");
+    const int rc2 = check_hip(hipFree(m->frag), "hipFree fragment weights");
     delete m;
+    if (!rc) rc = rc2;
     return rc;
 }
 
@@ -282,6 +305,24 @@ int dpt_rollout_bandit(const dpt_model* m, const dpt_bandit_rollout_args* a, voi
         return DPT_EUNSUPPORTED;
     }
     return launch_rollout_bandit(m->view, *a, S(stream));
+}
+
+int dpt_rollout_darkroom(const dpt_model* m, const dpt_darkroom_rollout_args* a, void* stream) {
+    REQUIRE(m && a, "null model/args");
+    REQUIRE(a->N >= 1 && a->Heps >= 1 && a->horizon >= 1 && a->ctx_episodes >= 1,
+            "N=%d Heps=%d horizon=%d ctx_episodes=%d", a->N, a->Heps, a->horizon, a->ctx_episodes);
+    REQUIRE(a->dim >= 1 && a->dim <= 255, "dim=%d", a->dim);
+    REQUIRE(a->goals && a->returns_out, "null goals/returns_out");
+    REQUIRE(!a->sample || a->temp > 0.0f, "temp=%g", (double)a->temp);
+    const int64_t window = 1 + (int64_t)a->ctx_episodes * a->horizon;
+    REQUIRE(window <= m->desc.n_positions, "window %lld exceeds n_positions=%d", (long long)window,
+            m->desc.n_positions);
+    if (m->desc.state_dim != 2 || m->desc.action_dim != 5 || window > darkroom_max_window()) {
+        set_error(DPT_EUNSUPPORTED, "fused darkroom rollout needs sd=2, A=5, window<=%d (sd=%d A=%d window=%lld)",
+                  darkroom_max_window(), m->desc.state_dim, m->desc.action_dim, (long long)window);
+        return DPT_EUNSUPPORTED;
+    }
+    return launch_rollout_darkroom(m->view, m->frag, *a, S(stream));
 }
 
 }  // extern "C"

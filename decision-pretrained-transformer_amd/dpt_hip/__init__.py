@@ -164,6 +164,33 @@ class DeviceModel:
         out["_keep"] = (kv, means_d, u_d, g_d)
         return out
 
+    def rollout_darkroom(self, goals, Heps, horizon, ctx_episodes, dim=10, perms=None, sample=True, temp=1.0,
+                         seed=0, counter=0, first_task=0, uniforms=None, want_actions=False, want_logits=False):
+        """Fused DarkRoom online evaluation (evals/eval_darkroom.py:20-84) on device.
+
+        Returns dict of device tensors: returns (N, Heps) int32, actions (N, Heps*horizon)
+        int32 and logits (Heps*horizon, N, 5) f32 if requested.  Raises
+        NotImplementedError outside sd=2 / A=5 / window <= 128 (use the per-step path).
+        """
+        dev = device()
+        goals_d = _dev(goals, torch.int32, dev).contiguous()
+        N = goals_d.shape[0]
+        steps = int(Heps) * int(horizon)
+        perms_d = None if perms is None else _dev(perms, torch.int32, dev).contiguous()
+        u_d = None if uniforms is None else _dev(uniforms, torch.float64, dev).contiguous()
+        out = dict(returns=torch.empty((N, int(Heps)), dtype=torch.int32, device=dev))
+        out["actions"] = torch.empty((N, steps), dtype=torch.int32, device=dev) if want_actions else None
+        out["logits"] = torch.empty((steps, N, 5), dtype=torch.float32, device=dev) if want_logits else None
+        args = _lib.DarkroomRolloutArgs(
+            N, int(Heps), int(horizon), int(ctx_episodes), int(dim), int(bool(sample)), int(first_task),
+            int(seed) & (2 ** 64 - 1), int(counter), float(temp), 0, _p(goals_d).value,
+            None if perms_d is None else _p(perms_d).value, None if u_d is None else _p(u_d).value,
+            _p(out["returns"]).value, None if out["actions"] is None else _p(out["actions"]).value,
+            None if out["logits"] is None else _p(out["logits"]).value)
+        _lib.call("dpt_rollout_darkroom", self._h, ctypes.byref(args), _stream())
+        out["_keep"] = (goals_d, perms_d, u_d)
+        return out
+
 
 # ----------------------------------------------------------------------------- element-wise ops
 

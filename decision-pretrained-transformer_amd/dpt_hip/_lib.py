@@ -146,3 +146,13 @@ SIGNATURES.update({
 
 TUNE_DECODE_TILE = 1
 SIGNATURES["dpt_tuning_set"] = (_i32, [_i32, _i64])
+
+
+class DarkroomRolloutArgs(ctypes.Structure):
+    _fields_ = [("N", _i32), ("Heps", _i32), ("horizon", _i32), ("ctx_episodes", _i32), ("dim", _i32),
+                ("sample", _i32), ("first_task", _i64), ("seed", _u64), ("counter", _u64), ("temp", _f32),
+                ("reserved0", _i32), ("goals", _c_void_p), ("perms", _c_void_p), ("uniforms", _c_void_p),
+                ("returns_out", _c_void_p), ("actions_out", _c_void_p), ("logits_out", _c_void_p)]
+
+
+SIGNATURES["dpt_rollout_darkroom"] = (_i32, [_c_void_p, ctypes.POINTER(DarkroomRolloutArgs), _c_void_p])

@@ -1,8 +1,9 @@
 """DarkRoom evaluation — drop-in for the reference evals/eval_darkroom.py.
 
 ``deploy_online_vec`` (evals/eval_darkroom.py:20-84): with the DPT controller
-over this package's ``Transformer`` and a ``DarkroomEnvVec`` the loop never
-leaves the device — per step one window forward (gfx950 kernel) over the fixed
+over this package's ``Transformer`` and a ``DarkroomEnvVec`` the whole loop is
+one fused kernel launch (dpt_rollout_darkroom) when the window fits (1 + H <=
+128); otherwise it stays on the device step by step — per step one window forward (gfx950 kernel) over the fixed
 in-context episodes with the current state as query, device sampling, the
 integer grid step kernel, and an on-device append into the episode buffers;
 returns are summed on device and copied once at the end.  Other controllers
@@ -45,8 +46,39 @@ def _episode_device(dm, ctrl, vec_env, ctx, horizon):
     return es, ea, ns, er
 
 
-def deploy_online_vec(vec_env, controller, Heps, H, horizon):
+_FUSED_MAX_WINDOW = 128  # dpt_rollout_darkroom: 1 + H tokens per forward
+
+
+def _fused_ok(vec_env, controller, H):
+    return (_device_ok(vec_env, controller) and vec_env.state_dim == 2 and vec_env.action_dim == 5
+            and 1 + H <= _FUSED_MAX_WINDOW and vec_env.dim <= 255)
+
+
+def rollout_fused(vec_env, controller, Heps, H, horizon, want_actions=False, want_logits=False):
+    """The whole deploy_online_vec loop as one dpt_rollout_darkroom launch.
+
+    Selection draws are the controller's own stream: the counters this loop
+    would consume step by step (one per select) are consumed here in one go,
+    so the fused and per-step paths act identically on the same draws.
+    """
+    dm = controller.model.device_model()
+    steps = Heps * horizon
+    seed, ctr0 = controller._stream.next()
+    controller._stream.counter = ctr0 + steps
+    u = None
+    if controller.sample and controller.uniforms is not None:
+        u = torch.stack([torch.as_tensor(controller.uniforms(ctr0 + k), dtype=torch.float64).reshape(-1)
+                         for k in range(steps)])
+    return dm.rollout_darkroom(vec_env.goals_device, Heps, horizon, H // horizon, dim=vec_env.dim,
+                               perms=vec_env.perms_device, sample=controller.sample, temp=controller.temp,
+                               seed=seed, counter=ctr0, uniforms=u, want_actions=want_actions,
+                               want_logits=want_logits)
+
+
+def deploy_online_vec(vec_env, controller, Heps, H, horizon, fused=True):
     assert H % horizon == 0
+    if fused and _fused_ok(vec_env, controller, H):
+        return rollout_fused(vec_env, controller, Heps, H, horizon)["returns"].to(torch.int64).cpu().numpy()
     ctx_rollouts = H // horizon
     num_envs = vec_env.num_envs
     dev = dpt_hip.device()

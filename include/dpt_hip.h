@@ -263,6 +263,36 @@ typedef struct dpt_policy_rollout_args {
 int dpt_policy_workspace_numel(int32_t N, int32_t A, int32_t H, int64_t* numel_out_host);
 int dpt_rollout_policy(const dpt_policy_rollout_args* args_host, void* stream);
 
+/* DarkRoom in-context online evaluation, one launch: replaces
+ * evals/eval_darkroom.py:20-84 deploy_online_vec with
+ * DarkroomTransformerController (ctrls/ctrl_darkroom.py:23-66) and
+ * DarkroomEnvVec.deploy_eval (envs/darkroom_env.py:151-175).  Episode e runs
+ * `horizon` steps from (0,0); its context is episodes max(0,e-R)..e-1 in order
+ * (R = ctx_episodes = H / horizon, shift-append :75-82), and every step is a
+ * full forward over the window [query = current state, context...] with the
+ * prediction at the last position.  Action a_t = select(logits, u_t) with
+ * u_t = uniforms[(e*horizon+t)*N + i] or Philox(seed, counter + e*horizon + t,
+ * first_task + i, DPT_STREAM_SELECT) -- the same draws as dpt_select_action.
+ * Requires sd = 2, A = 5, 1 + R*horizon <= 128 and dim <= 255 (else
+ * DPT_EUNSUPPORTED: use dpt_forward_window per step).                       */
+typedef struct dpt_darkroom_rollout_args {
+    int32_t N, Heps, horizon, ctx_episodes;
+    int32_t dim, sample;
+    int64_t first_task;
+    uint64_t seed, counter;
+    float temp;                 /* softmax temperature (1.0 in the reference) */
+    int32_t reserved0;
+    const int32_t* goals;       /* (N, 2) */
+    const int32_t* perms;       /* (N, 5) action permutation or NULL */
+    const double* uniforms;     /* (Heps*horizon, N) or NULL */
+    int32_t* returns_out;       /* (N, Heps) sum of rewards per episode */
+    int32_t* actions_out;       /* (N, Heps*horizon) or NULL */
+    float* logits_out;          /* (Heps*horizon, N, 5) or NULL */
+} dpt_darkroom_rollout_args;
+
+int dpt_rollout_darkroom(const dpt_model* model, const dpt_darkroom_rollout_args* args_host,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

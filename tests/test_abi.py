@@ -51,11 +51,34 @@ def test_abi_version_and_validation():
     assert b"action_dim" in lib.dpt_last_error()
 
 
-def test_struct_layout_matches_header():
+def test_struct_layout_matches_header(tmp_path):
+    """Every ctypes struct matches the C compiler's layout of include/dpt_hip.h field by field."""
+    import shutil
+    import subprocess
+
     from dpt_hip import _lib
-    assert ctypes.sizeof(_lib.ModelDesc) == 32
-    # int32 x6, int64, double, uint64, 8 pointers
-    assert ctypes.sizeof(_lib.BanditRolloutArgs) == 6 * 4 + 8 + 8 + 8 + 8 * 8
+    structs = {"dpt_model_desc": _lib.ModelDesc, "dpt_bandit_rollout_args": _lib.BanditRolloutArgs,
+               "dpt_policy_rollout_args": _lib.PolicyRolloutArgs,
+               "dpt_darkroom_rollout_args": _lib.DarkroomRolloutArgs}
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "dpt_hip.h"', 'int main(void) {']
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                              text=True).stdout.splitlines())
+    for cname, cls in structs.items():
+        assert int(got[f"{cname} size"]) == ctypes.sizeof(cls), cname
+        for fname, _ in cls._fields_:
+            assert int(got[f"{cname} {fname}"]) == getattr(cls, fname).offset, (cname, fname)
 
 
 def test_pack_weights_order():

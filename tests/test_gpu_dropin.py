@@ -159,7 +159,8 @@ def test_online_and_offline_eval_run():
     assert (base["opt"] >= base["lnr"] - 1e-12).all()
 
 
-def test_eval_darkroom_device_loop_matches_reference():
+@pytest.mark.parametrize("fused", [True, False])
+def test_eval_darkroom_device_loop_matches_reference(fused):
     from ctrls.ctrl_darkroom import DarkroomTransformerController
     from envs.darkroom_env import DarkroomEnv, DarkroomEnvPermuted, DarkroomEnvVec
     from evals import eval_darkroom
@@ -174,7 +175,9 @@ def test_eval_darkroom_device_loop_matches_reference():
         ctrl = DarkroomTransformerController(m, batch_size=n, sample=bool(sample))
         u = r["u"].reshape(-1, n)
         ctrl.uniforms = lambda k: u[k]
-        ret = eval_darkroom.deploy_online_vec(DarkroomEnvVec(envs), ctrl, Heps, H, horizon)
+        vec = DarkroomEnvVec(envs)
+        assert eval_darkroom._fused_ok(vec, ctrl, H) or not fused
+        ret = eval_darkroom.deploy_online_vec(vec, ctrl, Heps, H, horizon, fused=fused)
         assert np.array_equal(ret, r["returns"]), tag
 
 
