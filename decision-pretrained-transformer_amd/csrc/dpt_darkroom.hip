@@ -5,8 +5,8 @@
 // The query (current state) changes every step, so each step is a full causal
 // forward over the window [query, context transitions...] (models/net.py:41-60);
 // the prediction is the LAST position.  That is fp32-MFMA work: one workgroup
-// owns one task for all Heps x horizon steps, and wave w owns the 16 tokens
-// [16w, 16w+16) of the window (T <= 128).
+// owns one task for all Heps x horizon steps, and each wave owns 16 tokens of
+// the window (T <= 128).
 //
 // Dataflow is transposed (features x tokens): a wave keeps x^T of its 16
 // tokens in registers as MFMA 16x16x4 C-layout fragments -- lane (g = l>>4,
@@ -15,15 +15,39 @@
 // reads feature 16*(s>>2) + 4g + (s&3)), so c_attn, attention, c_proj, c_fc,
 // gelu and mlp.c_proj chain in registers; only K (token-major) and V
 // (feature-major) go through LDS, because every later token reads them.
-// Weights are the A operand, pre-packed per layer in fragment order
-// (FragOff) so one 16-B load per lane feeds four MFMAs.
+// Weights are the A operand, pre-packed per layer in fragment order (FragOff)
+// and read through one buffer descriptor, so one 16-B load per lane feeds four
+// MFMAs.
 //
-// Per step and layer: c_attn -> barrier -> causal flash attention (S^T = K Q^T
-// in registers, online softmax per token column, O^T += V^T P^T) -> barrier ->
-// c_proj, LayerNorm, MLP.  In the last layer only the wave that owns the last
-// position continues past the K/V exchange (nothing else is read), then it
-// applies ln_f + head, selects the action and steps the grid env.
+// Exact restructurings (same arithmetic up to fp32 summation order):
+//  * layer 0: within an episode the context tokens' layer-0 keys/values are
+//    fixed, so the causal softmax partial (m, l, o) of every token over keys
+//    1..t is computed once per episode; a step only projects the queries and
+//    the query token's key/value and merges key 0 into each partial;
+//  * last layer: only position T-1 is read, so after the K/V exchange its
+//    attention (one key tile per wave, flash-merged), c_proj and MLP (one
+//    hidden chunk per wave) are spread over the waves, then ln_f + head +
+//    selection + the grid step run on one wave.
 #include "dpt_common.h"
+
+// DPT_STAMPS (diagnostic build only): s_memtime at the barriers of a step,
+// accumulated by workgroup 0 thread 0 (see scripts/dr_stamps.py for the slots).
+#ifdef DPT_STAMPS
+__device__ unsigned long long g_dr_stamps[32];
+__device__ unsigned long long g_dr_last;
+#define DR_STAMP(k)                                                           \
+    do {                                                                      \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                            \
+            unsigned long long t_ = __builtin_amdgcn_s_memtime();             \
+            if (g_dr_last) g_dr_stamps[(k)] += t_ - g_dr_last;                \
+            g_dr_last = t_;                                                   \
+        }                                                                     \
+    } while (0)
+#else
+#define DR_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
 
 namespace dpt {
 
@@ -32,6 +56,7 @@ constexpr int kDrT = 16 * kDrWaves;         // max window (1 + R*horizon)
 constexpr int kKStride = kE + 4;            // K[token][feature]
 constexpr int kVStride = kDrT + 4;          // Vt[feature][token]
 constexpr int kDrA = 5;                     // DarkRoom actions
+constexpr int kDrF = 10;                    // token features 2*sd + A + 1
 
 // Fragment-packed weights of one block (floats), see pack_fragments_kernel.
 struct FragOff {
@@ -43,7 +68,8 @@ struct FragOff {
 };
 
 // A-operand fragment of W^T for a k=32 input (W is [in][out], Conv1D layout):
-// lane l, k-step s reads W[16*(s>>2) + 4*(l>>4) + (s&3)][ob*16 + (l&15)].
+// lane l, k-step s reads W[16*(s>>2) + 4*(l>>4) + (s&3)][ob*16 + (l&15)];
+// mlp.c_proj ([128][32]): chunk j, step s reads hidden 16j + 4*(l>>4) + s.
 __global__ void pack_fragments_kernel(ModelView M, float* __restrict__ frag) {
     const int total = M.n_layer * FragOff::size;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
@@ -52,26 +78,17 @@ __global__ void pack_fragments_kernel(ModelView M, float* __restrict__ frag) {
         const float* W = M.layers + (size_t)layer * LayerOff::size;
         const float* src;
         int n_out, in, out;
-        if (o < FragOff::fc && o >= 0) {
-            int base, width;
-            if (o < FragOff::proj) { base = FragOff::attn; src = W + LayerOff::attn_w; width = 3 * kE; }
-            else { base = FragOff::proj; src = W + LayerOff::proj_w; width = kE; }
+        if (o < FragOff::mp) {
+            int base;
+            if (o < FragOff::proj) { base = FragOff::attn; src = W + LayerOff::attn_w; n_out = 3 * kE; }
+            else if (o < FragOff::fc) { base = FragOff::proj; src = W + LayerOff::proj_w; n_out = kE; }
+            else { base = FragOff::fc; src = W + LayerOff::fc_w; n_out = kFF; }
             o -= base;
             const int s4 = o & 3, lane = (o >> 2) & 63, q = (o >> 8) & 1, ob = o >> 9;
             const int s = 4 * q + s4;
             in = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
             out = ob * 16 + (lane & 15);
-            n_out = width;
-        } else if (o < FragOff::mp) {
-            o -= FragOff::fc;
-            src = W + LayerOff::fc_w;
-            const int s4 = o & 3, lane = (o >> 2) & 63, q = (o >> 8) & 1, ob = o >> 9;
-            const int s = 4 * q + s4;
-            in = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
-            out = ob * 16 + (lane & 15);
-            n_out = kFF;
         } else {
-            // mlp.c_proj [128][32]: chunk j, step s reads hidden 16j + 4*(l>>4) + s
             o -= FragOff::mp;
             src = W + LayerOff::mp_w;
             const int s = o & 3, lane = (o >> 2) & 63, j = (o >> 8) & 7, ob = o >> 11;
@@ -83,11 +100,43 @@ __global__ void pack_fragments_kernel(ModelView M, float* __restrict__ frag) {
     }
 }
 
+// Small parameters copied to LDS once per launch (offsets in floats): per block
+// [ln1_g ln1_b attn_b proj_b ln2_g ln2_b fc_b mp_b], then the model-level ones.
+struct PL {
+    static constexpr int ln1_g = 0, ln1_b = 32, attn_b = 64, proj_b = 160, ln2_g = 192, ln2_b = 224,
+                         fc_b = 256, mp_b = 384, size = 416;
+};
+struct PTop {
+    int lnf_g, lnf_b, head_w, head_b, emb_b, wpe0, emb_w, total;
+    __host__ __device__ static PTop make(int L) {
+        PTop t;
+        int o = L * PL::size;
+        t.lnf_g = o; o += kE;
+        t.lnf_b = o; o += kE;
+        t.head_w = o; o += kE * kDrA;
+        t.head_b = o; o += 8;
+        t.emb_b = o; o += kE;
+        t.wpe0 = o; o += kE;
+        t.emb_w = o; o += kDrF * kE;
+        t.total = o;
+        return t;
+    }
+};
+
 struct DrSmem {
     float K[kDrT][kKStride];
     float Vt[kE][kVStride];
     int2 ctx[kDrT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
     int2 cur[kDrT];   // this episode's transitions
+    // layer-0 episode cache: the causal softmax partial of every token over keys
+    // 1..t, unnormalised o^T in C-layout per (wave, lane), m and l per token
+    float l0o[kDrWaves][64][8];
+    float l0m[kDrT], l0l[kDrT];
+    float k0[kE], v0[kE];             // layer 0: key / value of the query token
+    float ql[kE], xl[kE];             // last layer: q and residual of token T-1
+    float part_o[kDrWaves][kE];       // last layer: per-key-tile attention partials
+    float part_m[kDrWaves], part_l[kDrWaves];
+    float part_y[kDrWaves][kE];       // last layer: per-hidden-chunk MLP partials
     int sx, sy, ret, pad;
 };
 
@@ -96,6 +145,27 @@ __device__ inline floatx4 mfma4(float a, float b, floatx4 c) {
 }
 
 __device__ inline floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+
+// Lane index the compiler cannot hoist: every helper derives its lane-dependent
+// LDS addresses from this at its own start, so they are short-lived values
+// instead of loop invariants spilled across the whole rollout.
+__device__ inline int lane_id() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t & 63;
+}
+
+// Fragment-packed weights through one buffer descriptor: the per-lane part of
+// every address is lane*16; layer, region and block offsets are scalar.
+struct FragSrc {
+    __amdgpu_buffer_rsrc_t r;
+    int base;  // byte offset of this layer's block
+    __device__ floatx4 ld(int region_floats, int k) const {
+        return __builtin_bit_cast(
+            floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, base + 4 * region_floats + k * 1024, 0));
+    }
+    __device__ FragSrc layer(int l) const { return FragSrc{r, l * FragOff::size * 4}; }
+};
 
 __device__ inline void bar_lds_dr() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -106,7 +176,8 @@ __device__ inline void bar_lds_dr() {
 // LayerNorm over the 32 features of each token column (eps 1e-5): a lane holds
 // 8 of them; the other 24 live in lanes l^16, l^32, l^48.
 __device__ inline void ln_cols(const float (&v)[8], float (&out)[8], const float* __restrict__ gam,
-                               const float* __restrict__ bet, int g) {
+                               const float* __restrict__ bet) {
+    const int g = lane_id() >> 4;
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += v[k];
@@ -138,16 +209,137 @@ __device__ inline float gelu_fast(float x) {
     return 0.5f * x * (1.0f + t);
 }
 
-// out^T(ob) = bias + W^T xin^T for a k=32 input held as 8 C-layout values.
-__device__ inline floatx4 proj32(const float* __restrict__ frag, int ob, int lane, const float (&xin)[8],
-                                 floatx4 acc) {
-    const floatx4 w0 = ld4(frag + ((ob * 2 + 0) * 64 + lane) * 4);
-    const floatx4 w1 = ld4(frag + ((ob * 2 + 1) * 64 + lane) * 4);
+// acc + W^T xin^T for a k=32 input held as 8 C-layout values, given fragments
+__device__ inline floatx4 mfma32(const floatx4& w0, const floatx4& w1, const float (&xin)[8], floatx4 acc) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) acc = mfma4(w0[s], xin[s], acc);
 #pragma unroll
     for (int s = 0; s < 4; ++s) acc = mfma4(w1[s], xin[4 + s], acc);
     return acc;
+}
+
+// x^T += c_proj(o^T) (bias included)
+__device__ inline void attn_proj(const float* W, const FragSrc& fs, const float (&o)[8], float (&x)[8]) {
+    const int g = lane_id() >> 4;
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob) {
+        floatx4 acc = ld4(W + PL::proj_b + ob * 16 + 4 * g);
+        acc = mfma32(fs.ld(FragOff::proj, 2 * ob), fs.ld(FragOff::proj, 2 * ob + 1), o, acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[ob * 4 + r] += acc[r];
+    }
+}
+
+// x^T += MLP(xn^T) over the 8 hidden chunks, the next chunk's weight fragments
+// loaded while the current chunk computes.
+__device__ inline void mlp_cols(const float* W, const FragSrc& fs, const float (&xn)[8], float (&x)[8]) {
+    const int g = lane_id() >> 4;
+    floatx4 y0 = ld4(W + PL::mp_b + 4 * g), y1 = ld4(W + PL::mp_b + 16 + 4 * g);
+#pragma unroll 2
+    for (int j = 0; j < kFF / 16; ++j) {
+        const floatx4 a0 = fs.ld(FragOff::fc, 2 * j), a1 = fs.ld(FragOff::fc, 2 * j + 1);
+        const floatx4 b0 = fs.ld(FragOff::mp, j), b1 = fs.ld(FragOff::mp, 8 + j);
+        floatx4 h = mfma32(a0, a1, xn, ld4(W + PL::fc_b + j * 16 + 4 * g));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[r] = gelu_fast(h[r]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) y0 = mfma4(b0[s], h[s], y0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) y1 = mfma4(b1[s], h[s], y1);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        x[r] += y0[r];
+        x[4 + r] += y1[r];
+    }
+}
+
+// c_attn of one 16-token block: output blocks [ob0, ob1) of (Q0 Q1 K0 K1 V0 V1);
+// Q stays in registers, K -> LDS token-major, V -> LDS feature-major.
+__device__ inline void c_attn_block(DrSmem& S, const float* W, const FragSrc& fs, int qb, const float (&xn)[8],
+                                    float (&q)[8], int ob0, int ob1) {
+    floatx4 wf[4] = {fs.ld(FragOff::attn, 2 * ob0), fs.ld(FragOff::attn, 2 * ob0 + 1),
+                     fs.ld(FragOff::attn, 2 * ob0 + 2), fs.ld(FragOff::attn, 2 * ob0 + 3)};
+#pragma unroll
+    for (int ob = 0; ob < 6; ++ob) {
+        if (ob < ob0 || ob >= ob1) continue;
+        const floatx4 w0 = wf[0], w1 = wf[1];
+        wf[0] = wf[2];
+        wf[1] = wf[3];
+        if (ob + 2 < ob1) {
+            wf[2] = fs.ld(FragOff::attn, 2 * (ob + 2));
+            wf[3] = fs.ld(FragOff::attn, 2 * (ob + 2) + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const int lane = lane_id(), g = lane >> 4, tok = qb * 16 + (lane & 15);
+        const floatx4 acc = mfma32(w0, w1, xn, ld4(W + PL::attn_b + ob * 16 + 4 * g));
+        if (ob < 2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) q[ob * 4 + r] = acc[r];
+        } else if (ob < 4) {
+            *reinterpret_cast<floatx4*>(&S.K[tok][16 * (ob - 2) + 4 * g]) = acc;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S.Vt[16 * (ob - 4) + 4 * g + r][tok] = acc[r];
+        }
+    }
+}
+
+// Causal flash attention of query block qb over keys [key_lo, 16*qb + c]:
+// per token column the running max m (-inf when no key), sum l and the
+// unnormalised o^T (C-layout).
+__device__ inline void attend(const DrSmem& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
+                              float& lsum, float (&o)[8]) {
+    const int lane = lane_id(), g = lane >> 4, c = lane & 15;
+    m = -INFINITY;
+    lsum = 0.f;
+    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb <= qb; ++kb) {
+        const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
+        const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
+        floatx4 sc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sc = mfma4(k0[s], q[s], sc);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sc = mfma4(k1[s], q[4 + s], sc);
+        float sv[4];
+        float mt = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int key = kb * 16 + 4 * g + r;
+            sv[r] = sc[r] * scale;
+            if ((kb == qb && 4 * g + r > c) || key < key_lo) sv[r] = -INFINITY;
+            mt = fmaxf(mt, sv[r]);
+        }
+        mt = fmaxf(mt, __shfl_xor(mt, 16));
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float mn = fmaxf(m, mt);
+        const float base = mn == -INFINITY ? 0.f : mn;  // no key yet: keep 0, not NaN
+        const float corr = __expf(m - base);
+        float pr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - base);
+        lsum = lsum * corr + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
+        m = mn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            o0[r] *= corr;
+            o1[r] *= corr;
+        }
+        const floatx4 v0 = ld4(&S.Vt[c][kb * 16 + 4 * g]);
+        const floatx4 v1 = ld4(&S.Vt[16 + c][kb * 16 + 4 * g]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) o0 = mfma4(v0[s], pr[s], o0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
+    }
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        o[r] = o0[r];
+        o[4 + r] = o1[r];
+    }
 }
 
 __device__ inline int2 pack_tr(int x, int y, int a, int nx, int ny, int r) {
@@ -203,237 +395,387 @@ struct DarkroomParams {
     const float* frag;
 };
 
+// Query block of wave w: 0..3 on waves 0..3, then the longest blocks on waves
+// 4.. (waves w and w+4 share a SIMD, so their causal attention work pairs up
+// as (0, nqb-1), (1, nqb-2), ...).  -1 = no block this episode.
+__device__ inline int block_of_wave(int w, int nqb) {
+    if (w < 4) return w < nqb ? w : -1;
+    const int qb = nqb + 3 - w;
+    return qb >= 4 ? qb : -1;
+}
+
+// Token embeddings of block qb (embed_transition + wpe, models/net.py:52-54):
+// the query [state, 0...] at position 0, context transitions after it, zeros
+// past the window.
+__device__ inline void embed_block(const DrSmem& S, const float* P, const PTop& pt, const float* wpe, int qb, int T,
+                                   float (&x)[8]) {
+    const int lane = lane_id(), g = lane >> 4, tok = qb * 16 + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = 0.f;
+    if (tok >= T) return;
+    const int2 tr = tok >= 1 ? S.ctx[tok - 1] : make_int2(S.sx | (S.sy << 8), 0);
+    const float fv[6] = {(float)(tr.x & 255), (float)((tr.x >> 8) & 255), tok >= 1 ? 1.0f : 0.0f,
+                         (float)(tr.y & 255), (float)((tr.y >> 8) & 255), (float)((tr.x >> 24) & 255)};
+    const int rows[6] = {0, 1, 2 + ((tr.x >> 16) & 255), 7, 8, 9};
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+        const int d0 = 16 * blk + 4 * g;
+        floatx4 acc = ld4(P + pt.emb_b + d0);
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+            const floatx4 w = ld4(P + pt.emb_w + rows[f] * kE + d0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = fmaf(fv[f], w[r], acc[r]);
+        }
+        const floatx4 pe = tok == 0 ? ld4(P + pt.wpe0 + d0) : ld4(wpe + (size_t)tok * kE + d0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[blk * 4 + r] = acc[r] + pe[r];
+    }
+}
+
 __global__ void __launch_bounds__(kDrWaves * 64, 4)
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     __shared__ DrSmem S;
+    extern __shared__ float P[];
     const int task = blockIdx.x;
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
-    const int tok = wave * 16 + c;
-    const int gx = p.goals[2 * task], gy = p.goals[2 * task + 1];
-    int perm[kDrA];
-#pragma unroll
-    for (int k = 0; k < kDrA; ++k) perm[k] = p.perms ? p.perms[(size_t)task * kDrA + k] : k;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int steps_total = p.Heps * p.horizon;
     const float scale = 0.17677669529663687f;  // 1/sqrt(head_dim = 32)
-    // position-0 embedding pieces: emb_b + wpe[0] and the state rows of emb_w
-    const floatx4 eb0 = ld4(M.emb_b + 4 * g), eb1 = ld4(M.emb_b + 16 + 4 * g);
+    const int L = M.n_layer;
+    const PTop pt = PTop::make(L);
+    const FragSrc frag0{__builtin_amdgcn_make_buffer_rsrc((void*)p.frag, (short)0, L * FragOff::size * 4, 0x00020000),
+                        0};
+    for (int i = tid; i < L * PL::size; i += blockDim.x) {
+        const int l = i / PL::size, k = i % PL::size;
+        const float* Wg = M.layers + (size_t)l * LayerOff::size;
+        float v;
+        if (k < PL::ln1_b) v = Wg[LayerOff::ln1_g + k];
+        else if (k < PL::attn_b) v = Wg[LayerOff::ln1_b + k - PL::ln1_b];
+        else if (k < PL::proj_b) v = Wg[LayerOff::attn_b + k - PL::attn_b];
+        else if (k < PL::ln2_g) v = Wg[LayerOff::proj_b + k - PL::proj_b];
+        else if (k < PL::ln2_b) v = Wg[LayerOff::ln2_g + k - PL::ln2_g];
+        else if (k < PL::fc_b) v = Wg[LayerOff::ln2_b + k - PL::ln2_b];
+        else if (k < PL::mp_b) v = Wg[LayerOff::fc_b + k - PL::fc_b];
+        else v = Wg[LayerOff::mp_b + k - PL::mp_b];
+        P[i] = v;
+    }
+    for (int i = tid; i < kE; i += blockDim.x) {
+        P[pt.lnf_g + i] = M.lnf_g[i];
+        P[pt.lnf_b + i] = M.lnf_b[i];
+        P[pt.emb_b + i] = M.emb_b[i];
+        P[pt.wpe0 + i] = M.wpe[i];
+    }
+    for (int i = tid; i < kE * kDrA; i += blockDim.x) P[pt.head_w + i] = M.head_w[i];
+    for (int i = tid; i < kDrA; i += blockDim.x) P[pt.head_b + i] = M.head_b[i];
+    for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
 
     for (int ep = 0; ep < p.Heps; ++ep) {
         const int nctx = min(ep, p.R) * p.horizon;
         const int T = 1 + nctx;
         const int nqb = (T + 15) >> 4;
         const int qlast = (T - 1) >> 4, clast = (T - 1) & 15;
-        const bool active = wave < nqb;
+        const int qb = block_of_wave(wave, nqb);
+        const bool active = qb >= 0;
         if (tid == 0) {
             S.sx = 0;
             S.sy = 0;
             S.ret = 0;
         }
-        // context embeddings of this wave's tokens (fixed for the episode)
-        float x0[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) x0[k] = 0.f;
-        if (active && tok >= 1 && tok < T) {
-            const int2 tr = S.ctx[tok - 1];
-            const float fv[6] = {(float)(tr.x & 255), (float)((tr.x >> 8) & 255), 1.0f,
-                                (float)(tr.y & 255), (float)((tr.y >> 8) & 255), (float)((tr.x >> 24) & 255)};
-            const int rows[6] = {0, 1, 2 + ((tr.x >> 16) & 255), 7, 8, 9};
-#pragma unroll
-            for (int blk = 0; blk < 2; ++blk) {
-                const int d0 = 16 * blk + 4 * g;
-                floatx4 acc = blk ? eb1 : eb0;
-#pragma unroll
-                for (int f = 0; f < 6; ++f) {
-                    const floatx4 w = ld4(M.emb_w + rows[f] * kE + d0);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[r] = fmaf(fv[f], w[r], acc[r]);
-                }
-                const floatx4 pe = ld4(M.wpe + (size_t)tok * kE + d0);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) x0[blk * 4 + r] = acc[r] + pe[r];
-            }
-        }
         __syncthreads();
 
-        for (int t = 0; t < p.horizon; ++t) {
-            const int sx = S.sx, sy = S.sy;
-            float x[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) x[k] = x0[k];
-            if (tok == 0) {  // the query token [state, 0...] at position 0
-#pragma unroll
-                for (int blk = 0; blk < 2; ++blk) {
-                    const int d0 = 16 * blk + 4 * g;
-                    const floatx4 w0 = ld4(M.emb_w + 0 * kE + d0), w1 = ld4(M.emb_w + 1 * kE + d0);
-                    const floatx4 pe = ld4(M.wpe + d0);
-                    floatx4 acc = blk ? eb1 : eb0;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        acc[r] = fmaf((float)sx, w0[r], acc[r]);
-                        acc[r] = fmaf((float)sy, w1[r], acc[r]);
-                        x[blk * 4 + r] = acc[r] + pe[r];
-                    }
+        // layer-0 episode cache: causal partial over keys 1..t of every token
+        {
+            float q[8];
+            if (active) {
+                float x[8], xn[8];
+                embed_block(S, P, pt, M.wpe, qb, T, x);
+                ln_cols(x, xn, P + PL::ln1_g, P + PL::ln1_b);
+                c_attn_block(S, P, frag0, qb, xn, q, 0, 6);
+            }
+            bar_lds_dr();
+            if (active) {
+                float m, l, o[8];
+                attend(S, q, qb, 1, scale, m, l, o);
+                const int lane = lane_id();
+                *reinterpret_cast<floatx4*>(&S.l0o[wave][lane][0]) = {o[0], o[1], o[2], o[3]};
+                *reinterpret_cast<floatx4*>(&S.l0o[wave][lane][4]) = {o[4], o[5], o[6], o[7]};
+                if (lane < 16) {
+                    S.l0m[qb * 16 + lane] = m;
+                    S.l0l[qb * 16 + lane] = l;
                 }
             }
+            __syncthreads();
+        }
 
-            for (int layer = 0; layer < M.n_layer; ++layer) {
-                const bool last = layer == M.n_layer - 1;
-                const float* W = M.layers + (size_t)layer * LayerOff::size;
-                const float* F = p.frag + (size_t)layer * FragOff::size;
+        for (int t = 0; t < p.horizon; ++t) {
+            float x[8];
+            if (active) embed_block(S, P, pt, M.wpe, qb, T, x);
+            const int sx = S.sx, sy = S.sy;
+
+            // ---- layer 0: queries re-projected, the query token's key/value new
+            {
                 float q[8];
                 if (active) {
                     float xn[8];
-                    ln_cols(x, xn, W + LayerOff::ln1_g, W + LayerOff::ln1_b, g);
-                    // c_attn: Q stays in registers, K -> LDS token-major, V -> LDS feature-major
+                    ln_cols(x, xn, P + PL::ln1_g, P + PL::ln1_b);
+                    c_attn_block(S, P, frag0, qb, xn, q, 0, qb == 0 ? 6 : 2);
+                    const int lane = lane_id();
+                    if (qb == 0 && (lane & 15) == 0) {  // token 0's K row / Vt column -> k0, v0
 #pragma unroll
-                    for (int ob = 0; ob < 6; ++ob) {
-                        floatx4 acc = ld4(W + LayerOff::attn_b + ob * 16 + 4 * g);
-                        acc = proj32(F + FragOff::attn, ob, lane, xn, acc);
-                        if (ob < 2) {
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) q[ob * 4 + r] = acc[r];
-                        } else if (ob < 4) {
-                            *reinterpret_cast<floatx4*>(&S.K[tok][16 * (ob - 2) + 4 * g]) = acc;
-                        } else {
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) S.Vt[16 * (ob - 4) + 4 * g + r][tok] = acc[r];
+                        for (int k = 0; k < 8; ++k) {
+                            const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
+                            S.k0[d] = S.K[0][d];
+                            S.v0[d] = S.Vt[d][0];
                         }
                     }
                 }
                 bar_lds_dr();
-                const bool work = active && (!last || wave == qlast);
-                if (work) {
-                    // causal flash attention for this wave's query block
-                    float m = -INFINITY, lsum = 0.f;
-                    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-                    for (int kb = 0; kb <= wave; ++kb) {
-                        const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
-                        const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
-                        floatx4 sc = {0.f, 0.f, 0.f, 0.f};
+                DR_STAMP(0);
+                if (active) {
+                    // merge key 0 into the cached partial of every token column
+                    const int lane = lane_id(), g = lane >> 4, tok = qb * 16 + (lane & 15);
+                    const floatx4 ka = ld4(&S.k0[4 * g]), kc = ld4(&S.k0[16 + 4 * g]);
+                    float sdot = 0.f;
 #pragma unroll
-                        for (int s = 0; s < 4; ++s) sc = mfma4(k0[s], q[s], sc);
-#pragma unroll
-                        for (int s = 0; s < 4; ++s) sc = mfma4(k1[s], q[4 + s], sc);
-                        float sv[4];
-                        float mt = -INFINITY;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            sv[r] = sc[r] * scale;
-                            if (kb == wave && 4 * g + r > c) sv[r] = -INFINITY;
-                            mt = fmaxf(mt, sv[r]);
-                        }
-                        mt = fmaxf(mt, __shfl_xor(mt, 16));
-                        mt = fmaxf(mt, __shfl_xor(mt, 32));
-                        const float mn = fmaxf(m, mt);
-                        const float corr = __expf(m - mn);
-                        float pr[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - mn);
-                        lsum = lsum * corr + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
-                        m = mn;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            o0[r] *= corr;
-                            o1[r] *= corr;
-                        }
-                        const floatx4 v0 = ld4(&S.Vt[c][kb * 16 + 4 * g]);
-                        const floatx4 v1 = ld4(&S.Vt[16 + c][kb * 16 + 4 * g]);
-#pragma unroll
-                        for (int s = 0; s < 4; ++s) o0 = mfma4(v0[s], pr[s], o0);
-#pragma unroll
-                        for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
+                    for (int r = 0; r < 4; ++r) {
+                        sdot = fmaf(q[r], ka[r], sdot);
+                        sdot = fmaf(q[4 + r], kc[r], sdot);
                     }
-                    lsum += __shfl_xor(lsum, 16);
-                    lsum += __shfl_xor(lsum, 32);
-                    const float inv = 1.0f / lsum;
+                    sdot += __shfl_xor(sdot, 16);
+                    sdot += __shfl_xor(sdot, 32);
+                    const float s0 = sdot * scale;
+                    const float mt = S.l0m[tok], lt = S.l0l[tok];
+                    const float mn = fmaxf(mt, s0);
+                    const float ea = __expf(mt - mn), eb = __expf(s0 - mn);
+                    const float inv = 1.0f / (lt * ea + eb);
+                    const floatx4 oa = ld4(&S.l0o[wave][lane][0]), ob = ld4(&S.l0o[wave][lane][4]);
+                    const floatx4 va = ld4(&S.v0[4 * g]), vb = ld4(&S.v0[16 + 4 * g]);
                     float o[8];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        o[r] = o0[r] * inv;
-                        o[4 + r] = o1[r] * inv;
+                        o[r] = (oa[r] * ea + va[r] * eb) * inv;
+                        o[4 + r] = (ob[r] * ea + vb[r] * eb) * inv;
                     }
-                    // attn.c_proj + residual
+                    attn_proj(P, frag0, o, x);
+                    float xn[8];
+                    ln_cols(x, xn, P + PL::ln2_g, P + PL::ln2_b);
+                    mlp_cols(P, frag0, xn, x);
+                }
+                DR_STAMP(1);
+            }
+
+            for (int layer = 1; layer < L; ++layer) {
+                const bool last = layer == L - 1;
+                const float* W = P + layer * PL::size;
+                const FragSrc fs = frag0.layer(layer);
+                float q[8];
+                if (active) {
+                    float xn[8];
+                    ln_cols(x, xn, W + PL::ln1_g, W + PL::ln1_b);
+                    // the last layer needs q only for token T-1
+                    c_attn_block(S, W, fs, qb, xn, q, (!last || qb == qlast) ? 0 : 2, 6);
+                    const int lane = lane_id();
+                    if (last && qb == qlast && (lane & 15) == clast) {  // the one token the tail needs
 #pragma unroll
-                    for (int ob = 0; ob < 2; ++ob) {
-                        floatx4 acc = ld4(W + LayerOff::proj_b + ob * 16 + 4 * g);
-                        acc = proj32(F + FragOff::proj, ob, lane, o, acc);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) x[ob * 4 + r] += acc[r];
+                        for (int k = 0; k < 8; ++k) {
+                            const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
+                            S.ql[d] = q[k];
+                            S.xl[d] = x[k];
+                        }
                     }
                 }
-                if (!last) bar_lds_dr();  // every read of this layer's K/V is done
-                if (work) {
+                bar_lds_dr();
+                DR_STAMP(2 * layer);
+                if (last) break;
+                if (active) {
+                    float m, l, o[8];
+                    attend(S, q, qb, 0, scale, m, l, o);
+                    const float inv = 1.0f / l;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) o[k] *= inv;
+                    attn_proj(W, fs, o, x);
+                }
+                bar_lds_dr();  // every read of this layer's K/V is done
+                DR_STAMP(2 * layer + 1);
+                if (active) {
                     float xn[8];
-                    ln_cols(x, xn, W + LayerOff::ln2_g, W + LayerOff::ln2_b, g);
-                    floatx4 y0 = ld4(W + LayerOff::mp_b + 4 * g), y1 = ld4(W + LayerOff::mp_b + 16 + 4 * g);
-#pragma unroll 2
-                    for (int j = 0; j < kFF / 16; ++j) {
-                        floatx4 h = ld4(W + LayerOff::fc_b + j * 16 + 4 * g);
-                        h = proj32(F + FragOff::fc, j, lane, xn, h);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) h[r] = gelu_fast(h[r]);
-                        const floatx4 w0 = ld4(F + FragOff::mp + ((0 * 8 + j) * 64 + lane) * 4);
-                        const floatx4 w1 = ld4(F + FragOff::mp + ((1 * 8 + j) * 64 + lane) * 4);
-#pragma unroll
-                        for (int s = 0; s < 4; ++s) y0 = mfma4(w0[s], h[s], y0);
-#pragma unroll
-                        for (int s = 0; s < 4; ++s) y1 = mfma4(w1[s], h[s], y1);
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        x[r] += y0[r];
-                        x[4 + r] += y1[r];
-                    }
+                    ln_cols(x, xn, W + PL::ln2_g, W + PL::ln2_b);
+                    mlp_cols(W, fs, xn, x);
                 }
             }
 
-            // ln_f + head + selection + env step, by the wave holding position T-1
-            if (wave == qlast) {
-                float xf[8];
-                ln_cols(x, xf, M.lnf_g, M.lnf_b, g);
-                float lg[kDrA];
+            // ---- last layer for the one token T-1, spread over all waves.  Every
+            // column of these MFMAs carries the same token (B operands broadcast).
+            {
+                const float* W = P + (L - 1) * PL::size;
+                const FragSrc fs = frag0.layer(L - 1);
+                // this wave's weight fragments of the tail, in flight across the first barrier
+                floatx4 pw[4], fw[2], mw[2];
 #pragma unroll
-                for (int a = 0; a < kDrA; ++a) {
-                    float part = 0.f;
+                for (int k = 0; k < 4; ++k) pw[k] = fs.ld(FragOff::proj, k);
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int d = 16 * (k >> 2) + 4 * g + (k & 3);
-                        part = fmaf(xf[k], M.head_w[d * kDrA + a], part);
-                    }
-                    part += __shfl_xor(part, 16);
-                    part += __shfl_xor(part, 32);
-                    lg[a] = part + M.head_b[a];
+                for (int k = 0; k < 2; ++k) {
+                    fw[k] = fs.ld(FragOff::fc, wave * 2 + k);
+                    mw[k] = fs.ld(FragOff::mp, k * 8 + wave);
                 }
-                if (lane == clast) {
-                    const int step = ep * p.horizon + t;
-                    double u = 0.0;
-                    if (p.sample)
-                        u = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
-                                       : philox_uniform(p.seed, p.counter + step, p.first_task + task,
-                                                        DPT_STREAM_SELECT);
-                    const int a = select_fixed<kDrA>(lg, p.sample, p.temp, u);
-                    int ea = a;
+                const int step = ep * p.horizon + t;
+                double u = 0.0;
+                if (p.sample && tid == 0)
+                    u = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
+                                   : philox_uniform(p.seed, p.counter + step, p.first_task + task, DPT_STREAM_SELECT);
+                // (1) key tile `wave` of the attention, as a flash partial (m, l, o)
+                if (wave <= qlast) {
+                    const int lane = lane_id(), g = lane >> 4, c = lane & 15;
+                    const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
+                    const floatx4 k0 = ld4(&S.K[wave * 16 + c][4 * g]);
+                    const floatx4 k1 = ld4(&S.K[wave * 16 + c][16 + 4 * g]);
+                    floatx4 sc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int k = 0; k < kDrA; ++k)
-                        if (k == a) ea = perm[k];
-                    int nx = sx + (ea == 0) - (ea == 1);
-                    int ny = sy + (ea == 2) - (ea == 3);
-                    nx = min(max(nx, 0), p.dim - 1);
-                    ny = min(max(ny, 0), p.dim - 1);
-                    const int r = (nx == gx && ny == gy) ? 1 : 0;
-                    S.cur[t] = pack_tr(sx, sy, a, nx, ny, r);
-                    S.sx = nx;
-                    S.sy = ny;
-                    S.ret += r;
-                    if (p.actions_out) p.actions_out[(size_t)task * steps_total + step] = a;
-                    if (p.logits_out) {
+                    for (int s = 0; s < 4; ++s) sc = mfma4(k0[s], qa[s], sc);
 #pragma unroll
-                        for (int k = 0; k < kDrA; ++k) p.logits_out[((size_t)step * p.N + task) * kDrA + k] = lg[k];
+                    for (int s = 0; s < 4; ++s) sc = mfma4(k1[s], qc[s], sc);
+                    float sv[4], mt = -INFINITY;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        sv[r] = (wave * 16 + 4 * g + r <= T - 1) ? sc[r] * scale : -INFINITY;
+                        mt = fmaxf(mt, sv[r]);
+                    }
+                    mt = fmaxf(mt, __shfl_xor(mt, 16));
+                    mt = fmaxf(mt, __shfl_xor(mt, 32));
+                    float pr[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - mt);
+                    float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
+                    lt += __shfl_xor(lt, 16);
+                    lt += __shfl_xor(lt, 32);
+                    const floatx4 v0 = ld4(&S.Vt[c][wave * 16 + 4 * g]);
+                    const floatx4 v1 = ld4(&S.Vt[16 + c][wave * 16 + 4 * g]);
+                    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) o0 = mfma4(v0[s], pr[s], o0);
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
+                    if (c == 0) {
+                        *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
+                        *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;
+                    }
+                    if (lane == 0) {
+                        S.part_m[wave] = mt;
+                        S.part_l[wave] = lt;
+                    }
+                }
+                bar_lds_dr();
+                DR_STAMP(2 * L - 1);
+                // (2) every wave: merge the partials, c_proj + residual, ln_2, then MLP chunk `wave`
+                float xl[8];
+                {
+                    const int g = lane_id() >> 4;
+                    float mx = -INFINITY;
+                    for (int w = 0; w <= qlast; ++w) mx = fmaxf(mx, S.part_m[w]);
+                    float lsum = 0.f;
+                    floatx4 oa = {0.f, 0.f, 0.f, 0.f}, ob = {0.f, 0.f, 0.f, 0.f};
+                    for (int w = 0; w <= qlast; ++w) {
+                        const float e = __expf(S.part_m[w] - mx);
+                        lsum += S.part_l[w] * e;
+                        const floatx4 pa = ld4(&S.part_o[w][4 * g]), pb = ld4(&S.part_o[w][16 + 4 * g]);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            oa[r] = fmaf(pa[r], e, oa[r]);
+                            ob[r] = fmaf(pb[r], e, ob[r]);
+                        }
+                    }
+                    const float inv = 1.0f / lsum;
+                    float o[8];
+                    const floatx4 xa = ld4(&S.xl[4 * g]), xb = ld4(&S.xl[16 + 4 * g]);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        o[r] = oa[r] * inv;
+                        o[4 + r] = ob[r] * inv;
+                        xl[r] = xa[r];
+                        xl[4 + r] = xb[r];
+                    }
+#pragma unroll
+                    for (int ob2 = 0; ob2 < 2; ++ob2) {
+                        const floatx4 acc =
+                            mfma32(pw[2 * ob2], pw[2 * ob2 + 1], o, ld4(W + PL::proj_b + ob2 * 16 + 4 * g));
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) xl[ob2 * 4 + r] += acc[r];
+                    }
+                    float xn[8];
+                    ln_cols(xl, xn, W + PL::ln2_g, W + PL::ln2_b);
+                    floatx4 h = mfma32(fw[0], fw[1], xn, ld4(W + PL::fc_b + wave * 16 + 4 * g));
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) h[r] = gelu_fast(h[r]);
+                    floatx4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) y0 = mfma4(mw[0][s], h[s], y0);
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) y1 = mfma4(mw[1][s], h[s], y1);
+                    if ((lane_id() & 15) == 0) {
+                        *reinterpret_cast<floatx4*>(&S.part_y[wave][4 * g]) = y0;
+                        *reinterpret_cast<floatx4*>(&S.part_y[wave][16 + 4 * g]) = y1;
+                    }
+                }
+                bar_lds_dr();
+                DR_STAMP(2 * L);
+                // (3) wave 0: residual, ln_f, head, selection, env step
+                if (wave == 0) {
+                    const int lane = lane_id(), g = lane >> 4;
+                    floatx4 ya = ld4(W + PL::mp_b + 4 * g), yb = ld4(W + PL::mp_b + 16 + 4 * g);
+#pragma unroll
+                    for (int w = 0; w < kDrWaves; ++w) {
+                        const floatx4 pa = ld4(&S.part_y[w][4 * g]), pb = ld4(&S.part_y[w][16 + 4 * g]);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            ya[r] += pa[r];
+                            yb[r] += pb[r];
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        xl[r] += ya[r];
+                        xl[4 + r] += yb[r];
+                    }
+                    float xf[8];
+                    ln_cols(xl, xf, P + pt.lnf_g, P + pt.lnf_b);
+                    float lg[kDrA];
+#pragma unroll
+                    for (int a = 0; a < kDrA; ++a) {
+                        float part = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            const int d = 16 * (k >> 2) + 4 * g + (k & 3);
+                            part = fmaf(xf[k], P[pt.head_w + d * kDrA + a], part);
+                        }
+                        part += __shfl_xor(part, 16);
+                        part += __shfl_xor(part, 32);
+                        lg[a] = part + P[pt.head_b + a];
+                    }
+                    if (lane == 0) {
+                        const int a = select_fixed<kDrA>(lg, p.sample, p.temp, u);
+                        const int ea = p.perms ? p.perms[(size_t)task * kDrA + a] : a;
+                        int nx = sx + (ea == 0) - (ea == 1);
+                        int ny = sy + (ea == 2) - (ea == 3);
+                        nx = min(max(nx, 0), p.dim - 1);
+                        ny = min(max(ny, 0), p.dim - 1);
+                        const int gx = p.goals[2 * task], gy = p.goals[2 * task + 1];
+                        const int r = (nx == gx && ny == gy) ? 1 : 0;
+                        S.cur[t] = pack_tr(sx, sy, a, nx, ny, r);
+                        S.sx = nx;
+                        S.sy = ny;
+                        S.ret += r;
+                        if (p.actions_out) p.actions_out[(size_t)task * steps_total + step] = a;
+                        if (p.logits_out) {
+#pragma unroll
+                            for (int k = 0; k < kDrA; ++k)
+                                p.logits_out[((size_t)step * p.N + task) * kDrA + k] = lg[k];
+                        }
                     }
                 }
             }
             bar_lds_dr();
+            DR_STAMP(2 * L + 1);
         }
 
         // episode bookkeeping: returns, then shift-append the context (eval_darkroom.py:75-82)
@@ -478,10 +820,34 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     p.actions_out = a.actions_out;
     p.logits_out = a.logits_out;
     p.frag = frag;
-    hipLaunchKernelGGL(rollout_darkroom_kernel, dim3(a.N), dim3(kDrWaves * 64), 0, st, M, p);
+    if (M.n_layer < 2) {
+        set_error(DPT_EUNSUPPORTED, "fused darkroom rollout needs n_layer >= 2 (got %d)", M.n_layer);
+        return DPT_EUNSUPPORTED;
+    }
+    const size_t dyn = sizeof(float) * (size_t)PTop::make(M.n_layer).total;
+    if (dyn + sizeof(DrSmem) > 160 * 1024) {
+        set_error(DPT_EUNSUPPORTED, "n_layer=%d: parameter block does not fit in LDS", M.n_layer);
+        return DPT_EUNSUPPORTED;
+    }
+    if (dyn > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rollout_darkroom_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    hipLaunchKernelGGL(rollout_darkroom_kernel, dim3(a.N), dim3(kDrWaves * 64), dyn, st, M, p);
     return check_hip(hipGetLastError(), "rollout_darkroom_kernel launch");
 }
 
 int darkroom_max_window() { return kDrT; }
 
 }  // namespace dpt
+
+#ifdef DPT_STAMPS
+extern "C" int dpt_debug_dr_stamps(unsigned long long* out, int n, int reset) {
+    if (reset) {
+        unsigned long long z[32] = {0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dr_stamps), z, sizeof(z));
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dr_last), z, sizeof(unsigned long long));
+        return 0;
+    }
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dr_stamps), sizeof(unsigned long long) * (n < 32 ? n : 32));
+}
+#endif
