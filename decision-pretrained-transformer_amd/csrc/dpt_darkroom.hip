@@ -51,8 +51,9 @@ __device__ unsigned long long g_dr_last;
 
 namespace dpt {
 
-constexpr int kDrWaves = 8;                 // token blocks per window
-constexpr int kDrT = 16 * kDrWaves;         // max window (1 + R*horizon)
+constexpr int kDrWaves = 4;                 // waves per workgroup
+constexpr int kDrBlocks = 8;                // 16-token blocks per window (two per wave)
+constexpr int kDrT = 16 * kDrBlocks;        // max window (1 + R*horizon)
 constexpr int kKStride = kE + 4;            // K[token][feature]
 constexpr int kVStride = kDrT + 4;          // Vt[feature][token]
 constexpr int kDrA = 5;                     // DarkRoom actions
@@ -129,14 +130,14 @@ struct DrSmem {
     int2 ctx[kDrT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
     int2 cur[kDrT];   // this episode's transitions
     // layer-0 episode cache: the causal softmax partial of every token over keys
-    // 1..t, unnormalised o^T in C-layout per (wave, lane), m and l per token
-    float l0o[kDrWaves][64][8];
+    // 1..t, unnormalised o^T in C-layout per (block, lane), m and l per token
+    float l0o[kDrBlocks][64][8];
     float l0m[kDrT], l0l[kDrT];
     float k0[kE], v0[kE];             // layer 0: key / value of the query token
     float ql[kE], xl[kE];             // last layer: q and residual of token T-1
-    float part_o[kDrWaves][kE];       // last layer: per-key-tile attention partials
-    float part_m[kDrWaves], part_l[kDrWaves];
-    float part_y[kDrWaves][kE];       // last layer: per-hidden-chunk MLP partials
+    float part_o[kDrBlocks][kE];      // last layer: per-key-tile attention partials
+    float part_m[kDrBlocks], part_l[kDrBlocks];
+    float part_y[kFF / 16][kE];       // last layer: per-hidden-chunk MLP partials
     int sx, sy, ret, pad;
 };
 
@@ -203,10 +204,12 @@ __device__ inline void ln_cols(const float (&v)[8], float (&out)[8], const float
 }
 
 __device__ inline float gelu_fast(float x) {
-    // gelu_new (transformers/activations.py:65) with tanh(z) = 1 - 2/(exp(2z)+1)
-    const float z = 0.7978845608028654f * (x + 0.044715f * (x * x * x));
-    const float t = 1.0f - 2.0f / (__expf(2.0f * z) + 1.0f);
-    return 0.5f * x * (1.0f + t);
+    // gelu_new (transformers/activations.py:65): 0.5x(1 + tanh(z)) = x * sigmoid(2z)
+    // = x / (1 + 2^(x * (c1 + c2 x^2))), z = sqrt(2/pi)(x + 0.044715 x^3), log2(e) folded in
+    const float c1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+    const float c2 = c1 * 0.044715f;
+    const float e = __builtin_amdgcn_exp2f(x * fmaf(x * x, c2, c1));
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 // acc + W^T xin^T for a k=32 input held as 8 C-layout values, given fragments
@@ -218,69 +221,121 @@ __device__ inline floatx4 mfma32(const floatx4& w0, const floatx4& w1, const flo
     return acc;
 }
 
+// The same for the NB (1 or 2) blocks of a wave: one fragment load feeds NB
+// independent accumulation chains, interleaved.
+template <int NB>
+__device__ inline void mfma32n(const floatx4& w0, const floatx4& w1, const float (&xin)[2][8], floatx4 (&acc)[2]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = mfma4(w0[s], xin[j][s], acc[j]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = mfma4(w1[s], xin[j][4 + s], acc[j]);
+}
+
+template <int NB>
+__device__ inline void ln_n(const float (&x)[2][8], float (&xn)[2][8], const float* gam, const float* bet) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) ln_cols(x[j], xn[j], gam, bet);
+}
+
 // x^T += c_proj(o^T) (bias included)
-__device__ inline void attn_proj(const float* W, const FragSrc& fs, const float (&o)[8], float (&x)[8]) {
+template <int NB>
+__device__ inline void attn_proj(const float* W, const FragSrc& fs, const float (&o)[2][8], float (&x)[2][8]) {
     const int g = lane_id() >> 4;
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
-        floatx4 acc = ld4(W + PL::proj_b + ob * 16 + 4 * g);
-        acc = mfma32(fs.ld(FragOff::proj, 2 * ob), fs.ld(FragOff::proj, 2 * ob + 1), o, acc);
+        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g);
+        floatx4 acc[2] = {bias, bias};
+        mfma32n<NB>(fs.ld(FragOff::proj, 2 * ob), fs.ld(FragOff::proj, 2 * ob + 1), o, acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) x[ob * 4 + r] += acc[r];
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[j][ob * 4 + r] += acc[j][r];
     }
 }
 
-// x^T += MLP(xn^T) over the 8 hidden chunks, the next chunk's weight fragments
-// loaded while the current chunk computes.
-__device__ inline void mlp_cols(const float* W, const FragSrc& fs, const float (&xn)[8], float (&x)[8]) {
+// x^T += MLP(xn^T) over the 8 hidden chunks, software-pipelined: the c_fc
+// MFMAs of chunk c+1 are issued interleaved with the gelu of chunk c (an MFMA
+// leaves most of its 32 issue cycles to independent vector instructions),
+// then chunk c's mlp.c_proj MFMAs.
+template <int NB>
+__device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn)[2][8], float (&x)[2][8]) {
     const int g = lane_id() >> 4;
-    floatx4 y0 = ld4(W + PL::mp_b + 4 * g), y1 = ld4(W + PL::mp_b + 16 + 4 * g);
-#pragma unroll 2
-    for (int j = 0; j < kFF / 16; ++j) {
-        const floatx4 a0 = fs.ld(FragOff::fc, 2 * j), a1 = fs.ld(FragOff::fc, 2 * j + 1);
-        const floatx4 b0 = fs.ld(FragOff::mp, j), b1 = fs.ld(FragOff::mp, 8 + j);
-        floatx4 h = mfma32(a0, a1, xn, ld4(W + PL::fc_b + j * 16 + 4 * g));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h[r] = gelu_fast(h[r]);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) y0 = mfma4(b0[s], h[s], y0);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) y1 = mfma4(b1[s], h[s], y1);
+    const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);
+    floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
+    floatx4 h[2];
+    {
+        const floatx4 fb = ld4(W + PL::fc_b + 4 * g);
+        h[0] = fb;
+        h[1] = fb;
+        mfma32n<NB>(fs.ld(FragOff::fc, 0), fs.ld(FragOff::fc, 1), xn, h);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        x[r] += y0[r];
-        x[4 + r] += y1[r];
+    for (int c = 0; c < kFF / 16; ++c) {
+        const floatx4 b0 = fs.ld(FragOff::mp, c), b1 = fs.ld(FragOff::mp, 8 + c);
+        floatx4 hn[2] = {h[0], h[1]};
+        if (c + 1 < kFF / 16) {
+            const floatx4 fb = ld4(W + PL::fc_b + (c + 1) * 16 + 4 * g);
+            hn[0] = fb;
+            hn[1] = fb;
+            mfma32n<NB>(fs.ld(FragOff::fc, 2 * (c + 1)), fs.ld(FragOff::fc, 2 * (c + 1) + 1), xn, hn);
+        }
+        floatx4 gl[2];
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gl[j][r] = gelu_fast(h[j][r]);
+        if (c + 1 < kFF / 16) {
+#pragma unroll
+            for (int k = 0; k < 8 * NB; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      // one c_fc(c+1) MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 4 / NB, 0);  // gelu(c) VALU
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                y0[j] = mfma4(b0[s], gl[j][s], y0[j]);
+                y1[j] = mfma4(b1[s], gl[j][s], y1[j]);
+            }
+        h[0] = hn[0];
+        h[1] = hn[1];
     }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            x[j][r] += y0[j][r];
+            x[j][4 + r] += y1[j][r];
+        }
 }
 
-// c_attn of one 16-token block: output blocks [ob0, ob1) of (Q0 Q1 K0 K1 V0 V1);
+// c_attn output blocks [ob0, ob1) of (Q0 Q1 K0 K1 V0 V1) for the NB blocks qb[]:
 // Q stays in registers, K -> LDS token-major, V -> LDS feature-major.
-__device__ inline void c_attn_block(DrSmem& S, const float* W, const FragSrc& fs, int qb, const float (&xn)[8],
-                                    float (&q)[8], int ob0, int ob1) {
-    floatx4 wf[4] = {fs.ld(FragOff::attn, 2 * ob0), fs.ld(FragOff::attn, 2 * ob0 + 1),
-                     fs.ld(FragOff::attn, 2 * ob0 + 2), fs.ld(FragOff::attn, 2 * ob0 + 3)};
+template <int NB>
+__device__ inline void c_attn_n(DrSmem& S, const float* W, const FragSrc& fs, const int (&qb)[2],
+                                const float (&xn)[2][8], float (&q)[2][8], int ob0, int ob1) {
+    for (int ob = ob0; ob < ob1; ++ob) {
+        const int lane = lane_id(), g = lane >> 4;
+        const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);
+        floatx4 acc[2] = {bias, bias};
+        mfma32n<NB>(fs.ld(FragOff::attn, 2 * ob), fs.ld(FragOff::attn, 2 * ob + 1), xn, acc);
 #pragma unroll
-    for (int ob = 0; ob < 6; ++ob) {
-        if (ob < ob0 || ob >= ob1) continue;
-        const floatx4 w0 = wf[0], w1 = wf[1];
-        wf[0] = wf[2];
-        wf[1] = wf[3];
-        if (ob + 2 < ob1) {
-            wf[2] = fs.ld(FragOff::attn, 2 * (ob + 2));
-            wf[3] = fs.ld(FragOff::attn, 2 * (ob + 2) + 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const int lane = lane_id(), g = lane >> 4, tok = qb * 16 + (lane & 15);
-        const floatx4 acc = mfma32(w0, w1, xn, ld4(W + PL::attn_b + ob * 16 + 4 * g));
-        if (ob < 2) {
+        for (int j = 0; j < NB; ++j) {
+            const int tok = qb[j] * 16 + (lane & 15);
+            if (ob < 2) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) q[ob * 4 + r] = acc[r];
-        } else if (ob < 4) {
-            *reinterpret_cast<floatx4*>(&S.K[tok][16 * (ob - 2) + 4 * g]) = acc;
-        } else {
+                for (int r = 0; r < 4; ++r) q[j][ob * 4 + r] = acc[j][r];
+            } else if (ob < 4) {
+                *reinterpret_cast<floatx4*>(&S.K[tok][16 * (ob - 2) + 4 * g]) = acc[j];
+            } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) S.Vt[16 * (ob - 4) + 4 * g + r][tok] = acc[r];
+                for (int r = 0; r < 4; ++r) S.Vt[16 * (ob - 4) + 4 * g + r][tok] = acc[j][r];
+            }
         }
     }
 }
@@ -395,13 +450,15 @@ struct DarkroomParams {
     const float* frag;
 };
 
-// Query block of wave w: 0..3 on waves 0..3, then the longest blocks on waves
-// 4.. (waves w and w+4 share a SIMD, so their causal attention work pairs up
-// as (0, nqb-1), (1, nqb-2), ...).  -1 = no block this episode.
-__device__ inline int block_of_wave(int w, int nqb) {
-    if (w < 4) return w < nqb ? w : -1;
-    const int qb = nqb + 3 - w;
-    return qb >= 4 ? qb : -1;
+// Blocks of wave w: pairs (w, nqb-1-w), so a wave's causal attention rows sum
+// to the same length; the middle block of an odd count goes alone.  Returns
+// the number of blocks (0, 1 or 2).
+__device__ inline int blocks_of_wave(int w, int nqb, int (&qb)[2]) {
+    qb[0] = w;
+    qb[1] = nqb - 1 - w;
+    if (w < nqb / 2) return 2;
+    if ((nqb & 1) && w == nqb / 2) return 1;
+    return 0;
 }
 
 // Token embeddings of block qb (embed_transition + wpe, models/net.py:52-54):
@@ -433,7 +490,19 @@ __device__ inline void embed_block(const DrSmem& S, const float* P, const PTop& 
     }
 }
 
-__global__ void __launch_bounds__(kDrWaves * 64, 4)
+// One phase over the wave's blocks, dispatched on their count (uniform per wave).
+#define DR_BLOCKS(nb, CALL) \
+    do {                    \
+        if ((nb) == 2) {    \
+            constexpr int NB = 2; \
+            CALL;           \
+        } else if ((nb) == 1) { \
+            constexpr int NB = 1; \
+            CALL;           \
+        }                   \
+    } while (0)
+
+__global__ void __launch_bounds__(kDrWaves * 64, 2)
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     __shared__ DrSmem S;
     extern __shared__ float P[];
@@ -475,8 +544,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         const int T = 1 + nctx;
         const int nqb = (T + 15) >> 4;
         const int qlast = (T - 1) >> 4, clast = (T - 1) & 15;
-        const int qb = block_of_wave(wave, nqb);
-        const bool active = qb >= 0;
+        int qb[2];
+        const int nb = blocks_of_wave(wave, nqb, qb);
         if (tid == 0) {
             S.sx = 0;
             S.sy = 0;
@@ -486,81 +555,91 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 
         // layer-0 episode cache: causal partial over keys 1..t of every token
         {
-            float q[8];
-            if (active) {
-                float x[8], xn[8];
-                embed_block(S, P, pt, M.wpe, qb, T, x);
-                ln_cols(x, xn, P + PL::ln1_g, P + PL::ln1_b);
-                c_attn_block(S, P, frag0, qb, xn, q, 0, 6);
-            }
+            float x[2][8], xn[2][8], q[2][8];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
+            DR_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
+                           c_attn_n<NB>(S, P, frag0, qb, xn, q, 0, 6)));
             bar_lds_dr();
-            if (active) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (j >= nb) break;
                 float m, l, o[8];
-                attend(S, q, qb, 1, scale, m, l, o);
+                attend(S, q[j], qb[j], 1, scale, m, l, o);
                 const int lane = lane_id();
-                *reinterpret_cast<floatx4*>(&S.l0o[wave][lane][0]) = {o[0], o[1], o[2], o[3]};
-                *reinterpret_cast<floatx4*>(&S.l0o[wave][lane][4]) = {o[4], o[5], o[6], o[7]};
+                *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][0]) = {o[0], o[1], o[2], o[3]};
+                *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][4]) = {o[4], o[5], o[6], o[7]};
                 if (lane < 16) {
-                    S.l0m[qb * 16 + lane] = m;
-                    S.l0l[qb * 16 + lane] = l;
+                    S.l0m[qb[j] * 16 + lane] = m;
+                    S.l0l[qb[j] * 16 + lane] = l;
                 }
             }
             __syncthreads();
         }
 
         for (int t = 0; t < p.horizon; ++t) {
-            float x[8];
-            if (active) embed_block(S, P, pt, M.wpe, qb, T, x);
+            float x[2][8];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
             const int sx = S.sx, sy = S.sy;
 
             // ---- layer 0: queries re-projected, the query token's key/value new
             {
-                float q[8];
-                if (active) {
-                    float xn[8];
-                    ln_cols(x, xn, P + PL::ln1_g, P + PL::ln1_b);
-                    c_attn_block(S, P, frag0, qb, xn, q, 0, qb == 0 ? 6 : 2);
-                    const int lane = lane_id();
-                    if (qb == 0 && (lane & 15) == 0) {  // token 0's K row / Vt column -> k0, v0
+                float q[2][8];
+                {
+                    float xn[2][8];
+                    DR_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
+                                   c_attn_n<NB>(S, P, frag0, qb, xn, q, 0, 2)));
+                    if (wave == 0) {  // block 0 (slot 0 of wave 0): key/value of the query token
+                        c_attn_n<1>(S, P, frag0, qb, xn, q, 2, 6);
+                        const int lane = lane_id();
+                        if ((lane & 15) == 0) {
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
-                            S.k0[d] = S.K[0][d];
-                            S.v0[d] = S.Vt[d][0];
+                            for (int k = 0; k < 8; ++k) {
+                                const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
+                                S.k0[d] = S.K[0][d];
+                                S.v0[d] = S.Vt[d][0];
+                            }
                         }
                     }
                 }
                 bar_lds_dr();
                 DR_STAMP(0);
-                if (active) {
+                if (nb > 0) {
                     // merge key 0 into the cached partial of every token column
-                    const int lane = lane_id(), g = lane >> 4, tok = qb * 16 + (lane & 15);
+                    const int lane = lane_id(), g = lane >> 4;
                     const floatx4 ka = ld4(&S.k0[4 * g]), kc = ld4(&S.k0[16 + 4 * g]);
-                    float sdot = 0.f;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        sdot = fmaf(q[r], ka[r], sdot);
-                        sdot = fmaf(q[4 + r], kc[r], sdot);
-                    }
-                    sdot += __shfl_xor(sdot, 16);
-                    sdot += __shfl_xor(sdot, 32);
-                    const float s0 = sdot * scale;
-                    const float mt = S.l0m[tok], lt = S.l0l[tok];
-                    const float mn = fmaxf(mt, s0);
-                    const float ea = __expf(mt - mn), eb = __expf(s0 - mn);
-                    const float inv = 1.0f / (lt * ea + eb);
-                    const floatx4 oa = ld4(&S.l0o[wave][lane][0]), ob = ld4(&S.l0o[wave][lane][4]);
                     const floatx4 va = ld4(&S.v0[4 * g]), vb = ld4(&S.v0[16 + 4 * g]);
-                    float o[8];
+                    float o[2][8];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        o[r] = (oa[r] * ea + va[r] * eb) * inv;
-                        o[4 + r] = (ob[r] * ea + vb[r] * eb) * inv;
+                    for (int j = 0; j < 2; ++j) {
+                        if (j >= nb) break;
+                        const int tok = qb[j] * 16 + (lane & 15);
+                        float sdot = 0.f;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            sdot = fmaf(q[j][r], ka[r], sdot);
+                            sdot = fmaf(q[j][4 + r], kc[r], sdot);
+                        }
+                        sdot += __shfl_xor(sdot, 16);
+                        sdot += __shfl_xor(sdot, 32);
+                        const float s0 = sdot * scale;
+                        const float mt = S.l0m[tok], lt = S.l0l[tok];
+                        const float mn = fmaxf(mt, s0);
+                        const float ea = __expf(mt - mn), eb = __expf(s0 - mn);
+                        const float inv = 1.0f / (lt * ea + eb);
+                        const floatx4 oa = ld4(&S.l0o[qb[j]][lane][0]), ob = ld4(&S.l0o[qb[j]][lane][4]);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            o[j][r] = (oa[r] * ea + va[r] * eb) * inv;
+                            o[j][4 + r] = (ob[r] * ea + vb[r] * eb) * inv;
+                        }
                     }
-                    attn_proj(P, frag0, o, x);
-                    float xn[8];
-                    ln_cols(x, xn, P + PL::ln2_g, P + PL::ln2_b);
-                    mlp_cols(P, frag0, xn, x);
+                    float xn[2][8];
+                    DR_BLOCKS(nb, (attn_proj<NB>(P, frag0, o, x), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                                   mlp_n<NB>(P, frag0, xn, x)));
                 }
                 DR_STAMP(1);
             }
@@ -569,105 +648,121 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 const bool last = layer == L - 1;
                 const float* W = P + layer * PL::size;
                 const FragSrc fs = frag0.layer(layer);
-                float q[8];
-                if (active) {
-                    float xn[8];
-                    ln_cols(x, xn, W + PL::ln1_g, W + PL::ln1_b);
-                    // the last layer needs q only for token T-1
-                    c_attn_block(S, W, fs, qb, xn, q, (!last || qb == qlast) ? 0 : 2, 6);
-                    const int lane = lane_id();
-                    if (last && qb == qlast && (lane & 15) == clast) {  // the one token the tail needs
+                float q[2][8];
+                {
+                    float xn[2][8];
+                    if (!last) {
+                        DR_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
+                                       c_attn_n<NB>(S, W, fs, qb, xn, q, 0, 6)));
+                    } else {
+                        // the last layer needs q only for token T-1 (block qlast)
+                        DR_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
+                                       c_attn_n<NB>(S, W, fs, qb, xn, q, 2, 6)));
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
-                            S.ql[d] = q[k];
-                            S.xl[d] = x[k];
+                        for (int j = 0; j < 2; ++j) {
+                            if (j < nb && qb[j] == qlast) {
+                                const int one[2] = {qb[j], qb[j]};
+                                float xn1[2][8], q1[2][8];
+#pragma unroll
+                                for (int k = 0; k < 8; ++k) xn1[0][k] = xn[j][k];
+                                c_attn_n<1>(S, W, fs, one, xn1, q1, 0, 2);
+                                const int lane = lane_id();
+                                if ((lane & 15) == clast) {
+#pragma unroll
+                                    for (int k = 0; k < 8; ++k) {
+                                        const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
+                                        S.ql[d] = q1[0][k];
+                                        S.xl[d] = x[j][k];
+                                    }
+                                }
+                            }
                         }
                     }
                 }
                 bar_lds_dr();
                 DR_STAMP(2 * layer);
                 if (last) break;
-                if (active) {
-                    float m, l, o[8];
-                    attend(S, q, qb, 0, scale, m, l, o);
-                    const float inv = 1.0f / l;
+                if (nb > 0) {
+                    float o[2][8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) o[k] *= inv;
-                    attn_proj(W, fs, o, x);
+                    for (int j = 0; j < 2; ++j) {
+                        if (j >= nb) break;
+                        float m, l;
+                        attend(S, q[j], qb[j], 0, scale, m, l, o[j]);
+                        const float inv = 1.0f / l;
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) o[j][k] *= inv;
+                    }
+                    DR_BLOCKS(nb, attn_proj<NB>(W, fs, o, x));
                 }
                 bar_lds_dr();  // every read of this layer's K/V is done
                 DR_STAMP(2 * layer + 1);
-                if (active) {
-                    float xn[8];
-                    ln_cols(x, xn, W + PL::ln2_g, W + PL::ln2_b);
-                    mlp_cols(W, fs, xn, x);
+                {
+                    float xn[2][8];
+                    DR_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b), mlp_n<NB>(W, fs, xn, x)));
                 }
             }
 
-            // ---- last layer for the one token T-1, spread over all waves.  Every
+            // ---- last layer for the one token T-1, spread over the waves.  Every
             // column of these MFMAs carries the same token (B operands broadcast).
             {
                 const float* W = P + (L - 1) * PL::size;
                 const FragSrc fs = frag0.layer(L - 1);
-                // this wave's weight fragments of the tail, in flight across the first barrier
-                floatx4 pw[4], fw[2], mw[2];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) pw[k] = fs.ld(FragOff::proj, k);
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    fw[k] = fs.ld(FragOff::fc, wave * 2 + k);
-                    mw[k] = fs.ld(FragOff::mp, k * 8 + wave);
-                }
                 const int step = ep * p.horizon + t;
                 double u = 0.0;
                 if (p.sample && tid == 0)
                     u = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
                                    : philox_uniform(p.seed, p.counter + step, p.first_task + task, DPT_STREAM_SELECT);
-                // (1) key tile `wave` of the attention, as a flash partial (m, l, o)
-                if (wave <= qlast) {
+                // (1) key tiles wave and wave+4 of the attention, as flash partials (m, l, o)
+                {
                     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
                     const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
-                    const floatx4 k0 = ld4(&S.K[wave * 16 + c][4 * g]);
-                    const floatx4 k1 = ld4(&S.K[wave * 16 + c][16 + 4 * g]);
-                    floatx4 sc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) sc = mfma4(k0[s], qa[s], sc);
+                    for (int h = 0; h < 2; ++h) {
+                        const int kt = wave + 4 * h;
+                        if (kt > qlast) break;
+                        const floatx4 k0 = ld4(&S.K[kt * 16 + c][4 * g]);
+                        const floatx4 k1 = ld4(&S.K[kt * 16 + c][16 + 4 * g]);
+                        floatx4 sc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) sc = mfma4(k1[s], qc[s], sc);
-                    float sv[4], mt = -INFINITY;
+                        for (int s4 = 0; s4 < 4; ++s4) sc = mfma4(k0[s4], qa[s4], sc);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        sv[r] = (wave * 16 + 4 * g + r <= T - 1) ? sc[r] * scale : -INFINITY;
-                        mt = fmaxf(mt, sv[r]);
-                    }
-                    mt = fmaxf(mt, __shfl_xor(mt, 16));
-                    mt = fmaxf(mt, __shfl_xor(mt, 32));
-                    float pr[4];
+                        for (int s4 = 0; s4 < 4; ++s4) sc = mfma4(k1[s4], qc[s4], sc);
+                        float sv[4], mt = -INFINITY;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - mt);
-                    float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
-                    lt += __shfl_xor(lt, 16);
-                    lt += __shfl_xor(lt, 32);
-                    const floatx4 v0 = ld4(&S.Vt[c][wave * 16 + 4 * g]);
-                    const floatx4 v1 = ld4(&S.Vt[16 + c][wave * 16 + 4 * g]);
-                    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+                        for (int r = 0; r < 4; ++r) {
+                            sv[r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * scale : -INFINITY;
+                            mt = fmaxf(mt, sv[r]);
+                        }
+                        mt = fmaxf(mt, __shfl_xor(mt, 16));
+                        mt = fmaxf(mt, __shfl_xor(mt, 32));
+                        float pr[4];
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) o0 = mfma4(v0[s], pr[s], o0);
+                        for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - mt);
+                        float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
+                        lt += __shfl_xor(lt, 16);
+                        lt += __shfl_xor(lt, 32);
+                        const floatx4 v0 = ld4(&S.Vt[c][kt * 16 + 4 * g]);
+                        const floatx4 v1 = ld4(&S.Vt[16 + c][kt * 16 + 4 * g]);
+                        floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
-                    if (c == 0) {
-                        *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
-                        *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;
-                    }
-                    if (lane == 0) {
-                        S.part_m[wave] = mt;
-                        S.part_l[wave] = lt;
+                        for (int s4 = 0; s4 < 4; ++s4) o0 = mfma4(v0[s4], pr[s4], o0);
+#pragma unroll
+                        for (int s4 = 0; s4 < 4; ++s4) o1 = mfma4(v1[s4], pr[s4], o1);
+                        if (c == 0) {
+                            *reinterpret_cast<floatx4*>(&S.part_o[kt][4 * g]) = o0;
+                            *reinterpret_cast<floatx4*>(&S.part_o[kt][16 + 4 * g]) = o1;
+                        }
+                        if (lane == 0) {
+                            S.part_m[kt] = mt;
+                            S.part_l[kt] = lt;
+                        }
                     }
                 }
                 bar_lds_dr();
                 DR_STAMP(2 * L - 1);
-                // (2) every wave: merge the partials, c_proj + residual, ln_2, then MLP chunk `wave`
+                // (2) every wave: merge the partials, c_proj + residual, ln_2, then
+                // MLP hidden chunks wave and wave+4
                 float xl[8];
                 {
                     const int g = lane_id() >> 4;
@@ -697,24 +792,31 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
 #pragma unroll
                     for (int ob2 = 0; ob2 < 2; ++ob2) {
-                        const floatx4 acc =
-                            mfma32(pw[2 * ob2], pw[2 * ob2 + 1], o, ld4(W + PL::proj_b + ob2 * 16 + 4 * g));
+                        const floatx4 acc = mfma32(fs.ld(FragOff::proj, 2 * ob2), fs.ld(FragOff::proj, 2 * ob2 + 1), o,
+                                                   ld4(W + PL::proj_b + ob2 * 16 + 4 * g));
 #pragma unroll
                         for (int r = 0; r < 4; ++r) xl[ob2 * 4 + r] += acc[r];
                     }
                     float xn[8];
                     ln_cols(xl, xn, W + PL::ln2_g, W + PL::ln2_b);
-                    floatx4 h = mfma32(fw[0], fw[1], xn, ld4(W + PL::fc_b + wave * 16 + 4 * g));
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) h[r] = gelu_fast(h[r]);
-                    floatx4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
+                    for (int h = 0; h < 2; ++h) {
+                        const int cj = wave + 4 * h;
+                        floatx4 hh = mfma32(fs.ld(FragOff::fc, 2 * cj), fs.ld(FragOff::fc, 2 * cj + 1), xn,
+                                            ld4(W + PL::fc_b + cj * 16 + 4 * g));
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) y0 = mfma4(mw[0][s], h[s], y0);
+                        for (int r = 0; r < 4; ++r) hh[r] = gelu_fast(hh[r]);
+                        const floatx4 m0 = fs.ld(FragOff::mp, cj), m1 = fs.ld(FragOff::mp, 8 + cj);
+                        floatx4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) y1 = mfma4(mw[1][s], h[s], y1);
-                    if ((lane_id() & 15) == 0) {
-                        *reinterpret_cast<floatx4*>(&S.part_y[wave][4 * g]) = y0;
-                        *reinterpret_cast<floatx4*>(&S.part_y[wave][16 + 4 * g]) = y1;
+                        for (int s4 = 0; s4 < 4; ++s4) {
+                            y0 = mfma4(m0[s4], hh[s4], y0);
+                            y1 = mfma4(m1[s4], hh[s4], y1);
+                        }
+                        if ((lane_id() & 15) == 0) {
+                            *reinterpret_cast<floatx4*>(&S.part_y[cj][4 * g]) = y0;
+                            *reinterpret_cast<floatx4*>(&S.part_y[cj][16 + 4 * g]) = y1;
+                        }
                     }
                 }
                 bar_lds_dr();
@@ -724,7 +826,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     const int lane = lane_id(), g = lane >> 4;
                     floatx4 ya = ld4(W + PL::mp_b + 4 * g), yb = ld4(W + PL::mp_b + 16 + 4 * g);
 #pragma unroll
-                    for (int w = 0; w < kDrWaves; ++w) {
+                    for (int w = 0; w < kFF / 16; ++w) {
                         const floatx4 pa = ld4(&S.part_y[w][4 * g]), pb = ld4(&S.part_y[w][16 + 4 * g]);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -781,14 +883,21 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         // episode bookkeeping: returns, then shift-append the context (eval_darkroom.py:75-82)
         if (tid == 0) p.returns_out[(size_t)task * p.Heps + ep] = S.ret;
         const int R = p.R, H = p.horizon;
-        int2 v = make_int2(0, 0);
-        const bool mv = tid < R * H;
-        if (mv) {
-            if (ep < R) v = (tid >= ep * H && tid < (ep + 1) * H) ? S.cur[tid - ep * H] : S.ctx[tid];
-            else v = tid < (R - 1) * H ? S.ctx[tid + H] : S.cur[tid - (R - 1) * H];
+        int2 v[2] = {make_int2(0, 0), make_int2(0, 0)};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = tid + h * blockDim.x;
+            if (i < R * H) {
+                if (ep < R) v[h] = (i >= ep * H && i < (ep + 1) * H) ? S.cur[i - ep * H] : S.ctx[i];
+                else v[h] = i < (R - 1) * H ? S.ctx[i + H] : S.cur[i - (R - 1) * H];
+            }
         }
         __syncthreads();
-        if (mv) S.ctx[tid] = v;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = tid + h * blockDim.x;
+            if (i < R * H) S.ctx[i] = v[h];
+        }
         __syncthreads();
     }
 }
