@@ -166,8 +166,12 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
         for (int r = 0; r < kRows; ++r) {
             const int p = base + 8 * r + g;
             if (p < pos) {
-                kk[r] = __ldg(reinterpret_cast<const float4*>(kc + (size_t)p * kE) + c);
-                vv[r] = __ldg(reinterpret_cast<const float4*>(vc + (size_t)p * kE) + c);
+                // non-temporal: each K/V row is read once per step by this CU only, so it
+                // must not evict the weights every workgroup re-reads from L2
+                const floatx4 k4 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kc + (size_t)p * kE) + c);
+                const floatx4 v4 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vc + (size_t)p * kE) + c);
+                kk[r] = make_float4(k4[0], k4[1], k4[2], k4[3]);
+                vv[r] = make_float4(v4[0], v4[1], v4[2], v4[3]);
             } else {
                 kk[r] = make_float4(0.f, 0.f, 0.f, 0.f);
                 vv[r] = kk[r];
@@ -650,7 +654,7 @@ extern "C" int dpt_debug_stamps(unsigned long long* out, int n, int reset) {
 }
 #endif
 
-static int g_decode_tile = 16;  // tuning knob (dpt_tuning_set(DPT_TUNE_DECODE_TILE, 8|16))
+static int g_decode_tile = 8;  // tuning knob (dpt_tuning_set(DPT_TUNE_DECODE_TILE, 8|16))
 
 int set_decode_tile(int t) {
     if (t != 8 && t != 16) return DPT_EINVAL;

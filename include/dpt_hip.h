@@ -63,7 +63,8 @@ extern "C" {
 int dpt_abi_version(void);
 const char* dpt_last_error(void);
 /* Process-wide tuning knobs (no effect on results):
- * DPT_TUNE_DECODE_TILE = tasks per workgroup of the decode kernels, 8 or 16.  */
+ * DPT_TUNE_DECODE_TILE = tasks per workgroup of the decode kernels, 8 (default:
+ * two workgroups per CU) or 16.  */
 #define DPT_TUNE_DECODE_TILE 1
 int dpt_tuning_set(int32_t key, int64_t value);
 /* number of visible gfx950 devices (0 on a CPU-only host; never faults) */
