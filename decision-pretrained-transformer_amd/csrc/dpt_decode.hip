@@ -324,11 +324,13 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                         S.q[t][col] = v;
                     } else if (col < 2 * kE) {
                         S.kcur[t][col - kE] = v;
-                        if (task < N) kv[li * lstride + ((size_t)task * max_pos + pos) * kE + col - kE] = v;
+                        if (task < N)  // non-temporal like the stream that reads it back
+                            __builtin_nontemporal_store(v, kv + li * lstride + ((size_t)task * max_pos + pos) * kE + col - kE);
                     } else {
                         S.vcur[t][col - 2 * kE] = v;
                         if (task < N)
-                            kv[vhalf + li * lstride + ((size_t)task * max_pos + pos) * kE + col - 2 * kE] = v;
+                            __builtin_nontemporal_store(
+                                v, kv + vhalf + li * lstride + ((size_t)task * max_pos + pos) * kE + col - 2 * kE);
                     }
                 }
             }
