@@ -168,6 +168,30 @@ struct FragSrc {
     __device__ FragSrc layer(int l) const { return FragSrc{r, l * FragOff::size * 4}; }
 };
 
+// Cross-lane-group reductions with the gfx950 VALU permutes instead of
+// ds_bpermute: v_permlane16_swap / v_permlane32_swap applied to (v, v) return
+// the lane's own value and its xor-16 / xor-32 partner (in an order that
+// depends on the lane), so a symmetric op of the pair is the same on both.
+__device__ inline float sum_x16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float sum_x32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float max_x16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ inline float max_x32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+// sum / max over the 4 lane groups (the 4 feature slices of a token column)
+__device__ inline float sum_cols(float v) { return sum_x32(sum_x16(v)); }
+__device__ inline float max_cols(float v) { return max_x32(max_x16(v)); }
+
 __device__ inline void bar_lds_dr() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
@@ -182,8 +206,7 @@ __device__ inline void ln_cols(const float (&v)[8], float (&out)[8], const float
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += v[k];
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
+    s = sum_cols(s);
     const float mean = s * (1.0f / kE);
     float d[8], s2 = 0.f;
 #pragma unroll
@@ -191,8 +214,7 @@ __device__ inline void ln_cols(const float (&v)[8], float (&out)[8], const float
         d[k] = v[k] - mean;
         s2 += d[k] * d[k];
     }
-    s2 += __shfl_xor(s2, 16);
-    s2 += __shfl_xor(s2, 32);
+    s2 = sum_cols(s2);
     const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
     const floatx4 g0 = ld4(gam + 4 * g), g1 = ld4(gam + 16 + 4 * g);
     const floatx4 b0 = ld4(bet + 4 * g), b1 = ld4(bet + 16 + 4 * g);
@@ -352,11 +374,14 @@ __device__ inline void attend(const DrSmem& S, const float (&q)[8], int qb, int 
     for (int kb = 0; kb <= qb; ++kb) {
         const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
         const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
-        floatx4 sc = {0.f, 0.f, 0.f, 0.f};
+        // two independent 4-deep chains (features 0-15 / 16-31) instead of one 8-deep
+        floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) sc = mfma4(k0[s], q[s], sc);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) sc = mfma4(k1[s], q[4 + s], sc);
+        for (int s = 0; s < 4; ++s) {
+            sa = mfma4(k0[s], q[s], sa);
+            sb = mfma4(k1[s], q[4 + s], sb);
+        }
+        const floatx4 sc = sa + sb;
         float sv[4];
         float mt = -INFINITY;
 #pragma unroll
@@ -366,8 +391,7 @@ __device__ inline void attend(const DrSmem& S, const float (&q)[8], int qb, int 
             if ((kb == qb && 4 * g + r > c) || key < key_lo) sv[r] = -INFINITY;
             mt = fmaxf(mt, sv[r]);
         }
-        mt = fmaxf(mt, __shfl_xor(mt, 16));
-        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        mt = max_cols(mt);
         const float mn = fmaxf(m, mt);
         const float base = mn == -INFINITY ? 0.f : mn;  // no key yet: keep 0, not NaN
         const float corr = __expf(m - base);
@@ -388,8 +412,7 @@ __device__ inline void attend(const DrSmem& S, const float (&q)[8], int qb, int 
 #pragma unroll
         for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
     }
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
+    lsum = sum_cols(lsum);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         o[r] = o0[r];
@@ -623,8 +646,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             sdot = fmaf(q[j][r], ka[r], sdot);
                             sdot = fmaf(q[j][4 + r], kc[r], sdot);
                         }
-                        sdot += __shfl_xor(sdot, 16);
-                        sdot += __shfl_xor(sdot, 32);
+                        sdot = sum_cols(sdot);
                         const float s0 = sdot * scale;
                         const float mt = S.l0m[tok], lt = S.l0l[tok];
                         const float mn = fmaxf(mt, s0);
@@ -723,25 +745,25 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         if (kt > qlast) break;
                         const floatx4 k0 = ld4(&S.K[kt * 16 + c][4 * g]);
                         const floatx4 k1 = ld4(&S.K[kt * 16 + c][16 + 4 * g]);
-                        floatx4 sc = {0.f, 0.f, 0.f, 0.f};
+                        floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) sc = mfma4(k0[s4], qa[s4], sc);
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) sc = mfma4(k1[s4], qc[s4], sc);
+                        for (int s4 = 0; s4 < 4; ++s4) {
+                            sa = mfma4(k0[s4], qa[s4], sa);
+                            sb = mfma4(k1[s4], qc[s4], sb);
+                        }
+                        const floatx4 sc = sa + sb;
                         float sv[4], mt = -INFINITY;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             sv[r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * scale : -INFINITY;
                             mt = fmaxf(mt, sv[r]);
                         }
-                        mt = fmaxf(mt, __shfl_xor(mt, 16));
-                        mt = fmaxf(mt, __shfl_xor(mt, 32));
+                        mt = max_cols(mt);
                         float pr[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - mt);
                         float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
-                        lt += __shfl_xor(lt, 16);
-                        lt += __shfl_xor(lt, 32);
+                        lt = sum_cols(lt);
                         const floatx4 v0 = ld4(&S.Vt[c][kt * 16 + 4 * g]);
                         const floatx4 v1 = ld4(&S.Vt[16 + c][kt * 16 + 4 * g]);
                         floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
@@ -850,8 +872,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             const int d = 16 * (k >> 2) + 4 * g + (k & 3);
                             part = fmaf(xf[k], P[pt.head_w + d * kDrA + a], part);
                         }
-                        part += __shfl_xor(part, 16);
-                        part += __shfl_xor(part, 32);
+                        part = sum_cols(part);
                         lg[a] = part + P[pt.head_b + a];
                     }
                     if (lane == 0) {

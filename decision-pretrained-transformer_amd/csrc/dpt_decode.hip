@@ -150,6 +150,17 @@ __device__ inline float gelu_new(float x) {
     return 0.5f * x * (1.0f + tanhf(inner));
 }
 
+// Sum over the 8 lanes of an aligned lane group with DPP (VALU, no LDS
+// round trip): xor 1 and xor 2 by quad_perm, then row_half_mirror pairs the two
+// quads of the group.  Every lane of the group gets the same value, bit-identical
+// to the xor-1/2/4 shuffle butterfly.
+__device__ inline float dpp_sum8(float d) {
+    d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0xB1, 0xF, 0xF, false));
+    d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x4E, 0xF, 0xF, false));
+    d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x141, 0xF, 0xF, false));
+    return d;
+}
+
 // Flash-decoding attention of one task (one wave): positions 0..pos-1 from the
 // cache (global), position pos from LDS.  Writes o = softmax(qK^T/sqrt(E)) V.
 __device__ inline void attend_one(const float* __restrict__ kc, const float* __restrict__ vc, int pos,
@@ -185,9 +196,7 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
             d = fmaf(q4.y, kk[r].y, d);
             d = fmaf(q4.z, kk[r].z, d);
             d = fmaf(q4.w, kk[r].w, d);
-            d += __shfl_xor(d, 1);
-            d += __shfl_xor(d, 2);
-            d += __shfl_xor(d, 4);
+            d = dpp_sum8(d);
             const int p = base + 8 * r + g;
             s[r] = (p < pos) ? d * scale : -INFINITY;
             mx = fmaxf(mx, s[r]);
@@ -214,9 +223,7 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
         d = fmaf(q4.y, k4.y, d);
         d = fmaf(q4.z, k4.z, d);
         d = fmaf(q4.w, k4.w, d);
-        d += __shfl_xor(d, 1);
-        d += __shfl_xor(d, 2);
-        d += __shfl_xor(d, 4);
+        d = dpp_sum8(d);
         if (g == 0) {
             const float sc = d * scale;
             const float mn = fmaxf(m, sc);

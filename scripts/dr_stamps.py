@@ -42,10 +42,7 @@ for N in (256, 512, 4096):
     lib.dpt_debug_dr_stamps(ctypes.addressof(buf), 32, 0)
     v = np.array(buf[:2 * L + 2], dtype=np.float64) / (Heps * 100)
     res = {n: round(float(x)) for n, x in zip(names, v) if x > 0}
-    extra = np.array(buf[16:18], dtype=np.float64) / (Heps * 100)
-    res["wave0:ln2+mlp (layers 1..L-2)"] = round(float(extra[0]))
-    res["wave0:ln1+c_attn (layers 1..L-1)"] = round(float(extra[1]))
-    res["total_cycles_per_step"] = round(float(v.sum() + extra.sum()))
+    res["total_cycles_per_step"] = round(float(v.sum()))
     res["wall_s"] = dt
     res["env_steps_per_s"] = N * Heps * 100 / dt
     out[N] = res
