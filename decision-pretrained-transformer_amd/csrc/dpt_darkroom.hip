@@ -558,7 +558,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         P[pt.emb_b + i] = M.emb_b[i];
         P[pt.wpe0 + i] = M.wpe[i];
     }
-    for (int i = tid; i < kE * kDrA; i += blockDim.x) P[pt.head_w + i] = M.head_w[i];
+    for (int i = tid; i < kE * kDrA; i += blockDim.x)  // transposed to [a][E] for 16-B reads
+        P[pt.head_w + (i % kDrA) * kE + i / kDrA] = M.head_w[i];
     for (int i = tid; i < kDrA; i += blockDim.x) P[pt.head_b + i] = M.head_b[i];
     for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
 
@@ -730,6 +731,18 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             {
                 const float* W = P + (L - 1) * PL::size;
                 const FragSrc fs = frag0.layer(L - 1);
+                // this wave's tail weight fragments, in flight across the first barrier
+                floatx4 pw[4], fw[2][2], mw[2][2];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) pw[k] = fs.ld(FragOff::proj, k);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int cj = wave + 4 * h;
+                    fw[h][0] = fs.ld(FragOff::fc, 2 * cj);
+                    fw[h][1] = fs.ld(FragOff::fc, 2 * cj + 1);
+                    mw[h][0] = fs.ld(FragOff::mp, cj);
+                    mw[h][1] = fs.ld(FragOff::mp, 8 + cj);
+                }
                 const int step = ep * p.horizon + t;
                 double u = 0.0;
                 if (p.sample && tid == 0)
@@ -814,8 +827,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
 #pragma unroll
                     for (int ob2 = 0; ob2 < 2; ++ob2) {
-                        const floatx4 acc = mfma32(fs.ld(FragOff::proj, 2 * ob2), fs.ld(FragOff::proj, 2 * ob2 + 1), o,
-                                                   ld4(W + PL::proj_b + ob2 * 16 + 4 * g));
+                        const floatx4 acc = mfma32(pw[2 * ob2], pw[2 * ob2 + 1], o, ld4(W + PL::proj_b + ob2 * 16 + 4 * g));
 #pragma unroll
                         for (int r = 0; r < 4; ++r) xl[ob2 * 4 + r] += acc[r];
                     }
@@ -824,11 +836,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int cj = wave + 4 * h;
-                        floatx4 hh = mfma32(fs.ld(FragOff::fc, 2 * cj), fs.ld(FragOff::fc, 2 * cj + 1), xn,
-                                            ld4(W + PL::fc_b + cj * 16 + 4 * g));
+                        floatx4 hh = mfma32(fw[h][0], fw[h][1], xn, ld4(W + PL::fc_b + cj * 16 + 4 * g));
 #pragma unroll
                         for (int r = 0; r < 4; ++r) hh[r] = gelu_fast(hh[r]);
-                        const floatx4 m0 = fs.ld(FragOff::mp, cj), m1 = fs.ld(FragOff::mp, 8 + cj);
+                        const floatx4 m0 = mw[h][0], m1 = mw[h][1];
                         floatx4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                         for (int s4 = 0; s4 < 4; ++s4) {
@@ -866,14 +877,15 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     float lg[kDrA];
 #pragma unroll
                     for (int a = 0; a < kDrA; ++a) {
+                        const floatx4 w0 = ld4(P + pt.head_w + a * kE + 4 * g);
+                        const floatx4 w1 = ld4(P + pt.head_w + a * kE + 16 + 4 * g);
                         float part = 0.f;
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            const int d = 16 * (k >> 2) + 4 * g + (k & 3);
-                            part = fmaf(xf[k], P[pt.head_w + d * kDrA + a], part);
+                        for (int r = 0; r < 4; ++r) {
+                            part = fmaf(xf[r], w0[r], part);
+                            part = fmaf(xf[4 + r], w1[r], part);
                         }
-                        part = sum_cols(part);
-                        lg[a] = part + P[pt.head_b + a];
+                        lg[a] = sum_cols(part) + P[pt.head_b + a];
                     }
                     if (lane == 0) {
                         const int a = select_fixed<kDrA>(lg, p.sample, p.temp, u);
