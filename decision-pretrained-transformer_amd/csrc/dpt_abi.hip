@@ -53,6 +53,9 @@ int launch_pack_fragments(const ModelView&, float*, hipStream_t);
 int64_t fragments_numel(int n_layer);
 int launch_rollout_darkroom(const ModelView&, const float*, const dpt_darkroom_rollout_args&, hipStream_t);
 int darkroom_max_window();
+int prefill_max_window();
+int launch_prefill(const ModelView&, const float*, const float*, const float*, const float*, const float*,
+                   const float*, int, int, int, float*, hipStream_t);
 int set_decode_tile(int);
 
 }  // namespace dpt
@@ -96,9 +99,16 @@ int dpt_abi_version(void) { return DPT_ABI_VERSION; }
 
 const char* dpt_last_error(void) { return g_last_error.c_str(); }
 
+static bool g_prefill = true;  // DPT_TUNE_PREFILL
+
 int dpt_tuning_set(int32_t key, int64_t value) {
     if (key == DPT_TUNE_DECODE_TILE) {
         REQUIRE(set_decode_tile((int)value) == DPT_OK, "decode tile %lld: 8 or 16", (long long)value);
+        return DPT_OK;
+    }
+    if (key == DPT_TUNE_PREFILL) {
+        REQUIRE(value == 0 || value == 1, "prefill %lld: 0 or 1", (long long)value);
+        g_prefill = value == 1;
         return DPT_OK;
     }
     set_error(DPT_EINVAL, "unknown tuning key %d", key);
@@ -184,8 +194,12 @@ int dpt_forward_window(const dpt_model* m, const float* query, const float* stat
     REQUIRE(C + 1 <= m->desc.n_positions, "context length %d + query exceeds n_positions=%d", C,
             m->desc.n_positions);
     REQUIRE(out_mode == 0 || (out_mode == 1 && C >= 1), "out_mode=%d with C=%d", out_mode, C);
-    REQUIRE(query && out && workspace, "null query/out/workspace");
+    REQUIRE(query && out, "null query/out");
     REQUIRE(C == 0 || (states && actions && next_states && rewards), "null context arrays with C=%d", C);
+    if (g_prefill && C + 1 <= prefill_max_window())  // all positions at once (MFMA)
+        return launch_prefill(m->view, m->frag, query, states, actions, next_states, rewards, N, C, out_mode, out,
+                              S(stream));
+    REQUIRE(workspace, "null workspace (needed for windows over %d tokens)", prefill_max_window());
     return launch_window_decode(m->view, workspace, N, C, query, states, actions, next_states, rewards, out_mode,
                                 out, S(stream));
 }

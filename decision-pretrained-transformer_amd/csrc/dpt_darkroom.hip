@@ -28,7 +28,7 @@
 //    attention (one key tile per wave, flash-merged), c_proj and MLP (one
 //    hidden chunk per wave) are spread over the waves, then ln_f + head +
 //    selection + the grid step run on one wave.
-#include "dpt_common.h"
+#include "dpt_mfma_fwd.h"
 
 // DPT_STAMPS (diagnostic build only): s_memtime at the barriers of a step,
 // accumulated by workgroup 0 thread 0 (see scripts/dr_stamps.py for the slots).
@@ -51,22 +51,8 @@ __device__ unsigned long long g_dr_last;
 
 namespace dpt {
 
-constexpr int kDrWaves = 4;                 // waves per workgroup
-constexpr int kDrBlocks = 8;                // 16-token blocks per window (two per wave)
-constexpr int kDrT = 16 * kDrBlocks;        // max window (1 + R*horizon)
-constexpr int kKStride = kE + 4;            // K[token][feature]
-constexpr int kVStride = kDrT + 4;          // Vt[feature][token]
 constexpr int kDrA = 5;                     // DarkRoom actions
 constexpr int kDrF = 10;                    // token features 2*sd + A + 1
-
-// Fragment-packed weights of one block (floats), see pack_fragments_kernel.
-struct FragOff {
-    static constexpr int attn = 0;            // [6 ob][2 q][64 lanes][4]
-    static constexpr int proj = attn + 3072;  // [2 ob][2 q][64][4]
-    static constexpr int fc = proj + 1024;    // [8 ob][2 q][64][4]
-    static constexpr int mp = fc + 4096;      // [2 ob][8 chunk][64][4]
-    static constexpr int size = mp + 4096;    // 12,288
-};
 
 // A-operand fragment of W^T for a k=32 input (W is [in][out], Conv1D layout):
 // lane l, k-step s reads W[16*(s>>2) + 4*(l>>4) + (s&3)][ob*16 + (l&15)];
@@ -101,12 +87,6 @@ __global__ void pack_fragments_kernel(ModelView M, float* __restrict__ frag) {
     }
 }
 
-// Small parameters copied to LDS once per launch (offsets in floats): per block
-// [ln1_g ln1_b attn_b proj_b ln2_g ln2_b fc_b mp_b], then the model-level ones.
-struct PL {
-    static constexpr int ln1_g = 0, ln1_b = 32, attn_b = 64, proj_b = 160, ln2_g = 192, ln2_b = 224,
-                         fc_b = 256, mp_b = 384, size = 416;
-};
 struct PTop {
     int lnf_g, lnf_b, head_w, head_b, emb_b, wpe0, emb_w, total;
     __host__ __device__ static PTop make(int L) {
@@ -125,300 +105,20 @@ struct PTop {
 };
 
 struct DrSmem {
-    float K[kDrT][kKStride];
-    float Vt[kE][kVStride];
-    int2 ctx[kDrT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
-    int2 cur[kDrT];   // this episode's transitions
+    KVLds kv;
+    int2 ctx[kFwdT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
+    int2 cur[kFwdT];   // this episode's transitions
     // layer-0 episode cache: the causal softmax partial of every token over keys
     // 1..t, unnormalised o^T in C-layout per (block, lane), m and l per token
-    float l0o[kDrBlocks][64][8];
-    float l0m[kDrT], l0l[kDrT];
+    float l0o[kFwdBlocks][64][8];
+    float l0m[kFwdT], l0l[kFwdT];
     float k0[kE], v0[kE];             // layer 0: key / value of the query token
     float ql[kE], xl[kE];             // last layer: q and residual of token T-1
-    float part_o[kDrBlocks][kE];      // last layer: per-key-tile attention partials
-    float part_m[kDrBlocks], part_l[kDrBlocks];
+    float part_o[kFwdBlocks][kE];      // last layer: per-key-tile attention partials
+    float part_m[kFwdBlocks], part_l[kFwdBlocks];
     float part_y[kFF / 16][kE];       // last layer: per-hidden-chunk MLP partials
     int sx, sy, ret, pad;
 };
-
-__device__ inline floatx4 mfma4(float a, float b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-__device__ inline floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
-
-// Lane index the compiler cannot hoist: every helper derives its lane-dependent
-// LDS addresses from this at its own start, so they are short-lived values
-// instead of loop invariants spilled across the whole rollout.
-__device__ inline int lane_id() {
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return t & 63;
-}
-
-// Fragment-packed weights through one buffer descriptor: the per-lane part of
-// every address is lane*16; layer, region and block offsets are scalar.
-struct FragSrc {
-    __amdgpu_buffer_rsrc_t r;
-    int base;  // byte offset of this layer's block
-    __device__ floatx4 ld(int region_floats, int k) const {
-        return __builtin_bit_cast(
-            floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, base + 4 * region_floats + k * 1024, 0));
-    }
-    __device__ FragSrc layer(int l) const { return FragSrc{r, l * FragOff::size * 4}; }
-};
-
-// Cross-lane-group reductions with the gfx950 VALU permutes instead of
-// ds_bpermute: v_permlane16_swap / v_permlane32_swap applied to (v, v) return
-// the lane's own value and its xor-16 / xor-32 partner (in an order that
-// depends on the lane), so a symmetric op of the pair is the same on both.
-__device__ inline float sum_x16(float v) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ inline float sum_x32(float v) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ inline float max_x16(float v) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ inline float max_x32(float v) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-// sum / max over the 4 lane groups (the 4 feature slices of a token column)
-__device__ inline float sum_cols(float v) { return sum_x32(sum_x16(v)); }
-__device__ inline float max_cols(float v) { return max_x32(max_x16(v)); }
-
-__device__ inline void bar_lds_dr() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// LayerNorm over the 32 features of each token column (eps 1e-5): a lane holds
-// 8 of them; the other 24 live in lanes l^16, l^32, l^48.
-__device__ inline void ln_cols(const float (&v)[8], float (&out)[8], const float* __restrict__ gam,
-                               const float* __restrict__ bet) {
-    const int g = lane_id() >> 4;
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s += v[k];
-    s = sum_cols(s);
-    const float mean = s * (1.0f / kE);
-    float d[8], s2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        d[k] = v[k] - mean;
-        s2 += d[k] * d[k];
-    }
-    s2 = sum_cols(s2);
-    const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
-    const floatx4 g0 = ld4(gam + 4 * g), g1 = ld4(gam + 16 + 4 * g);
-    const floatx4 b0 = ld4(bet + 4 * g), b1 = ld4(bet + 16 + 4 * g);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        out[r] = fmaf(d[r] * rstd, g0[r], b0[r]);
-        out[4 + r] = fmaf(d[4 + r] * rstd, g1[r], b1[r]);
-    }
-}
-
-__device__ inline float gelu_fast(float x) {
-    // gelu_new (transformers/activations.py:65): 0.5x(1 + tanh(z)) = x * sigmoid(2z)
-    // = x / (1 + 2^(x * (c1 + c2 x^2))), z = sqrt(2/pi)(x + 0.044715 x^3), log2(e) folded in
-    const float c1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
-    const float c2 = c1 * 0.044715f;
-    const float e = __builtin_amdgcn_exp2f(x * fmaf(x * x, c2, c1));
-    return x * __builtin_amdgcn_rcpf(1.0f + e);
-}
-
-// acc + W^T xin^T for a k=32 input held as 8 C-layout values, given fragments
-__device__ inline floatx4 mfma32(const floatx4& w0, const floatx4& w1, const float (&xin)[8], floatx4 acc) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma4(w0[s], xin[s], acc);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma4(w1[s], xin[4 + s], acc);
-    return acc;
-}
-
-// The same for the NB (1 or 2) blocks of a wave: one fragment load feeds NB
-// independent accumulation chains, interleaved.
-template <int NB>
-__device__ inline void mfma32n(const floatx4& w0, const floatx4& w1, const float (&xin)[2][8], floatx4 (&acc)[2]) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = mfma4(w0[s], xin[j][s], acc[j]);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = mfma4(w1[s], xin[j][4 + s], acc[j]);
-}
-
-template <int NB>
-__device__ inline void ln_n(const float (&x)[2][8], float (&xn)[2][8], const float* gam, const float* bet) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) ln_cols(x[j], xn[j], gam, bet);
-}
-
-// x^T += c_proj(o^T) (bias included)
-template <int NB>
-__device__ inline void attn_proj(const float* W, const FragSrc& fs, const float (&o)[2][8], float (&x)[2][8]) {
-    const int g = lane_id() >> 4;
-#pragma unroll
-    for (int ob = 0; ob < 2; ++ob) {
-        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g);
-        floatx4 acc[2] = {bias, bias};
-        mfma32n<NB>(fs.ld(FragOff::proj, 2 * ob), fs.ld(FragOff::proj, 2 * ob + 1), o, acc);
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) x[j][ob * 4 + r] += acc[j][r];
-    }
-}
-
-// x^T += MLP(xn^T) over the 8 hidden chunks, software-pipelined: the c_fc
-// MFMAs of chunk c+1 are issued interleaved with the gelu of chunk c (an MFMA
-// leaves most of its 32 issue cycles to independent vector instructions),
-// then chunk c's mlp.c_proj MFMAs.
-template <int NB>
-__device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn)[2][8], float (&x)[2][8]) {
-    const int g = lane_id() >> 4;
-    const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);
-    floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
-    floatx4 h[2];
-    {
-        const floatx4 fb = ld4(W + PL::fc_b + 4 * g);
-        h[0] = fb;
-        h[1] = fb;
-        mfma32n<NB>(fs.ld(FragOff::fc, 0), fs.ld(FragOff::fc, 1), xn, h);
-    }
-#pragma unroll
-    for (int c = 0; c < kFF / 16; ++c) {
-        const floatx4 b0 = fs.ld(FragOff::mp, c), b1 = fs.ld(FragOff::mp, 8 + c);
-        floatx4 hn[2] = {h[0], h[1]};
-        if (c + 1 < kFF / 16) {
-            const floatx4 fb = ld4(W + PL::fc_b + (c + 1) * 16 + 4 * g);
-            hn[0] = fb;
-            hn[1] = fb;
-            mfma32n<NB>(fs.ld(FragOff::fc, 2 * (c + 1)), fs.ld(FragOff::fc, 2 * (c + 1) + 1), xn, hn);
-        }
-        floatx4 gl[2];
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) gl[j][r] = gelu_fast(h[j][r]);
-        if (c + 1 < kFF / 16) {
-#pragma unroll
-            for (int k = 0; k < 8 * NB; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      // one c_fc(c+1) MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, 4 / NB, 0);  // gelu(c) VALU
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int j = 0; j < NB; ++j) {
-                y0[j] = mfma4(b0[s], gl[j][s], y0[j]);
-                y1[j] = mfma4(b1[s], gl[j][s], y1[j]);
-            }
-        h[0] = hn[0];
-        h[1] = hn[1];
-    }
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            x[j][r] += y0[j][r];
-            x[j][4 + r] += y1[j][r];
-        }
-}
-
-// c_attn output blocks [ob0, ob1) of (Q0 Q1 K0 K1 V0 V1) for the NB blocks qb[]:
-// Q stays in registers, K -> LDS token-major, V -> LDS feature-major.
-template <int NB>
-__device__ inline void c_attn_n(DrSmem& S, const float* W, const FragSrc& fs, const int (&qb)[2],
-                                const float (&xn)[2][8], float (&q)[2][8], int ob0, int ob1) {
-    for (int ob = ob0; ob < ob1; ++ob) {
-        const int lane = lane_id(), g = lane >> 4;
-        const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);
-        floatx4 acc[2] = {bias, bias};
-        mfma32n<NB>(fs.ld(FragOff::attn, 2 * ob), fs.ld(FragOff::attn, 2 * ob + 1), xn, acc);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const int tok = qb[j] * 16 + (lane & 15);
-            if (ob < 2) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) q[j][ob * 4 + r] = acc[j][r];
-            } else if (ob < 4) {
-                *reinterpret_cast<floatx4*>(&S.K[tok][16 * (ob - 2) + 4 * g]) = acc[j];
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) S.Vt[16 * (ob - 4) + 4 * g + r][tok] = acc[j][r];
-            }
-        }
-    }
-}
-
-// Causal flash attention of query block qb over keys [key_lo, 16*qb + c]:
-// per token column the running max m (-inf when no key), sum l and the
-// unnormalised o^T (C-layout).
-__device__ inline void attend(const DrSmem& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
-                              float& lsum, float (&o)[8]) {
-    const int lane = lane_id(), g = lane >> 4, c = lane & 15;
-    m = -INFINITY;
-    lsum = 0.f;
-    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-    for (int kb = 0; kb <= qb; ++kb) {
-        const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
-        const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
-        // two independent 4-deep chains (features 0-15 / 16-31) instead of one 8-deep
-        floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            sa = mfma4(k0[s], q[s], sa);
-            sb = mfma4(k1[s], q[4 + s], sb);
-        }
-        const floatx4 sc = sa + sb;
-        float sv[4];
-        float mt = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int key = kb * 16 + 4 * g + r;
-            sv[r] = sc[r] * scale;
-            if ((kb == qb && 4 * g + r > c) || key < key_lo) sv[r] = -INFINITY;
-            mt = fmaxf(mt, sv[r]);
-        }
-        mt = max_cols(mt);
-        const float mn = fmaxf(m, mt);
-        const float base = mn == -INFINITY ? 0.f : mn;  // no key yet: keep 0, not NaN
-        const float corr = __expf(m - base);
-        float pr[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - base);
-        lsum = lsum * corr + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
-        m = mn;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            o0[r] *= corr;
-            o1[r] *= corr;
-        }
-        const floatx4 v0 = ld4(&S.Vt[c][kb * 16 + 4 * g]);
-        const floatx4 v1 = ld4(&S.Vt[16 + c][kb * 16 + 4 * g]);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) o0 = mfma4(v0[s], pr[s], o0);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
-    }
-    lsum = sum_cols(lsum);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        o[r] = o0[r];
-        o[4 + r] = o1[r];
-    }
-}
 
 __device__ inline int2 pack_tr(int x, int y, int a, int nx, int ny, int r) {
     return make_int2(x | (y << 8) | (a << 16) | (r << 24), nx | (ny << 8));
@@ -473,17 +173,6 @@ struct DarkroomParams {
     const float* frag;
 };
 
-// Blocks of wave w: pairs (w, nqb-1-w), so a wave's causal attention rows sum
-// to the same length; the middle block of an odd count goes alone.  Returns
-// the number of blocks (0, 1 or 2).
-__device__ inline int blocks_of_wave(int w, int nqb, int (&qb)[2]) {
-    qb[0] = w;
-    qb[1] = nqb - 1 - w;
-    if (w < nqb / 2) return 2;
-    if ((nqb & 1) && w == nqb / 2) return 1;
-    return 0;
-}
-
 // Token embeddings of block qb (embed_transition + wpe, models/net.py:52-54):
 // the query [state, 0...] at position 0, context transitions after it, zeros
 // past the window.
@@ -513,19 +202,7 @@ __device__ inline void embed_block(const DrSmem& S, const float* P, const PTop& 
     }
 }
 
-// One phase over the wave's blocks, dispatched on their count (uniform per wave).
-#define DR_BLOCKS(nb, CALL) \
-    do {                    \
-        if ((nb) == 2) {    \
-            constexpr int NB = 2; \
-            CALL;           \
-        } else if ((nb) == 1) { \
-            constexpr int NB = 1; \
-            CALL;           \
-        }                   \
-    } while (0)
-
-__global__ void __launch_bounds__(kDrWaves * 64, 2)
+__global__ void __launch_bounds__(kFwdWaves * 64, 2)
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     __shared__ DrSmem S;
     extern __shared__ float P[];
@@ -538,20 +215,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     const PTop pt = PTop::make(L);
     const FragSrc frag0{__builtin_amdgcn_make_buffer_rsrc((void*)p.frag, (short)0, L * FragOff::size * 4, 0x00020000),
                         0};
-    for (int i = tid; i < L * PL::size; i += blockDim.x) {
-        const int l = i / PL::size, k = i % PL::size;
-        const float* Wg = M.layers + (size_t)l * LayerOff::size;
-        float v;
-        if (k < PL::ln1_b) v = Wg[LayerOff::ln1_g + k];
-        else if (k < PL::attn_b) v = Wg[LayerOff::ln1_b + k - PL::ln1_b];
-        else if (k < PL::proj_b) v = Wg[LayerOff::attn_b + k - PL::attn_b];
-        else if (k < PL::ln2_g) v = Wg[LayerOff::proj_b + k - PL::proj_b];
-        else if (k < PL::ln2_b) v = Wg[LayerOff::ln2_g + k - PL::ln2_g];
-        else if (k < PL::fc_b) v = Wg[LayerOff::ln2_b + k - PL::ln2_b];
-        else if (k < PL::mp_b) v = Wg[LayerOff::fc_b + k - PL::fc_b];
-        else v = Wg[LayerOff::mp_b + k - PL::mp_b];
-        P[i] = v;
-    }
+    load_layer_params(P, M, tid, blockDim.x);
     for (int i = tid; i < kE; i += blockDim.x) {
         P[pt.lnf_g + i] = M.lnf_g[i];
         P[pt.lnf_b + i] = M.lnf_b[i];
@@ -583,14 +247,14 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
-            DR_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                           c_attn_n<NB>(S, P, frag0, qb, xn, q, 0, 6)));
-            bar_lds_dr();
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
+                           c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 6)));
+            bar_lds();
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 if (j >= nb) break;
                 float m, l, o[8];
-                attend(S, q[j], qb[j], 1, scale, m, l, o);
+                attend(S.kv, q[j], qb[j], 1, scale, m, l, o);
                 const int lane = lane_id();
                 *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][0]) = {o[0], o[1], o[2], o[3]};
                 *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][4]) = {o[4], o[5], o[6], o[7]};
@@ -614,22 +278,22 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 float q[2][8];
                 {
                     float xn[2][8];
-                    DR_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                                   c_attn_n<NB>(S, P, frag0, qb, xn, q, 0, 2)));
+                    DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
+                                   c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 2)));
                     if (wave == 0) {  // block 0 (slot 0 of wave 0): key/value of the query token
-                        c_attn_n<1>(S, P, frag0, qb, xn, q, 2, 6);
+                        c_attn_n<1>(S.kv, P, frag0, qb, xn, q, 2, 6);
                         const int lane = lane_id();
                         if ((lane & 15) == 0) {
 #pragma unroll
                             for (int k = 0; k < 8; ++k) {
                                 const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
-                                S.k0[d] = S.K[0][d];
-                                S.v0[d] = S.Vt[d][0];
+                                S.k0[d] = S.kv.K[0][d];
+                                S.v0[d] = S.kv.Vt[d][0];
                             }
                         }
                     }
                 }
-                bar_lds_dr();
+                bar_lds();
                 DR_STAMP(0);
                 if (nb > 0) {
                     // merge key 0 into the cached partial of every token column
@@ -661,7 +325,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                     }
                     float xn[2][8];
-                    DR_BLOCKS(nb, (attn_proj<NB>(P, frag0, o, x), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                    DPT_BLOCKS(nb, (attn_proj<NB>(P, frag0, o, x), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
                                    mlp_n<NB>(P, frag0, xn, x)));
                 }
                 DR_STAMP(1);
@@ -675,12 +339,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 {
                     float xn[2][8];
                     if (!last) {
-                        DR_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       c_attn_n<NB>(S, W, fs, qb, xn, q, 0, 6)));
+                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
+                                       c_attn_n<NB>(S.kv, W, fs, qb, xn, q, 0, 6)));
                     } else {
                         // the last layer needs q only for token T-1 (block qlast)
-                        DR_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       c_attn_n<NB>(S, W, fs, qb, xn, q, 2, 6)));
+                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
+                                       c_attn_n<NB>(S.kv, W, fs, qb, xn, q, 2, 6)));
 #pragma unroll
                         for (int j = 0; j < 2; ++j) {
                             if (j < nb && qb[j] == qlast) {
@@ -688,7 +352,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                                 float xn1[2][8], q1[2][8];
 #pragma unroll
                                 for (int k = 0; k < 8; ++k) xn1[0][k] = xn[j][k];
-                                c_attn_n<1>(S, W, fs, one, xn1, q1, 0, 2);
+                                c_attn_n<1>(S.kv, W, fs, one, xn1, q1, 0, 2);
                                 const int lane = lane_id();
                                 if ((lane & 15) == clast) {
 #pragma unroll
@@ -702,7 +366,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                     }
                 }
-                bar_lds_dr();
+                bar_lds();
                 DR_STAMP(2 * layer);
                 if (last) break;
                 if (nb > 0) {
@@ -711,18 +375,18 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     for (int j = 0; j < 2; ++j) {
                         if (j >= nb) break;
                         float m, l;
-                        attend(S, q[j], qb[j], 0, scale, m, l, o[j]);
+                        attend(S.kv, q[j], qb[j], 0, scale, m, l, o[j]);
                         const float inv = 1.0f / l;
 #pragma unroll
                         for (int k = 0; k < 8; ++k) o[j][k] *= inv;
                     }
-                    DR_BLOCKS(nb, attn_proj<NB>(W, fs, o, x));
+                    DPT_BLOCKS(nb, attn_proj<NB>(W, fs, o, x));
                 }
-                bar_lds_dr();  // every read of this layer's K/V is done
+                bar_lds();  // every read of this layer's K/V is done
                 DR_STAMP(2 * layer + 1);
                 {
                     float xn[2][8];
-                    DR_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b), mlp_n<NB>(W, fs, xn, x)));
+                    DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b), mlp_n<NB>(W, fs, xn, x)));
                 }
             }
 
@@ -756,8 +420,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     for (int h = 0; h < 2; ++h) {
                         const int kt = wave + 4 * h;
                         if (kt > qlast) break;
-                        const floatx4 k0 = ld4(&S.K[kt * 16 + c][4 * g]);
-                        const floatx4 k1 = ld4(&S.K[kt * 16 + c][16 + 4 * g]);
+                        const floatx4 k0 = ld4(&S.kv.K[kt * 16 + c][4 * g]);
+                        const floatx4 k1 = ld4(&S.kv.K[kt * 16 + c][16 + 4 * g]);
                         floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                         for (int s4 = 0; s4 < 4; ++s4) {
@@ -777,8 +441,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - mt);
                         float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
                         lt = sum_cols(lt);
-                        const floatx4 v0 = ld4(&S.Vt[c][kt * 16 + 4 * g]);
-                        const floatx4 v1 = ld4(&S.Vt[16 + c][kt * 16 + 4 * g]);
+                        const floatx4 v0 = ld4(&S.kv.Vt[c][kt * 16 + 4 * g]);
+                        const floatx4 v1 = ld4(&S.kv.Vt[16 + c][kt * 16 + 4 * g]);
                         floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                         for (int s4 = 0; s4 < 4; ++s4) o0 = mfma4(v0[s4], pr[s4], o0);
@@ -794,7 +458,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                     }
                 }
-                bar_lds_dr();
+                bar_lds();
                 DR_STAMP(2 * L - 1);
                 // (2) every wave: merge the partials, c_proj + residual, ln_2, then
                 // MLP hidden chunks wave and wave+4
@@ -852,7 +516,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                     }
                 }
-                bar_lds_dr();
+                bar_lds();
                 DR_STAMP(2 * L);
                 // (3) wave 0: residual, ln_f, head, selection, env step
                 if (wave == 0) {
@@ -909,7 +573,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
                 }
             }
-            bar_lds_dr();
+            bar_lds();
             DR_STAMP(2 * L + 1);
         }
 
@@ -974,11 +638,11 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     if (dyn > 64 * 1024)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rollout_darkroom_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-    hipLaunchKernelGGL(rollout_darkroom_kernel, dim3(a.N), dim3(kDrWaves * 64), dyn, st, M, p);
+    hipLaunchKernelGGL(rollout_darkroom_kernel, dim3(a.N), dim3(kFwdWaves * 64), dyn, st, M, p);
     return check_hip(hipGetLastError(), "rollout_darkroom_kernel launch");
 }
 
-int darkroom_max_window() { return kDrT; }
+int darkroom_max_window() { return kFwdT; }
 
 }  // namespace dpt
 

@@ -124,7 +124,8 @@ class DeviceModel:
             cs_ = ca_ = cn_ = cr_ = None
         out = torch.empty((N, self.action_dim) if out_mode == 0 else (N, C, self.action_dim),
                           dtype=torch.float32, device=dev)
-        ws = torch.empty(self.kv_numel(N, C + 1), dtype=torch.float32, device=dev)
+        ws = (None if _prefill[0] and C + 1 <= _lib.PREFILL_MAX_WINDOW
+              else torch.empty(self.kv_numel(N, C + 1), dtype=torch.float32, device=dev))
         _lib.call("dpt_forward_window", self._h, _p(q), _p(cs_), _p(ca_), _p(cn_), _p(cr_), N, C,
                   int(out_mode), _p(out), _p(ws), _stream())
         return out
@@ -329,3 +330,12 @@ def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=Tr
 def set_decode_tile(tile):
     """Tasks per workgroup of the decode kernels (8: two workgroups per CU; 16: one)."""
     _lib.call("dpt_tuning_set", _lib.TUNE_DECODE_TILE, int(tile))
+
+
+_prefill = [True]
+
+
+def set_prefill(on):
+    """Windows of <= PREFILL_MAX_WINDOW tokens as one MFMA prefill (default) or position by position."""
+    _lib.call("dpt_tuning_set", _lib.TUNE_PREFILL, int(bool(on)))
+    _prefill[0] = bool(on)

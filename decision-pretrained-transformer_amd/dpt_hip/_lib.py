@@ -27,6 +27,7 @@ BANDIT_F32 = 16
 STREAM_SELECT = 0
 STREAM_REWARD = 1
 STREAM_ROLLIN = 2
+STREAM_POLICY = 16  # + arm index (baseline-policy draws)
 
 _c_void_p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -145,6 +146,8 @@ SIGNATURES.update({
 })
 
 TUNE_DECODE_TILE = 1
+TUNE_PREFILL = 2
+PREFILL_MAX_WINDOW = 128  # DPT_PREFILL_MAX_WINDOW
 SIGNATURES["dpt_tuning_set"] = (_i32, [_i32, _i64])
 
 

@@ -62,10 +62,14 @@ extern "C" {
 
 int dpt_abi_version(void);
 const char* dpt_last_error(void);
-/* Process-wide tuning knobs (no effect on results):
+/* Process-wide tuning knobs (no effect on results beyond fp32 summation order):
  * DPT_TUNE_DECODE_TILE = tasks per workgroup of the decode kernels, 8 (default:
- * two workgroups per CU) or 16.  */
+ * two workgroups per CU) or 16.
+ * DPT_TUNE_PREFILL = 1 (default): dpt_forward_window runs windows of up to
+ * DPT_PREFILL_MAX_WINDOW tokens as one MFMA prefill; 0: always position by
+ * position through the K/V workspace.  */
 #define DPT_TUNE_DECODE_TILE 1
+#define DPT_TUNE_PREFILL 2
 int dpt_tuning_set(int32_t key, int64_t value);
 /* number of visible gfx950 devices (0 on a CPU-only host; never faults) */
 int dpt_device_count(int* count_out_host);
@@ -114,9 +118,12 @@ int dpt_forward_window(const dpt_model* model, const float* query, const float* 
                        const float* actions, const float* next_states, const float* rewards,
                        int32_t N, int32_t C, int32_t out_mode, float* out, float* workspace,
                        void* stream);
-/* `workspace` holds dpt_kvcache_numel(model, N, C + 1) floats: the window is
- * evaluated causally, position by position, through a K/V cache (identical to
- * the full causal recompute; each row attends to rows <= itself).            */
+/* Windows of T = C + 1 <= DPT_PREFILL_MAX_WINDOW tokens run as one MFMA prefill
+ * (all positions at once, one workgroup per sequence) and `workspace` may be
+ * NULL.  Longer windows are evaluated causally, position by position, through
+ * a K/V cache in `workspace` (dpt_kvcache_numel(model, N, C + 1) floats);
+ * both are the full causal forward (each row attends to rows <= itself).     */
+#define DPT_PREFILL_MAX_WINDOW 128
 
 /* ------------------------------------------------------------------ KV-cache decode
  * Exact incremental form of the growing-window forward used by the bandit

@@ -106,3 +106,17 @@ def test_product_path_has_no_oracle_import():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, flags=re.M), f
+
+
+def test_header_constants_match_binding():
+    """Every numeric #define DPT_* of include/dpt_hip.h has the same value in dpt_hip._lib
+    (DPT_X -> X, or DPT_X itself for the error codes)."""
+    from dpt_hip import _lib
+    defs = dict(re.findall(r"^#define DPT_(\w+)\s+\(?(-?\d+)\)?", open(HEADER).read(), re.M))
+    assert len(defs) >= 20
+    for name, val in defs.items():
+        if name == "HIP_H":
+            continue
+        py = getattr(_lib, "DPT_" + name, getattr(_lib, name, None))
+        assert py is not None, name
+        assert int(py) == int(val), (name, py, val)

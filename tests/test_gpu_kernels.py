@@ -141,9 +141,14 @@ def test_decode_steps_equal_window():
     kv = torch.empty(m.kv_numel(N, C + 1), dtype=torch.float32, device=dpt_hip.device())
     for p in range(C + 1):
         lg = m.decode_step(kv, C + 1, p, seq[:, p]).cpu().numpy()
-    win = m.forward_window(q, cs, ca, cn, cr).cpu().numpy()
+    try:  # the position-by-position window path is the same arithmetic as the decode steps
+        dpt_hip.set_prefill(False)
+        win = m.forward_window(q, cs, ca, cn, cr).cpu().numpy()
+    finally:
+        dpt_hip.set_prefill(True)
     assert np.array_equal(lg, win)
     assert_logits(lg, g["T101/logits"])
+    assert_logits(m.forward_window(q, cs, ca, cn, cr).cpu().numpy(), lg)  # MFMA prefill: summation order differs
 
 
 @pytest.mark.parametrize("tag", ["sample", "greedy", "var0"])
@@ -305,3 +310,32 @@ def test_rollout_darkroom_large_properties():
         assert_logits(lg[100 + t], w)
         ns, _ = O.darkroom_transit(st, acts[:, 100 + t], goals[:64])
         st = ns
+
+
+def test_prefill_equals_positionwise_window():
+    """The MFMA prefill (windows <= 128 tokens) and the position-by-position K/V path give the
+    same logits (out_mode 0 and 1) on random contexts of every model; both within the bar
+    of the reference's recorded logits where fixtures exist."""
+    import dpt_hip
+    rs = np.random.RandomState(21)
+    for name in ("bandit5", "darkroom", "linear20"):
+        g, m, _ = model_from_golden(name)
+        H, sd, A, L, E = (int(x) for x in g["cfg"])
+        for N, C in ((3, 0), (37, 5), (64, 100), (17, 127)):
+            if C + 1 > 4 * (1 + H):
+                continue
+            q = rs.randn(N, sd).astype(np.float32)
+            cs, cn = rs.randn(N, C, sd).astype(np.float32), rs.randn(N, C, sd).astype(np.float32)
+            ca = np.eye(A, dtype=np.float32)[rs.randint(0, A, (N, C))]
+            cr = rs.randn(N, C).astype(np.float32)
+            outs = []
+            try:
+                for on in (True, False):
+                    dpt_hip.set_prefill(on)
+                    for mode in ((0, 1) if C else (0,)):
+                        outs.append(m.forward_window(q, cs, ca, cn, cr, out_mode=mode).cpu().numpy())
+            finally:
+                dpt_hip.set_prefill(True)
+            half = len(outs) // 2
+            for a, b in zip(outs[:half], outs[half:]):
+                assert_logits(a, b)
