@@ -339,3 +339,24 @@ def test_prefill_equals_positionwise_window():
             half = len(outs) // 2
             for a, b in zip(outs[:half], outs[half:]):
                 assert_logits(a, b)
+
+
+def test_rollout_bernoulli_philox_vs_oracle():
+    """Fused rollout with Bernoulli rewards (r = u < mean, envs/gpu_bandit_env.py:58-61): Philox
+    draws through the kernel equal the oracle fed the same uniforms."""
+    d = dh()
+    _, m, W = model_from_golden("bandit5")
+    rs = np.random.RandomState(8)
+    N, H, seed = 20, 24, 4242
+    means = rs.beta(1, 1, (N, 5))
+    out = m.rollout_bandit(means, H, 0.0, True, bandit_type=d.BANDIT_BERNOULLI, seed=seed, want_logits=True)
+    u = np.stack([philox_np.uniform(seed, h, np.arange(N), d.STREAM_SELECT) for h in range(H)])
+    gu = np.stack([d.draw(0, seed, h, 0, N, d.STREAM_REWARD).cpu().numpy() for h in range(H)])
+    ref = O.bandit_online_rollout(W, means, H, 0.0, u, gu, True, bernoulli=True)
+    margin = O.boundary_margin(O.softmax_f32(ref["logits"]), u)
+    k = H if not (margin < 1e-5).any() else int(np.argmax((margin < 1e-5).any(-1)))
+    assert_logits(out["logits"].cpu().numpy()[:k + 1], ref["logits"][:k + 1])
+    if k == H:
+        assert np.array_equal(out["actions"].cpu().numpy(), ref["actions"])
+        assert np.array_equal(out["rewards"].cpu().numpy(), ref["rewards"])
+        assert set(np.unique(out["rewards"].cpu().numpy())) <= {0.0, 1.0}
