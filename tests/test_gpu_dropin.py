@@ -1,5 +1,7 @@
 """The reference-named drop-in layer (envs/, ctrls/, evals/, models/, collect_data) on the GPU,
 against golden vectors recorded from the reference and the oracle."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -246,3 +248,39 @@ def test_gpu_bandit_env():
         env.step(us)
     m = env.means[torch.arange(64), us.argmax(1)]
     assert float((r - m).abs().max()) < 0.3 * 6
+
+
+def test_cli_collect_then_eval(tmp_path, monkeypatch):
+    """The reference command lines end to end (run_bandit.sh / run_darkroom.sh shape, small sizes):
+    collect_data.py writes its dataset pickles under datasets/, a checkpoint of a fresh
+    Transformer loads strictly, and eval.py runs online/offline evaluation and writes its figures."""
+    import glob
+    import importlib
+
+    import matplotlib
+    matplotlib.use("Agg")
+    import collect_data
+    from models.net import Transformer
+    ev = importlib.import_module("eval")
+    monkeypatch.chdir(tmp_path)
+    runs = [
+        ("bandit", 1, 5, ["--envs", "50", "--envs_eval", "8", "--H", "20", "--dim", "5", "--var", "0.3"],
+         ["--n_eval", "8"]),
+        ("linear_bandit", 1, 5, ["--envs", "50", "--envs_eval", "8", "--H", "20", "--dim", "5", "--lin_d", "2",
+                                 "--var", "0.3"], ["--n_eval", "8"]),
+        ("darkroom_heldout", 2, 5, ["--envs", "100", "--H", "20", "--dim", "10"], ["--n_eval", "100"]),
+    ]
+    for env, sd, A, data_args, eval_args in runs:
+        collect_data.main(["--env", env] + data_args)
+        assert len(glob.glob(f"datasets/*{env}*")) == 3, env
+        H = int(data_args[data_args.index("--H") + 1])
+        torch.manual_seed(0)
+        model = Transformer(dict(horizon=H, state_dim=sd, action_dim=A, n_layer=3, n_embd=32, n_head=1,
+                                 dropout=0.0, test=True))
+        ckpt = tmp_path / f"{env}.pt"
+        torch.save(model.state_dict(), ckpt)
+        ev.main(["--env", env, "--checkpoint", str(ckpt)] + data_args + eval_args)
+        figs = glob.glob("figs/evals_epoch-1/*/*.png")
+        assert len(figs) >= 2, (env, figs)
+        for f in figs:
+            os.remove(f)
