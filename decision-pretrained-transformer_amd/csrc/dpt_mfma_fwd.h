@@ -60,8 +60,13 @@ struct FragSrc {
     __amdgpu_buffer_rsrc_t r;
     int base;  // byte offset of this layer's block
     __device__ floatx4 ld(int region_floats, int k) const {
+#ifdef DPT_FRAG_L1  // timing-only diagnostic build: every fragment load hits the first 4 KB (wrong results)
+        return __builtin_bit_cast(
+            floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, (base + 4 * region_floats + k * 1024) & 3072, 0));
+#else
         return __builtin_bit_cast(
             floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, base + 4 * region_floats + k * 1024, 0));
+#endif
     }
     __device__ FragSrc layer(int l) const { return FragSrc{r, l * FragOff::size * 4}; }
 };

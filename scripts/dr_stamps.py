@@ -12,7 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "decision-pretrained-transformer_amd"), ROOT]
 from dpt_hip import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(os.path.dirname(_lib.__file__), "libdpt_hip_stamps.so")
+_lib.LIB_PATH = os.path.join(os.path.dirname(_lib.__file__),
+                             os.environ.get("DPT_STAMPS_LIB", "libdpt_hip_stamps.so"))
 lib = _lib.load()
 lib.dpt_debug_dr_stamps.restype = ctypes.c_int
 lib.dpt_debug_dr_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
