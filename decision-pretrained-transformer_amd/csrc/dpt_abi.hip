@@ -53,7 +53,7 @@ int launch_pack_fragments(const ModelView&, float*, hipStream_t);
 int64_t fragments_numel(int n_layer);
 int launch_rollout_darkroom(const ModelView&, const float*, const dpt_darkroom_rollout_args&, hipStream_t);
 int darkroom_max_window();
-int prefill_max_window();
+int prefill_max_window(const ModelView&);
 int launch_prefill(const ModelView&, const float*, const float*, const float*, const float*, const float*,
                    const float*, int, int, int, float*, hipStream_t);
 int set_decode_tile(int);
@@ -186,6 +186,12 @@ int dpt_kvcache_numel(const dpt_model* m, int32_t N, int32_t max_pos, int64_t* n
     return DPT_OK;
 }
 
+int dpt_prefill_max_window(const dpt_model* m, int32_t* out) {
+    REQUIRE(m && out, "null model/out");
+    *out = g_prefill ? prefill_max_window(m->view) : 0;
+    return DPT_OK;
+}
+
 int dpt_forward_window(const dpt_model* m, const float* query, const float* states, const float* actions,
                        const float* next_states, const float* rewards, int32_t N, int32_t C, int32_t out_mode,
                        float* out, float* workspace, void* stream) {
@@ -196,10 +202,10 @@ int dpt_forward_window(const dpt_model* m, const float* query, const float* stat
     REQUIRE(out_mode == 0 || (out_mode == 1 && C >= 1), "out_mode=%d with C=%d", out_mode, C);
     REQUIRE(query && out, "null query/out");
     REQUIRE(C == 0 || (states && actions && next_states && rewards), "null context arrays with C=%d", C);
-    if (g_prefill && C + 1 <= prefill_max_window())  // all positions at once (MFMA)
+    if (g_prefill && C + 1 <= prefill_max_window(m->view))  // all positions at once (MFMA)
         return launch_prefill(m->view, m->frag, query, states, actions, next_states, rewards, N, C, out_mode, out,
                               S(stream));
-    REQUIRE(workspace, "null workspace (needed for windows over %d tokens)", prefill_max_window());
+    REQUIRE(workspace, "null workspace (needed for windows over %d tokens)", prefill_max_window(m->view));
     return launch_window_decode(m->view, workspace, N, C, query, states, actions, next_states, rewards, out_mode,
                                 out, S(stream));
 }

@@ -16,7 +16,7 @@ constexpr int kFwdWaves = 4;                 // waves per workgroup
 constexpr int kFwdBlocks = 8;                // 16-token blocks per window (two per wave)
 constexpr int kFwdT = 16 * kFwdBlocks;        // max window
 constexpr int kKStride = kE + 4;            // K[token][feature]
-constexpr int kVStride = kFwdT + 4;          // Vt[feature][token]
+constexpr int kVStride = kFwdT + 4;          // Vt[feature][token] (128-token buffer)
 
 // Fragment-packed weights of one block (floats), see pack_fragments_kernel.
 struct FragOff {
@@ -33,11 +33,13 @@ struct PL {
     static constexpr int ln1_g = 0, ln1_b = 32, attn_b = 64, proj_b = 160, ln2_g = 192, ln2_b = 224,
                          fc_b = 256, mp_b = 384, size = 416;
 };
-// This workgroup's keys and values of the current layer.
-struct KVLds {
-    float K[kFwdT][kKStride];
-    float Vt[kE][kVStride];
+// This workgroup's keys and values of the current layer, for windows of up to TMAX tokens.
+template <int TMAX>
+struct KVBuf {
+    float K[TMAX][kKStride];
+    float Vt[kE][TMAX + 4];
 };
+using KVLds = KVBuf<kFwdT>;
 
 __device__ inline floatx4 mfma4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -241,8 +243,8 @@ __device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn
 
 // c_attn output blocks [ob0, ob1) of (Q0 Q1 K0 K1 V0 V1) for the NB blocks qb[]:
 // Q stays in registers, K -> LDS token-major, V -> LDS feature-major.
-template <int NB>
-__device__ inline void c_attn_n(KVLds& S, const float* W, const FragSrc& fs, const int (&qb)[2],
+template <int NB, class KV>
+__device__ inline void c_attn_n(KV& S, const float* W, const FragSrc& fs, const int (&qb)[2],
                                 const float (&xn)[2][8], float (&q)[2][8], int ob0, int ob1) {
     for (int ob = ob0; ob < ob1; ++ob) {
         const int lane = lane_id(), g = lane >> 4;
@@ -268,7 +270,8 @@ __device__ inline void c_attn_n(KVLds& S, const float* W, const FragSrc& fs, con
 // Causal flash attention of query block qb over keys [key_lo, 16*qb + c]:
 // per token column the running max m (-inf when no key), sum l and the
 // unnormalised o^T (C-layout).
-__device__ inline void attend(const KVLds& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
+template <class KV>
+__device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
                               float& lsum, float (&o)[8]) {
     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
     m = -INFINITY;

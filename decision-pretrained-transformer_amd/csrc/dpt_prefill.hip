@@ -1,13 +1,15 @@
 // Window prefill on gfx950: Transformer.forward (models/net.py:41-60) for
 // windows of T = 1 + C <= 128 tokens, all positions at once.
 //
-// One workgroup (4 waves) per sequence; each wave owns two 16-token blocks and
+// One workgroup per sequence; each of its NW waves owns two 16-token blocks and
 // runs the transposed-dataflow MFMA forward of dpt_mfma_fwd.h: token packing
 // (net.py:42-54) + embed_transition + wpe, then per GPT-2 block ln_1 -> c_attn
 // -> causal attention -> c_proj -> residual -> ln_2 -> c_fc -> gelu_new ->
 // mlp.c_proj -> residual, then ln_f + pred_actions for the positions asked for
 // (out_mode 0: the last one, test=True; out_mode 1: positions 1..C, test=False).
-// Longer windows go to window_decode_kernel (dpt_decode.hip).
+// NW = 4, 8, 16 waves cover windows of 128, 256, 512 tokens (16 waves: K and V
+// of 512 tokens fill 140 KB of LDS, one workgroup per CU).  Longer windows go
+// to window_decode_kernel (dpt_decode.hip).
 #include "dpt_mfma_fwd.h"
 
 namespace dpt {
@@ -47,9 +49,10 @@ __device__ inline float token_feature(const PrefillArgs& a, int sd, int A, int n
     return a.rewards[j];
 }
 
-__global__ void __launch_bounds__(kFwdWaves * 64, 2)
+template <int NW>
+__global__ void __launch_bounds__(NW * 64, (NW + 3) / 4)
 prefill_kernel(ModelView M, PrefillArgs a) {
-    __shared__ KVLds S;
+    __shared__ KVBuf<32 * NW> S;
     extern __shared__ float P[];
     const int n = blockIdx.x;
     const int tid = threadIdx.x;
@@ -163,21 +166,37 @@ prefill_kernel(ModelView M, PrefillArgs a) {
     }
 }
 
-int prefill_max_window() { return kFwdT; }
+constexpr int kPrefillMaxT = 512;
+
+// Largest window the prefill takes for this model (the parameter block must
+// fit in LDS next to the K/V buffer); 0 if none.
+int prefill_max_window(const ModelView& M) {
+    const size_t dyn = sizeof(float) * (size_t)PfTop::make(M.n_layer, M.F, M.A).total;
+    for (int t = kPrefillMaxT; t >= 128; t /= 2)
+        if (dyn + sizeof(KVBuf<512>) * t / 512 + 64 <= 160 * 1024) return t;
+    return 0;
+}
+
+template <int NW>
+static int launch_nw(const ModelView& M, const PrefillArgs& a, size_t dyn, hipStream_t st) {
+    if (dyn + sizeof(KVBuf<32 * NW>) > 160 * 1024) {
+        set_error(DPT_EUNSUPPORTED, "prefill: parameter block does not fit in LDS");
+        return DPT_EUNSUPPORTED;
+    }
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prefill_kernel<NW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    hipLaunchKernelGGL(prefill_kernel<NW>, dim3(a.N), dim3(NW * 64), dyn, st, M, a);
+    return check_hip(hipGetLastError(), "prefill_kernel launch");
+}
 
 int launch_prefill(const ModelView& M, const float* frag, const float* q, const float* cs, const float* ca,
                    const float* cn, const float* cr, int N, int C, int out_mode, float* out, hipStream_t st) {
     PrefillArgs a{q, cs, ca, cn, cr, N, C, out_mode, out, frag};
     const size_t dyn = sizeof(float) * (size_t)PfTop::make(M.n_layer, M.F, M.A).total;
-    if (dyn + sizeof(KVLds) > 160 * 1024) {
-        set_error(DPT_EUNSUPPORTED, "n_layer=%d: parameter block does not fit in LDS", M.n_layer);
-        return DPT_EUNSUPPORTED;
-    }
-    if (dyn > 64 * 1024)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prefill_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-    hipLaunchKernelGGL(prefill_kernel, dim3(N), dim3(kFwdWaves * 64), dyn, st, M, a);
-    return check_hip(hipGetLastError(), "prefill_kernel launch");
+    const int T = C + 1;
+    if (T <= 128) return launch_nw<4>(M, a, dyn, st);
+    if (T <= 256) return launch_nw<8>(M, a, dyn, st);
+    return launch_nw<16>(M, a, dyn, st);
 }
 
 }  // namespace dpt

@@ -124,11 +124,17 @@ class DeviceModel:
             cs_ = ca_ = cn_ = cr_ = None
         out = torch.empty((N, self.action_dim) if out_mode == 0 else (N, C, self.action_dim),
                           dtype=torch.float32, device=dev)
-        ws = (None if _prefill[0] and C + 1 <= _lib.PREFILL_MAX_WINDOW
+        ws = (None if C + 1 <= self.prefill_max_window()
               else torch.empty(self.kv_numel(N, C + 1), dtype=torch.float32, device=dev))
         _lib.call("dpt_forward_window", self._h, _p(q), _p(cs_), _p(ca_), _p(cn_), _p(cr_), N, C,
                   int(out_mode), _p(out), _p(ws), _stream())
         return out
+
+    def prefill_max_window(self):
+        """Longest window dpt_forward_window runs as one MFMA prefill (0 when switched off)."""
+        n = ctypes.c_int32()
+        _lib.call("dpt_prefill_max_window", self._h, ctypes.byref(n))
+        return n.value
 
     def decode_step(self, kv, max_pos, pos, token):
         token = _dev(token, torch.float32)
@@ -332,10 +338,6 @@ def set_decode_tile(tile):
     _lib.call("dpt_tuning_set", _lib.TUNE_DECODE_TILE, int(tile))
 
 
-_prefill = [True]
-
-
 def set_prefill(on):
-    """Windows of <= PREFILL_MAX_WINDOW tokens as one MFMA prefill (default) or position by position."""
+    """Windows up to DeviceModel.prefill_max_window() as one MFMA prefill (default) or position by position."""
     _lib.call("dpt_tuning_set", _lib.TUNE_PREFILL, int(bool(on)))
-    _prefill[0] = bool(on)

@@ -147,7 +147,6 @@ SIGNATURES.update({
 
 TUNE_DECODE_TILE = 1
 TUNE_PREFILL = 2
-PREFILL_MAX_WINDOW = 128  # DPT_PREFILL_MAX_WINDOW
 SIGNATURES["dpt_tuning_set"] = (_i32, [_i32, _i64])
 
 
@@ -158,4 +157,5 @@ class DarkroomRolloutArgs(ctypes.Structure):
                 ("returns_out", _c_void_p), ("actions_out", _c_void_p), ("logits_out", _c_void_p)]
 
 
+SIGNATURES["dpt_prefill_max_window"] = (_i32, [_c_void_p, ctypes.POINTER(_i32)])
 SIGNATURES["dpt_rollout_darkroom"] = (_i32, [_c_void_p, ctypes.POINTER(DarkroomRolloutArgs), _c_void_p])

@@ -66,7 +66,7 @@ const char* dpt_last_error(void);
  * DPT_TUNE_DECODE_TILE = tasks per workgroup of the decode kernels, 8 (default:
  * two workgroups per CU) or 16.
  * DPT_TUNE_PREFILL = 1 (default): dpt_forward_window runs windows of up to
- * DPT_PREFILL_MAX_WINDOW tokens as one MFMA prefill; 0: always position by
+ * dpt_prefill_max_window() tokens as one MFMA prefill; 0: always position by
  * position through the K/V workspace.  */
 #define DPT_TUNE_DECODE_TILE 1
 #define DPT_TUNE_PREFILL 2
@@ -118,12 +118,13 @@ int dpt_forward_window(const dpt_model* model, const float* query, const float* 
                        const float* actions, const float* next_states, const float* rewards,
                        int32_t N, int32_t C, int32_t out_mode, float* out, float* workspace,
                        void* stream);
-/* Windows of T = C + 1 <= DPT_PREFILL_MAX_WINDOW tokens run as one MFMA prefill
- * (all positions at once, one workgroup per sequence) and `workspace` may be
- * NULL.  Longer windows are evaluated causally, position by position, through
- * a K/V cache in `workspace` (dpt_kvcache_numel(model, N, C + 1) floats);
- * both are the full causal forward (each row attends to rows <= itself).     */
-#define DPT_PREFILL_MAX_WINDOW 128
+/* Windows of T = C + 1 <= dpt_prefill_max_window(model) tokens (512 for the
+ * reference models) run as one MFMA prefill (all positions at once, one
+ * workgroup per sequence) and `workspace` may be NULL.  Longer windows are
+ * evaluated causally, position by position, through a K/V cache in
+ * `workspace` (dpt_kvcache_numel(model, N, C + 1) floats); both are the full
+ * causal forward (each row attends to rows <= itself).                        */
+int dpt_prefill_max_window(const dpt_model* model, int32_t* tokens_out_host);
 
 /* ------------------------------------------------------------------ KV-cache decode
  * Exact incremental form of the growing-window forward used by the bandit

@@ -27,7 +27,8 @@ def timed(fn, reps=5):
 
 
 res = {}
-for name, sd, A, H, N, C in (("darkroom_C3", 2, 5, 100, 4096, 100), ("bandit_offline", 1, 5, 500, 200, 127)):
+for name, sd, A, H, N, C in (("darkroom_C3", 2, 5, 100, 4096, 100), ("bandit_offline_T128", 1, 5, 500, 200, 127),
+                             ("bandit_offline_T501", 1, 5, 500, 200, 500), ("bandit_T501_N4096", 1, 5, 500, 4096, 500)):
     sdict, _ = bench.synthetic_state_dict(4, sd, A, H, seed=0)
     m = dpt_hip.DeviceModel(sdict, 4, sd, A, 4 * (1 + H))
     rs = np.random.RandomState(0)

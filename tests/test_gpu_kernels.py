@@ -313,7 +313,7 @@ def test_rollout_darkroom_large_properties():
 
 
 def test_prefill_equals_positionwise_window():
-    """The MFMA prefill (windows <= 128 tokens) and the position-by-position K/V path give the
+    """The MFMA prefill (4/8/16 waves: windows of 128/256/512 tokens) and the position-by-position K/V path give the
     same logits (out_mode 0 and 1) on random contexts of every model; both within the bar
     of the reference's recorded logits where fixtures exist."""
     import dpt_hip
@@ -321,7 +321,8 @@ def test_prefill_equals_positionwise_window():
     for name in ("bandit5", "darkroom", "linear20"):
         g, m, _ = model_from_golden(name)
         H, sd, A, L, E = (int(x) for x in g["cfg"])
-        for N, C in ((3, 0), (37, 5), (64, 100), (17, 127)):
+        assert m.prefill_max_window() == 512
+        for N, C in ((3, 0), (37, 5), (64, 100), (17, 127), (9, 128), (20, 255), (5, 300), (6, 500)):
             if C + 1 > 4 * (1 + H):
                 continue
             q = rs.randn(N, sd).astype(np.float32)
