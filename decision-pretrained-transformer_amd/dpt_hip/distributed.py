@@ -42,3 +42,26 @@ def sharded_online(rollout_fn, means_all, group=None):
     first, count = shard(n_total, world, rank)
     out = rollout_fn(means_all[first:first + count], first)
     return gather_rows(out["arm_value"], n_total, group), out
+
+
+def regret_stats_allreduce(opt_local, lnr_local, n_total, group=None):
+    """Suboptimality and cumulative-regret mean / SEM curves over ALL tasks of all ranks
+    (evals/eval_bandit.py:169-178: diff = opt - lnr, cumsum over steps, mean and
+    scipy.stats.sem with ddof=1 over tasks) from one all_reduce of per-step moments
+    (4 x H fp64) instead of gathering every task's curve.  Same values as the gathered
+    computation up to fp64 summation order (sum-of-squares form of the variance).
+    opt_local / lnr_local: (count, H) arm-value curves of this rank's tasks."""
+    diff = opt_local.to(torch.float64) - lnr_local.to(torch.float64)
+    cr = torch.cumsum(diff, dim=1)
+    mom = torch.stack([diff.sum(0), (diff * diff).sum(0), cr.sum(0), (cr * cr).sum(0)])
+    dist.all_reduce(mom, group=group)
+    n = float(n_total)
+
+    def mean_sem(s1, s2):
+        mean = s1 / n
+        var = (s2 - s1 * mean) / (n - 1.0)
+        return mean, torch.sqrt(torch.clamp(var, min=0.0) / n)
+
+    sm, ss = mean_sem(mom[0], mom[1])
+    rm, rsem = mean_sem(mom[2], mom[3])
+    return dict(subopt_mean=sm, subopt_sem=ss, regret_mean=rm, regret_sem=rsem)

@@ -45,10 +45,14 @@ def _worker(rank, port, blob, means, H, seed, q):
     sys.path[:0] = [PKG, ROOT]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
-    from dpt_hip.distributed import sharded_online
+    from dpt_hip.distributed import regret_stats_allreduce, shard, sharded_online
     full, local = sharded_online(_rollout_fn(blob, H, seed), means)
+    first, count = shard(means.shape[0], WORLD, rank)
+    opt = torch.from_numpy(np.repeat(means[first:first + count].max(1, keepdims=True), H, axis=1))
+    stats = regret_stats_allreduce(opt, local["arm_value"], means.shape[0])
     if rank == 0:
         q.put(full.numpy())
+        q.put({k: v.numpy() for k, v in stats.items()})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -78,7 +82,16 @@ def test_gloo_world2_sharded_equals_single():
     for p in procs:
         p.start()
     full = q.get(timeout=240)
+    stats = q.get(timeout=60)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert np.array_equal(full, single)
+    # online regret statistics through one all_reduce == the oracle's curves over all tasks
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import dpt_oracle as O
+    opt = np.repeat(means.max(1, keepdims=True), H, axis=1)
+    ref = O.regret_curves(opt, single)
+    for k, v in ref.items():
+        assert np.allclose(stats[k], v, rtol=1e-9, atol=1e-12), k
