@@ -48,13 +48,24 @@ def synthetic_state_dict(n_layer, state_dim, action_dim, horizon, seed=0):
 
 
 def algorithmic_bytes(N, H, n_layer, E=32):
-    """Minimal HBM bytes of one fused rollout launch: at step h the K/V rows of
-    positions < h are streamed (2*L*E*4 B each), the new K/V row is written,
-    and means[a] (8 B) is read + action (4 B), reward and arm value (8 B each)
-    are written."""
-    kvb = 2 * n_layer * E * 4
-    per_task = kvb * H * (H - 1) // 2 + (kvb + 28) * H
+    """Minimal HBM bytes of one fused rollout launch (rollout_bandit_kernel's
+    algorithm): at step h, blocks 1..L-1 stream the K/V rows of positions < h
+    (2*(L-1)*E*4 B each) and block 0 reads the 8-B (action, reward) record of
+    each position < h (its attention is recomputed from the tokens, DESIGN.md);
+    the new K/V rows and record are written, and means[a] (8 B) is read +
+    action (4 B), reward and arm value (8 B each) are written.  wpe and the
+    weights are shared by every task and served from L2 (not counted)."""
+    per_pos = 2 * (n_layer - 1) * E * 4 + 8
+    per_task = per_pos * H * (H - 1) // 2 + (per_pos + 28) * H
     return N * per_task
+
+
+def kvcache_bytes(N, H, n_layer, E=32):
+    """SURVEY.md 8(d)'s bytes for the plain K/V-cache decode (every block's K/V
+    streamed, 2*L*E*4 B per position): what the same rollout would move without
+    the block-0 recompute."""
+    kvb = 2 * n_layer * E * 4
+    return N * (kvb * H * (H - 1) // 2 + (kvb + 28) * H)
 
 
 def window_flops(T, n_layer, F, A, E=32):
@@ -214,7 +225,8 @@ def main():
                 traffic = p.get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "rollout_bandit_kernel",
-                "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": abytes}
+                "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": abytes,
+                "kvcache_bytes_per_launch": kvcache_bytes(count, H, L)}
     else:
         F = 2 * 2 + 5 + 1
         flops = count * H * (window_flops(1, L, F, 5) + (Heps - 1) * window_flops(1 + H, L, F, 5))

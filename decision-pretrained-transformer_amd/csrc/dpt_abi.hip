@@ -51,6 +51,8 @@ int launch_rollin_darkroom(const int32_t*, const int32_t*, int, int, int, int, c
 int launch_rollout_policy(const dpt_policy_rollout_args&, hipStream_t);
 int launch_pack_fragments(const ModelView&, float*, hipStream_t);
 int64_t fragments_numel(int n_layer);
+int launch_derive_l0(const ModelView&, float*, hipStream_t);
+int64_t l0_numel();
 int launch_rollout_darkroom(const ModelView&, const float*, const dpt_darkroom_rollout_args&, hipStream_t);
 int darkroom_max_window();
 int prefill_max_window(const ModelView&);
@@ -66,6 +68,7 @@ struct dpt_model {
     dpt_model_desc desc;
     float* blob;
     float* frag;  // the blocks' weights in MFMA fragment order (dpt_darkroom.hip FragOff)
+    float* l0;    // block 0 folded for the K/V-free bandit rollout (dpt_decode.hip L0Off)
     ModelView view;
 };
 
@@ -146,25 +149,32 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
         (void)hipFree(blob);
         return rc;
     }
-    const ModelView view = make_view(blob, *d);
+    ModelView view = make_view(blob, *d);
     float* frag = nullptr;
+    float* l0 = nullptr;
     const size_t frag_bytes = (size_t)fragments_numel(d->n_layer) * sizeof(float);
-    if (hipMalloc(&frag, frag_bytes) != hipSuccess) {
+    const size_t l0_bytes = (size_t)l0_numel() * sizeof(float);
+    if (hipMalloc(&frag, frag_bytes) != hipSuccess || hipMalloc(&l0, l0_bytes) != hipSuccess) {
         (void)hipFree(blob);
-        set_error(DPT_ENOMEM, "hipMalloc(%zu) for the fragment-packed weights failed", frag_bytes);
+        (void)hipFree(frag);
+        set_error(DPT_ENOMEM, "hipMalloc(%zu + %zu) for the derived weights failed", frag_bytes, l0_bytes);
         return DPT_ENOMEM;
     }
     rc = launch_pack_fragments(view, frag, nullptr);
-    if (!rc) rc = check_hip(hipDeviceSynchronize(), "fragment packing");
+    if (!rc) rc = launch_derive_l0(view, l0, nullptr);
+    if (!rc) rc = check_hip(hipDeviceSynchronize(), "weight derivation");
     if (rc) {
         (void)hipFree(blob);
         (void)hipFree(frag);
+        (void)hipFree(l0);
         return rc;
     }
+    view.l0 = l0;
     dpt_model* m = new dpt_model;
     m->desc = *d;
     m->blob = blob;
     m->frag = frag;
+    m->l0 = l0;
     m->view = view;
     *out = m;
     return DPT_OK;
@@ -173,7 +183,9 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
 int dpt_model_free(dpt_model* m) {
     if (!m) return DPT_OK;
     int rc = check_hip(hipFree(m->blob), "hipFree weight blob");
-    const int rc2 = check_hip(hipFree(m->frag), "hipFree fragment weights");
+    int rc2 = check_hip(hipFree(m->frag), "hipFree fragment weights");
+    const int rc3 = check_hip(hipFree(m->l0), "hipFree derived block-0 weights");
+    if (!rc2) rc2 = rc3;
     delete m;
     if (!rc) rc = rc2;
     return rc;

@@ -54,6 +54,9 @@ struct ModelView {
     const float* lnf_b;
     const float* head_w;  // [E][A]
     const float* head_b;  // [A]
+    // block 0's attention folded into the K/V-free form the bandit rollout uses
+    // (dpt_decode.hip L0Off): G = Wq Wk^T, g0 = Wk bq, Wvp = Wv Wproj, bvp = bv Wproj + bproj
+    const float* l0;
     int n_layer, sd, A, F, n_positions;
 };
 

@@ -70,8 +70,6 @@ struct Smem {
     float part[kChunks][kM][kE]; // mlp.c_proj partial sums, one per 16-unit hidden chunk
     float logits[kM][kMaxA];
     float tok[kM][kMaxF];        // packed token features of the current position
-    double draw_u[kM];           // this step's selection uniform (rollout)
-    double draw_g[kM];           // this step's reward normal / Bernoulli uniform (rollout)
     double means[kM][kMaxA];     // the tile's arm means (rollout)
 };
 static_assert(sizeof(Smem) % 16 == 0, "parameter block must start 16-B aligned");
@@ -100,6 +98,35 @@ struct ParamLDS {
 
 __host__ inline size_t decode_smem_bytes(const ModelView& M) {
     return sizeof(Smem) + sizeof(float) * (size_t)ParamLDS::make(M.F, M.n_layer, M.A).total;
+}
+
+// Block 0 folded for the K/V-free bandit rollout (ModelView::l0, derived at model
+// creation by derive_l0_kernel).  All matrices [in][out], E x E.
+struct L0Off {
+    static constexpr int G = 0;                 // Wq Wk^T: u = xn G + g0 = Wk q
+    static constexpr int g0 = G + kE * kE;      // Wk bq
+    static constexpr int Wvp = g0 + kE;         // Wv Wproj
+    static constexpr int bvp = Wvp + kE * kE;   // bv Wproj + bproj
+    static constexpr int size = bvp + kE;
+};
+
+// LDS block of the rollout after ParamLDS (offsets in floats): the embedding of
+// every bandit token up to its reward term, base[k] = ((w_s + w_a=k) + w_s') + emb_b
+// for k < A and base[A] = w_s + emb_b (the query token), then g0 and bvp.
+struct RolloutLDS {
+    int base, g0, bvp, total;
+    __host__ __device__ static RolloutLDS make(int A) {
+        RolloutLDS r;
+        r.base = 0;
+        r.g0 = (A + 1) * kE;
+        r.bvp = r.g0 + kE;
+        r.total = r.bvp + kE;
+        return r;
+    }
+};
+
+__host__ inline size_t rollout_smem_bytes(const ModelView& M) {
+    return decode_smem_bytes(M) + sizeof(float) * (size_t)RolloutLDS::make(M.A).total;
 }
 
 template <int NT>
@@ -167,7 +194,7 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
                                   const float* q, const float* kcur, const float* vcur, float* o,
                                   int lane) {
     const int g = lane >> 3, c = lane & 7;
-    const float scale = 0.17677669529663687f;  // 32 ** -0.5
+    const float scale = 0.17677669529663687f * 1.4426950408889634f;  // 32 ** -0.5 * log2(e): exp2 domain
     const float4 q4 = *reinterpret_cast<const float4*>(q + 4 * c);
     float m = -1e30f, l = 0.f;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -202,12 +229,12 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
             mx = fmaxf(mx, s[r]);
         }
         const float mn = fmaxf(m, mx);
-        const float corr = expf(m - mn);
+        const float corr = __builtin_amdgcn_exp2f(m - mn);
         l *= corr;
         acc.x *= corr; acc.y *= corr; acc.z *= corr; acc.w *= corr;
 #pragma unroll
         for (int r = 0; r < kRows; ++r) {
-            const float pr = expf(s[r] - mn);
+            const float pr = __builtin_amdgcn_exp2f(s[r] - mn);
             l += pr;
             acc.x = fmaf(pr, vv[r].x, acc.x);
             acc.y = fmaf(pr, vv[r].y, acc.y);
@@ -227,8 +254,8 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
         if (g == 0) {
             const float sc = d * scale;
             const float mn = fmaxf(m, sc);
-            const float corr = expf(m - mn);
-            const float pr = expf(sc - mn);
+            const float corr = __builtin_amdgcn_exp2f(m - mn);
+            const float pr = __builtin_amdgcn_exp2f(sc - mn);
             l = l * corr + pr;
             acc.x = fmaf(pr, v4.x, acc.x * corr);
             acc.y = fmaf(pr, v4.y, acc.y * corr);
@@ -244,7 +271,7 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
         const float ax = __shfl_xor(acc.x, off), ay = __shfl_xor(acc.y, off);
         const float az = __shfl_xor(acc.z, off), aw = __shfl_xor(acc.w, off);
         const float mn = fmaxf(m, mo);
-        const float sa = expf(m - mn), sb = expf(mo - mn);
+        const float sa = __builtin_amdgcn_exp2f(m - mn), sb = __builtin_amdgcn_exp2f(mo - mn);
         l = l * sa + lo * sb;
         acc.x = acc.x * sa + ax * sb;
         acc.y = acc.y * sa + ay * sb;
@@ -261,15 +288,125 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
     }
 }
 
-// Per-step Philox draws of a rollout, computed off the critical path by an
-// otherwise idle wave (during the c_proj phase of block 0).
-struct DrawJob {
-    uint64_t seed;
-    int64_t first_task;
-    const double* uniforms;  // (H, N) or null
-    const double* noise;     // (H, N) or null
-    int N, step, sample, bernoulli;
-};
+// Block-0 attention of one bandit task (one wave) without a K/V cache.  Every
+// bandit context token is [1, onehot(a), 1, r], so block 0's input at position p
+// is x_p = fma(r_p, w_r, base[a_p]) + wpe[p], rebuilt from the 8-byte (a_p, r_p)
+// record instead of streaming 256 B of K and V.  With y_p = LN1(x_p) =
+// rstd_p d_p * g + b (d_p = x_p - mean_p):
+//   q . k_p = y_p . (Wk q) + const = rstd_p d_p . (g * u) + const'   (u = Wk q)
+//   sum_p P_p v_p = (sum_p P_p y_p) Wv + bv
+// The constants shift every score alike and cancel in the softmax; Wv, bv are
+// folded into c_proj (L0Off::Wvp, bvp).  Writes o = sum_p P_p y_p.  The current
+// position's x is xcur (the residual row, before attention).  A record is
+// (a_p * E as int bits, r_p); scores are kept in the log2 domain (v_exp_f32).
+__device__ inline void attend_l0(const float2* __restrict__ tok, const float* __restrict__ wpe, int pos,
+                                 const float* u, const float* xcur, const float* baseT, const float* wr,
+                                 const float* lng, const float* lnb, float* o, int lane) {
+    const int g = lane >> 3, c = lane & 7;
+    const float scale2 = 0.17677669529663687f * 1.4426950408889634f;  // 32 ** -0.5 * log2(e)
+    const float4 u4 = *reinterpret_cast<const float4*>(u + 4 * c);
+    const float4 g4 = *reinterpret_cast<const float4*>(lng + 4 * c);
+    const float4 gu = make_float4(g4.x * u4.x, g4.y * u4.y, g4.z * u4.z, g4.w * u4.w);
+    const float4 wr4 = *reinterpret_cast<const float4*>(wr + 4 * c);
+    const float* bT = baseT + 4 * c;
+    // centred row, 1/std and log2-domain score of one position's x (8-lane group sums)
+    auto row = [&](float4 x, float4& d, float& rstd, float& sc) {
+        const float mean = dpp_sum8((x.x + x.y) + (x.z + x.w)) * (1.0f / kE);
+        d = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+        float vv = d.x * d.x;
+        vv = fmaf(d.y, d.y, vv);
+        vv = fmaf(d.z, d.z, vv);
+        vv = fmaf(d.w, d.w, vv);
+        float dg = d.x * gu.x;
+        dg = fmaf(d.y, gu.y, dg);
+        dg = fmaf(d.z, gu.z, dg);
+        dg = fmaf(d.w, gu.w, dg);
+        vv = dpp_sum8(vv);
+        dg = dpp_sum8(dg);
+        rstd = __builtin_amdgcn_rsqf(vv * (1.0f / kE) + 1e-5f);
+        sc = (rstd * dg) * scale2;
+    };
+    float m = -1e30f, l = 0.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int base = 0; base < pos; base += 8 * kRows) {
+        float2 tk[kRows];
+        float4 wp[kRows];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {  // past the end: re-read position pos-1, masked below
+            const int p = min(base + 8 * r + g, pos - 1);
+            tk[r] = tok[p];
+            wp[r] = *reinterpret_cast<const float4*>(wpe + (size_t)p * kE + 4 * c);
+        }
+        float4 d[kRows];
+        float rs[kRows], s[kRows];
+        float mx = -1e30f;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            const float4 b4 = *reinterpret_cast<const float4*>(bT + __float_as_int(tk[r].x));
+            const float rr = tk[r].y;
+            const float4 x = make_float4(fmaf(rr, wr4.x, b4.x) + wp[r].x, fmaf(rr, wr4.y, b4.y) + wp[r].y,
+                                         fmaf(rr, wr4.z, b4.z) + wp[r].z, fmaf(rr, wr4.w, b4.w) + wp[r].w);
+            row(x, d[r], rs[r], s[r]);
+            s[r] = (base + 8 * r + g < pos) ? s[r] : -INFINITY;
+            mx = fmaxf(mx, s[r]);
+        }
+        const float mn = fmaxf(m, mx);
+        const float corr = __builtin_amdgcn_exp2f(m - mn);
+        l *= corr;
+        acc.x *= corr; acc.y *= corr; acc.z *= corr; acc.w *= corr;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            const float pr = __builtin_amdgcn_exp2f(s[r] - mn);
+            l += pr;
+            const float w = pr * rs[r];
+            acc.x = fmaf(w, d[r].x, acc.x);
+            acc.y = fmaf(w, d[r].y, acc.y);
+            acc.z = fmaf(w, d[r].z, acc.z);
+            acc.w = fmaf(w, d[r].w, acc.w);
+        }
+        m = mn;
+    }
+    {   // the current position (group 0 merges it; all lanes run the group sums)
+        float4 dc;
+        float rc, sc;
+        row(*reinterpret_cast<const float4*>(xcur + 4 * c), dc, rc, sc);
+        if (g == 0) {
+            const float mn = fmaxf(m, sc);
+            const float corr = __builtin_amdgcn_exp2f(m - mn);
+            const float pr = __builtin_amdgcn_exp2f(sc - mn);
+            const float w = pr * rc;
+            l = l * corr + pr;
+            acc.x = fmaf(w, dc.x, acc.x * corr);
+            acc.y = fmaf(w, dc.y, acc.y * corr);
+            acc.z = fmaf(w, dc.z, acc.z * corr);
+            acc.w = fmaf(w, dc.w, acc.w * corr);
+            m = mn;
+        }
+    }
+#pragma unroll
+    for (int off = 8; off <= 32; off <<= 1) {
+        const float mo = __shfl_xor(m, off);
+        const float lo = __shfl_xor(l, off);
+        const float ax = __shfl_xor(acc.x, off), ay = __shfl_xor(acc.y, off);
+        const float az = __shfl_xor(acc.z, off), aw = __shfl_xor(acc.w, off);
+        const float mn = fmaxf(m, mo);
+        const float sa = __builtin_amdgcn_exp2f(m - mn), sb = __builtin_amdgcn_exp2f(mo - mn);
+        l = l * sa + lo * sb;
+        acc.x = acc.x * sa + ax * sb;
+        acc.y = acc.y * sa + ay * sb;
+        acc.z = acc.z * sa + az * sb;
+        acc.w = acc.w * sa + aw * sb;
+        m = mn;
+    }
+    if (lane < 8) {  // sum_p P_p y_p = g * (sum_p P_p rstd_p d_p) + b   (sum_p P_p = 1)
+        const float inv = 1.0f / l;
+        const float4 b4 = *reinterpret_cast<const float4*>(lnb + 4 * c);
+        o[4 * c + 0] = fmaf(g4.x, acc.x * inv, b4.x);
+        o[4 * c + 1] = fmaf(g4.y, acc.y * inv, b4.y);
+        o[4 * c + 2] = fmaf(g4.z, acc.z * inv, b4.z);
+        o[4 * c + 3] = fmaf(g4.w, acc.w * inv, b4.w);
+    }
+}
 
 template <int TILE>
 __device__ inline void zero_smem(Smem& S) {
@@ -284,12 +421,20 @@ __device__ inline void zero_smem(Smem& S) {
 //   split-K reduce + residual + next LayerNorm (half-wave per task)
 // `wpe_j` is wpe[pos][tid & 31] (prefetched by the caller); P is the LDS
 // parameter block.
-template <int TILE>
+// L0R (bandit rollout only): block 0 runs K/V-free (attend_l0); layer 0's K slot
+// of each task holds its (a_p, r_p) token records instead, and D is the
+// RolloutLDS block.
+template <int TILE, bool L0R = false>
 __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, const ModelView& M,
                                 float* __restrict__ kv, int N, int max_pos, int tile0, int pos, float wpe_j,
-                                const DrawJob* dj) {
+                                const float* D = nullptr) {
     constexpr int kProjWave = TILE - 1;  // a wave with no c_attn tile (TILE >= 8)
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // opaque copy of the thread id: every lane-derived address is recomputed per call
+    // instead of being hoisted out of the caller's step loop (128-VGPR budget, no spills)
+    int tid_ = threadIdx.x;
+    asm volatile("" : "+v"(tid_));
+    const int tid = tid_, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: addresses in SGPRs
     const size_t lstride = (size_t)N * max_pos * kE;            // one layer of K (or V)
     const size_t vhalf = (size_t)M.n_layer * lstride;
     const int i16 = lane & 15, kq = lane >> 4;
@@ -307,10 +452,32 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
     DPT_STAMP(0);
 
     for (int li = 0; li < M.n_layer; ++li) {
+        asm volatile("" : "+v"(tid_));  // and per layer (see above)
+        const int lane = tid_ & 63, i16 = lane & 15, kq = lane >> 4;
         const float* W = M.layers + (size_t)li * LayerOff::size;
         const float* PL = P + pl.layers + li * PLay::size;
+        const bool l0 = L0R && li == 0;
+        if (l0) {
+            // u = xn G + g0 (= Wk q), two 16-column tiles; block 0 stores no K/V
+            if (wave < 2) {
+                const float* B = M.l0 + L0Off::G + wave * 16;
+                float w[8];
+#pragma unroll
+                for (int s = 0; s < 8; ++s) w[s] = __ldg(B + (size_t)(4 * s + kq) * kE + i16);
+                floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(S.xn[i16][4 * s + kq], w[s], acc, 0, 0, 0);
+                const int col = wave * 16 + i16;
+                const float bias = D[RolloutLDS::make(M.A).g0 + col];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int t = kq * 4 + r;
+                    if (t < TILE) S.q[t][col] = acc[r] + bias;
+                }
+            }
+        } else if (wave < 6) {
         // c_attn: [16 x 32] x [32 x 96] -> q | k | v, one 16-column tile per wave
-        if (wave < 6) {
             const float* B = W + LayerOff::attn_w + wave * 16;
             float w[8];
 #pragma unroll
@@ -350,14 +517,19 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
             if (task < N) {
                 const float* kc = kv + li * lstride + (size_t)task * max_pos * kE;
                 const float* vc = kv + vhalf + li * lstride + (size_t)task * max_pos * kE;
-                attend_one(kc, vc, pos, S.q[wave], S.kcur[wave], S.vcur[wave], S.o[wave], lane);
+                if (l0)
+                    attend_l0(reinterpret_cast<const float2*>(kc), M.wpe, pos, S.q[wave], S.x[wave],
+                              D + RolloutLDS::make(M.A).base, P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
+                              PL + PLay::ln1_b, S.o[wave], lane);
+                else
+                    attend_one(kc, vc, pos, S.q[wave], S.kcur[wave], S.vcur[wave], S.o[wave], lane);
             }
         }
         bar_lds();
         DPT_STAMP(2);
         // c_proj + residual + ln_2, one wave: both 16-column tiles, rows reduced over 16 lanes
         if (wave == kProjWave) {
-            const float* B = W + LayerOff::proj_w;
+            const float* B = l0 ? M.l0 + L0Off::Wvp : W + LayerOff::proj_w;
             float w0[8], w1[8];
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
@@ -372,7 +544,8 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w1[s], a1, 0, 0, 0);
             }
             const int c0 = i16, c1 = 16 + i16;
-            const float b0 = PL[PLay::proj_b + c0], b1 = PL[PLay::proj_b + c1];
+            const float* pb = l0 ? D + RolloutLDS::make(M.A).bvp : PL + PLay::proj_b;
+            const float b0 = pb[c0], b1 = pb[c1];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int t = kq * 4 + r;
@@ -393,18 +566,6 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                     S.xn[t][c0] = fmaf(d0 * rstd, PL[PLay::ln2_g + c0], PL[PLay::ln2_b + c0]);
                     S.xn[t][c1] = fmaf(d1 * rstd, PL[PLay::ln2_g + c1], PL[PLay::ln2_b + c1]);
                 }
-            }
-        } else if (li == 0 && dj && wave == 0 && lane < TILE) {
-            // this step's draws (select uniform, reward normal / Bernoulli uniform)
-            const int task = tile0 + lane;
-            if (task < dj->N) {
-                const int64_t gtask = dj->first_task + task;
-                if (dj->sample)
-                    S.draw_u[lane] = dj->uniforms ? dj->uniforms[(size_t)dj->step * dj->N + task]
-                                                  : philox_uniform(dj->seed, dj->step, gtask, DPT_STREAM_SELECT);
-                S.draw_g[lane] = dj->noise ? dj->noise[(size_t)dj->step * dj->N + task]
-                                 : dj->bernoulli ? philox_uniform(dj->seed, dj->step, gtask, DPT_STREAM_REWARD)
-                                                 : philox_normal(dj->seed, dj->step, gtask, DPT_STREAM_REWARD);
             }
         }
         bar_lds();
@@ -504,7 +665,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void decode_step_kernel(ModelView M, 
     }
     const float wpe_j = M.wpe[(size_t)pos * kE + (tid & 31)];
     __syncthreads();
-    decode_position<TILE>(S, P, pl, M, kv, N, max_pos, tile0, pos, wpe_j, nullptr);
+    decode_position<TILE>(S, P, pl, M, kv, N, max_pos, tile0, pos, wpe_j);
     for (int i = tid; i < TILE * M.A; i += TILE * 64) {
         const int t = i / M.A, a = i % M.A;
         if (tile0 + t < N) logits[(size_t)(tile0 + t) * M.A + a] = S.logits[t][a];
@@ -546,7 +707,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void window_decode_kernel(
             wpe_next = M.wpe[(size_t)(pos + 1) * kE + (tid & 31)];
         }
         bar_lds();
-        decode_position<TILE>(S, P, pl, M, kv, N, T, tile0, pos, wpe_j, nullptr);
+        decode_position<TILE>(S, P, pl, M, kv, N, T, tile0, pos, wpe_j);
         if (out_mode == 0 && pos == C) {
             for (int i = tid; i < TILE * A; i += TILE * 64) {
                 const int t = i / A, a = i % A;
@@ -563,7 +724,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void window_decode_kernel(
 }
 
 struct BanditRolloutParams {
-    int N, H, A, type, sample;
+    int N, H, A, type, sample, n_layer;
     int64_t first_task;
     double var;
     uint64_t seed;
@@ -577,6 +738,33 @@ struct BanditRolloutParams {
     float* logits_out;
 };
 
+// Block 0's V slot of a task (unused by the K/V-free block 0) holds the task's
+// per-step draw pairs (u = selection uniform, g = reward normal or Bernoulli
+// uniform), 16 B x H of the slot's 128 B x H.
+__device__ inline double2* draw_pairs(const BanditRolloutParams& Pr, int task) {
+    const size_t vhalf = (size_t)Pr.n_layer * Pr.N * Pr.H * kE;
+    return reinterpret_cast<double2*>(Pr.kv + vhalf + (size_t)task * Pr.H * kE);
+}
+
+// Every draw of the rollout, one thread per (task, step), before the rollout
+// launch: Philox by (step, global task, stream), or the caller's injected draws.
+__global__ void rollout_draws_kernel(BanditRolloutParams Pr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Pr.N * Pr.H) return;
+    const int task = (int)(i / Pr.H), h = (int)(i % Pr.H);
+    const int64_t gtask = Pr.first_task + task;
+    double u = 0.0, g;
+    if (Pr.sample)
+        u = Pr.uniforms ? Pr.uniforms[(size_t)h * Pr.N + task] : philox_uniform(Pr.seed, h, gtask, DPT_STREAM_SELECT);
+    if (Pr.noise)
+        g = Pr.noise[(size_t)h * Pr.N + task];
+    else if (Pr.type == DPT_BANDIT_BERNOULLI)
+        g = philox_uniform(Pr.seed, h, gtask, DPT_STREAM_REWARD);
+    else
+        g = philox_normal(Pr.seed, h, gtask, DPT_STREAM_REWARD);
+    draw_pairs(Pr, task)[h] = make_double2(u, g);
+}
+
 // The bandit online loop (evals/eval_bandit.py:70-89) for one tile of tasks,
 // all H steps: decode -> select -> env step -> append transition.
 template <int TILE>
@@ -589,23 +777,45 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         const int t = i / A, k = i % A;
         S.means[t][k] = (tile0 + t < Pr.N) ? Pr.means[(size_t)(tile0 + t) * A + k] : 0.0;
     }
+    // block 0 runs K/V-free (attend_l0): token embedding table and folded biases in LDS
+    float* D = P + pl.total;
+    const RolloutLDS rl = RolloutLDS::make(A);
+    for (int i = tid; i < (A + 1) * kE; i += TILE * 64) {
+        const int k = i / kE, j = i % kE;
+        const float* ew = P + pl.emb_w;
+        // the embedding's own rounding order (decode_position: fmaf over features, + emb_b)
+        const float acc = (k < A) ? (ew[j] + ew[(1 + k) * kE + j]) + ew[(1 + A) * kE + j] : ew[j];
+        D[rl.base + i] = acc + P[pl.emb_b + j];
+    }
+    for (int j = tid; j < kE; j += TILE * 64) {
+        D[rl.g0 + j] = M.l0[L0Off::g0 + j];
+        D[rl.bvp + j] = M.l0[L0Off::bvp + j];
+    }
+    // per task, block 0's K slot holds the (a_p, r_p) record of every position
+    auto tokrec = [&](int task) {
+        return reinterpret_cast<float2*>(Pr.kv + (size_t)task * Pr.H * kE);
+    };
     // position 0: the query token [state=1, 0_A, 0, 0] (BanditEnv.state = [1], ctrl_bandit.py:426)
-    if (tid < TILE) S.tok[tid][0] = 1.f;
-    DrawJob dj{Pr.seed, Pr.first_task, Pr.uniforms, Pr.noise, Pr.N, 0, Pr.sample, Pr.type == DPT_BANDIT_BERNOULLI};
+    if (tid < TILE) {
+        S.tok[tid][0] = 1.f;
+        if (tile0 + tid < Pr.N) tokrec(tile0 + tid)[0] = make_float2(__int_as_float(A * kE), 0.f);
+    }
+    // this thread's task's (u, g) draw pairs (rollout_draws_kernel), one per step
+    const double2* draws = (tid < TILE && tile0 + tid < Pr.N) ? draw_pairs(Pr, tile0 + tid) : nullptr;
     float wpe_next = M.wpe[tid & 31];
     __syncthreads();
     for (int h = 0; h < Pr.H; ++h) {
         const float wpe_j = wpe_next;
         if (h + 1 < Pr.H) wpe_next = M.wpe[(size_t)(h + 1) * kE + (tid & 31)];
-        dj.step = h;
-        decode_position<TILE>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, &dj);
+        const double2 dr = draws ? draws[h] : make_double2(0.0, 0.0);  // consumed after the forward
+        decode_position<TILE, true>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D);
         if (tid < TILE) {
             const int t = tid, task = tile0 + t;
             if (task < Pr.N) {
-                const int a = select_from_logits(S.logits[t], A, Pr.sample, 1.0f, S.draw_u[t]);
+                const int a = select_from_logits(S.logits[t], A, Pr.sample, 1.0f, dr.x);
                 const double mean = S.means[t][a];
-                const double r = (Pr.type == DPT_BANDIT_BERNOULLI) ? ((S.draw_g[t] < mean) ? 1.0 : 0.0)
-                                                                  : gaussian_reward(mean, Pr.var, S.draw_g[t]);
+                const double r = (Pr.type == DPT_BANDIT_BERNOULLI) ? ((dr.y < mean) ? 1.0 : 0.0)
+                                                                  : gaussian_reward(mean, Pr.var, dr.y);
                 Pr.actions_out[(size_t)task * Pr.H + h] = a;
                 Pr.rewards_out[(size_t)task * Pr.H + h] = r;
                 Pr.arm_value_out[(size_t)task * Pr.H + h] = mean;
@@ -616,6 +826,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
                 for (int k = 0; k < A; ++k) S.tok[t][1 + k] = (k == a) ? 1.f : 0.f;
                 S.tok[t][1 + A] = 1.f;
                 S.tok[t][2 + A] = (float)r;
+                if (h + 1 < Pr.H) tokrec(task)[h + 1] = make_float2(__int_as_float(a * kE), (float)r);
             }
         }
         __syncthreads();  // K/V stores of step h visible before step h+1 reads them
@@ -637,12 +848,46 @@ ModelView make_view(const float* blob, const dpt_model_desc& d) {
     v.lnf_b = blob + off; off += kE;
     v.head_w = blob + off; off += (size_t)kE * d.action_dim;
     v.head_b = blob + off;
+    v.l0 = nullptr;  // set by dpt_model_create once derived
     v.n_layer = d.n_layer;
     v.sd = d.state_dim;
     v.A = d.action_dim;
     v.F = F;
     v.n_positions = d.n_positions;
     return v;
+}
+
+// ModelView::l0 from block 0's weights (fp64 sums, one rounding per element).
+__global__ void derive_l0_kernel(ModelView M, float* __restrict__ l0) {
+    const float* W = M.layers;
+    const float* aw = W + LayerOff::attn_w;  // [E][3E]: q | k | v columns
+    const float* ab = W + LayerOff::attn_b;
+    const float* pw = W + LayerOff::proj_w;  // [E][E]
+    for (int i = threadIdx.x; i < L0Off::size; i += blockDim.x) {
+        double acc = 0.0;
+        if (i < L0Off::g0) {  // G[m][n] = sum_j Wq[m][j] Wk[n][j]
+            const int m = i / kE, n = i % kE;
+            for (int j = 0; j < kE; ++j) acc += (double)aw[m * 3 * kE + j] * (double)aw[n * 3 * kE + kE + j];
+        } else if (i < L0Off::Wvp) {  // g0[n] = sum_j Wk[n][j] bq[j]
+            const int n = i - L0Off::g0;
+            for (int j = 0; j < kE; ++j) acc += (double)aw[n * 3 * kE + kE + j] * (double)ab[j];
+        } else if (i < L0Off::bvp) {  // Wvp[m][n] = sum_j Wv[m][j] Wproj[j][n]
+            const int m = (i - L0Off::Wvp) / kE, n = (i - L0Off::Wvp) % kE;
+            for (int j = 0; j < kE; ++j) acc += (double)aw[m * 3 * kE + 2 * kE + j] * (double)pw[j * kE + n];
+        } else {  // bvp[n] = sum_j bv[j] Wproj[j][n] + bproj[n]
+            const int n = i - L0Off::bvp;
+            for (int j = 0; j < kE; ++j) acc += (double)ab[2 * kE + j] * (double)pw[j * kE + n];
+            acc += (double)W[LayerOff::proj_b + n];
+        }
+        l0[i] = (float)acc;
+    }
+}
+
+int64_t l0_numel() { return L0Off::size; }
+
+int launch_derive_l0(const ModelView& M, float* l0, hipStream_t st) {
+    hipLaunchKernelGGL(derive_l0_kernel, dim3(1), dim3(256), 0, st, M, l0);
+    return check_hip(hipGetLastError(), "derive_l0_kernel launch");
 }
 
 int64_t weights_numel(const dpt_model_desc& d) {
@@ -725,12 +970,24 @@ int launch_window_decode(const ModelView& M, float* kv, int N, int C, const floa
 int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, hipStream_t st) {
     size_t sm;
     if (int rc = check_smem(M, &sm)) return rc;
+    sm = rollout_smem_bytes(M);
+    if (sm > 160 * 1024) {
+        set_error(DPT_EUNSUPPORTED, "rollout LDS %zu B > 160 KiB (n_layer=%d, action_dim=%d)", sm, M.n_layer, M.A);
+        return DPT_EUNSUPPORTED;
+    }
+    if (!M.l0) {
+        set_error(DPT_EINVAL, "model has no derived block-0 weights");
+        return DPT_EINVAL;
+    }
     BanditRolloutParams P;
     P.N = a.N; P.H = a.H; P.A = a.A; P.type = a.type; P.sample = a.sample;
     P.first_task = a.first_task; P.var = a.var; P.seed = a.seed;
     P.means = a.means; P.uniforms = a.uniforms; P.noise = a.noise; P.kv = a.kvcache;
     P.actions_out = a.actions_out; P.rewards_out = a.rewards_out; P.arm_value_out = a.arm_value_out;
     P.logits_out = a.logits_out;
+    P.n_layer = M.n_layer;
+    const int64_t nd = (int64_t)a.N * a.H;
+    hipLaunchKernelGGL(rollout_draws_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st, P);
     allow_smem(rollout_bandit_kernel<8>, sm);
     allow_smem(rollout_bandit_kernel<16>, sm);
     if (g_decode_tile == 8)

@@ -217,7 +217,10 @@ typedef struct dpt_bandit_rollout_args {
     const double* means;  /* (N, A)                                       */
     const double* uniforms; /* (H, N) or NULL                             */
     const double* noise;    /* (H, N) or NULL (normals, or bernoulli uniforms) */
-    float* kvcache;         /* dpt_kvcache_numel(model, N, H) floats        */
+    float* kvcache;         /* dpt_kvcache_numel(model, N, H) floats: blocks
+                             * 1..L-1 keep their K/V; block 0 is recomputed
+                             * from the tokens, so its K slot holds the (a, r)
+                             * records and its V slot the per-step draws     */
     int32_t* actions_out;   /* (N, H)                                       */
     double* rewards_out;    /* (N, H)                                       */
     double* arm_value_out;  /* (N, H)  = cum_means.T                         */
