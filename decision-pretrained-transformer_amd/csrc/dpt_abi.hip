@@ -59,6 +59,7 @@ int prefill_max_window(const ModelView&);
 int launch_prefill(const ModelView&, const float*, const float*, const float*, const float*, const float*,
                    const float*, int, int, int, float*, hipStream_t);
 int set_decode_tile(int);
+int set_darkroom_memo(int);
 
 }  // namespace dpt
 
@@ -112,6 +113,10 @@ int dpt_tuning_set(int32_t key, int64_t value) {
     if (key == DPT_TUNE_PREFILL) {
         REQUIRE(value == 0 || value == 1, "prefill %lld: 0 or 1", (long long)value);
         g_prefill = value == 1;
+        return DPT_OK;
+    }
+    if (key == DPT_TUNE_DARKROOM_MEMO) {
+        REQUIRE(set_darkroom_memo((int)value) == DPT_OK, "darkroom memo %lld: 0 or 1", (long long)value);
         return DPT_OK;
     }
     set_error(DPT_EINVAL, "unknown tuning key %d", key);

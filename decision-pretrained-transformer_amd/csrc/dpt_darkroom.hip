@@ -53,6 +53,7 @@ namespace dpt {
 
 constexpr int kDrA = 5;                     // DarkRoom actions
 constexpr int kDrF = 10;                    // token features 2*sd + A + 1
+constexpr int kMemoStates = 128;            // logits memo rows (grids up to 11 x 11)
 
 // A-operand fragment of W^T for a k=32 input (W is [in][out], Conv1D layout):
 // lane l, k-step s reads W[16*(s>>2) + 4*(l>>4) + (s&3)][ob*16 + (l&15)];
@@ -117,7 +118,10 @@ struct DrSmem {
     float part_o[kFwdBlocks][kE];      // last layer: per-key-tile attention partials
     float part_m[kFwdBlocks], part_l[kFwdBlocks];
     float part_y[kFF / 16][kE];       // last layer: per-hidden-chunk MLP partials
-    int sx, sy, ret, pad;
+    // per-episode logits memo, one row per grid state (dim * dim <= kMemoStates)
+    float memo_lg[kMemoStates][kDrA];
+    int memo_ok[kMemoStates];
+    int sx, sy, ret, nfwd;
 };
 
 __device__ inline int2 pack_tr(int x, int y, int a, int nx, int ny, int r) {
@@ -170,6 +174,8 @@ struct DarkroomParams {
     int32_t* returns_out;
     int32_t* actions_out;
     float* logits_out;
+    int32_t* forwards_out;
+    int memo;  // 1: reuse this episode's logits for a state already queried (see the kernel)
     const float* frag;
 };
 
@@ -238,7 +244,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             S.sx = 0;
             S.sy = 0;
             S.ret = 0;
+            S.nfwd = 0;
         }
+        for (int i = tid; i < kMemoStates; i += blockDim.x) S.memo_ok[i] = 0;
         __syncthreads();
 
         // layer-0 episode cache: causal partial over keys 1..t of every token
@@ -266,7 +274,47 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             __syncthreads();
         }
 
+        // the policy's logits are a pure function of (window, query state) and the
+        // window is fixed for the whole episode: a state queried before in this
+        // episode reuses that forward's logits (bit-identical to re-running it)
+        auto finish_step = [&](const float (&lg)[kDrA], int t, int sx, int sy) {
+            const int step = ep * p.horizon + t;
+            double u = 0.0;
+            if (p.sample)
+                u = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
+                               : philox_uniform(p.seed, p.counter + step, p.first_task + task, DPT_STREAM_SELECT);
+            const int a = select_fixed<kDrA>(lg, p.sample, p.temp, u);
+            const int ea = p.perms ? p.perms[(size_t)task * kDrA + a] : a;
+            int nx = sx + (ea == 0) - (ea == 1);
+            int ny = sy + (ea == 2) - (ea == 3);
+            nx = min(max(nx, 0), p.dim - 1);
+            ny = min(max(ny, 0), p.dim - 1);
+            const int gx = p.goals[2 * task], gy = p.goals[2 * task + 1];
+            const int r = (nx == gx && ny == gy) ? 1 : 0;
+            S.cur[t] = pack_tr(sx, sy, a, nx, ny, r);
+            S.sx = nx;
+            S.sy = ny;
+            S.ret += r;
+            if (p.actions_out) p.actions_out[(size_t)task * steps_total + step] = a;
+            if (p.logits_out) {
+#pragma unroll
+                for (int k = 0; k < kDrA; ++k) p.logits_out[((size_t)step * p.N + task) * kDrA + k] = lg[k];
+            }
+        };
         for (int t = 0; t < p.horizon; ++t) {
+            if (p.memo) {
+                const int sidx = S.sx * p.dim + S.sy;  // same value in every lane (LDS, after a barrier)
+                if (S.memo_ok[sidx]) {
+                    if (tid == 0) {
+                        float lg[kDrA];
+#pragma unroll
+                        for (int k = 0; k < kDrA; ++k) lg[k] = S.memo_lg[sidx][k];
+                        finish_step(lg, t, S.sx, S.sy);
+                    }
+                    bar_lds();
+                    continue;
+                }
+            }
             float x[2][8];
 #pragma unroll
             for (int j = 0; j < 2; ++j)
@@ -407,11 +455,6 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     mw[h][0] = fs.ld(FragOff::mp, cj);
                     mw[h][1] = fs.ld(FragOff::mp, 8 + cj);
                 }
-                const int step = ep * p.horizon + t;
-                double u = 0.0;
-                if (p.sample && tid == 0)
-                    u = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
-                                   : philox_uniform(p.seed, p.counter + step, p.first_task + task, DPT_STREAM_SELECT);
                 // (1) key tiles wave and wave+4 of the attention, as flash partials (m, l, o)
                 {
                     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
@@ -552,24 +595,14 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         lg[a] = sum_cols(part) + P[pt.head_b + a];
                     }
                     if (lane == 0) {
-                        const int a = select_fixed<kDrA>(lg, p.sample, p.temp, u);
-                        const int ea = p.perms ? p.perms[(size_t)task * kDrA + a] : a;
-                        int nx = sx + (ea == 0) - (ea == 1);
-                        int ny = sy + (ea == 2) - (ea == 3);
-                        nx = min(max(nx, 0), p.dim - 1);
-                        ny = min(max(ny, 0), p.dim - 1);
-                        const int gx = p.goals[2 * task], gy = p.goals[2 * task + 1];
-                        const int r = (nx == gx && ny == gy) ? 1 : 0;
-                        S.cur[t] = pack_tr(sx, sy, a, nx, ny, r);
-                        S.sx = nx;
-                        S.sy = ny;
-                        S.ret += r;
-                        if (p.actions_out) p.actions_out[(size_t)task * steps_total + step] = a;
-                        if (p.logits_out) {
+                        if (p.memo) {
+                            const int sidx = sx * p.dim + sy;
 #pragma unroll
-                            for (int k = 0; k < kDrA; ++k)
-                                p.logits_out[((size_t)step * p.N + task) * kDrA + k] = lg[k];
+                            for (int k = 0; k < kDrA; ++k) S.memo_lg[sidx][k] = lg[k];
+                            S.memo_ok[sidx] = 1;
                         }
+                        S.nfwd += 1;
+                        finish_step(lg, t, sx, sy);
                     }
                 }
             }
@@ -578,7 +611,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         }
 
         // episode bookkeeping: returns, then shift-append the context (eval_darkroom.py:75-82)
-        if (tid == 0) p.returns_out[(size_t)task * p.Heps + ep] = S.ret;
+        if (tid == 0) {
+            p.returns_out[(size_t)task * p.Heps + ep] = S.ret;
+            if (p.forwards_out) p.forwards_out[(size_t)task * p.Heps + ep] = S.nfwd;
+        }
         const int R = p.R, H = p.horizon;
         int2 v[2] = {make_int2(0, 0), make_int2(0, 0)};
 #pragma unroll
@@ -606,6 +642,14 @@ int launch_pack_fragments(const ModelView& M, float* frag, hipStream_t st) {
 
 int64_t fragments_numel(int n_layer) { return (int64_t)n_layer * FragOff::size; }
 
+static bool g_darkroom_memo = true;  // DPT_TUNE_DARKROOM_MEMO
+
+int set_darkroom_memo(int on) {
+    if (on != 0 && on != 1) return DPT_EINVAL;
+    g_darkroom_memo = on == 1;
+    return DPT_OK;
+}
+
 int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_darkroom_rollout_args& a,
                             hipStream_t st) {
     DarkroomParams p;
@@ -625,6 +669,8 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     p.returns_out = a.returns_out;
     p.actions_out = a.actions_out;
     p.logits_out = a.logits_out;
+    p.forwards_out = a.forwards_out;
+    p.memo = g_darkroom_memo && a.dim * a.dim <= kMemoStates;
     p.frag = frag;
     if (M.n_layer < 2) {
         set_error(DPT_EUNSUPPORTED, "fused darkroom rollout needs n_layer >= 2 (got %d)", M.n_layer);

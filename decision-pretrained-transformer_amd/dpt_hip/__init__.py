@@ -172,11 +172,14 @@ class DeviceModel:
         return out
 
     def rollout_darkroom(self, goals, Heps, horizon, ctx_episodes, dim=10, perms=None, sample=True, temp=1.0,
-                         seed=0, counter=0, first_task=0, uniforms=None, want_actions=False, want_logits=False):
+                         seed=0, counter=0, first_task=0, uniforms=None, want_actions=False, want_logits=False,
+                         want_forwards=False):
         """Fused DarkRoom online evaluation (evals/eval_darkroom.py:20-84) on device.
 
         Returns dict of device tensors: returns (N, Heps) int32, actions (N, Heps*horizon)
-        int32 and logits (Heps*horizon, N, 5) f32 if requested.  Raises
+        int32, logits (Heps*horizon, N, 5) f32 and forwards (N,) int32 (window forwards
+        run per task: one per distinct state per episode under set_darkroom_memo) if
+        requested.  Raises
         NotImplementedError outside sd=2 / A=5 / window <= 128 (use the per-step path).
         """
         dev = device()
@@ -188,12 +191,14 @@ class DeviceModel:
         out = dict(returns=torch.empty((N, int(Heps)), dtype=torch.int32, device=dev))
         out["actions"] = torch.empty((N, steps), dtype=torch.int32, device=dev) if want_actions else None
         out["logits"] = torch.empty((steps, N, 5), dtype=torch.float32, device=dev) if want_logits else None
+        out["forwards"] = torch.empty((N, int(Heps)), dtype=torch.int32, device=dev) if want_forwards else None
         args = _lib.DarkroomRolloutArgs(
             N, int(Heps), int(horizon), int(ctx_episodes), int(dim), int(bool(sample)), int(first_task),
             int(seed) & (2 ** 64 - 1), int(counter), float(temp), 0, _p(goals_d).value,
             None if perms_d is None else _p(perms_d).value, None if u_d is None else _p(u_d).value,
             _p(out["returns"]).value, None if out["actions"] is None else _p(out["actions"]).value,
-            None if out["logits"] is None else _p(out["logits"]).value)
+            None if out["logits"] is None else _p(out["logits"]).value,
+            None if out["forwards"] is None else _p(out["forwards"]).value)
         _lib.call("dpt_rollout_darkroom", self._h, ctypes.byref(args), _stream())
         out["_keep"] = (goals_d, perms_d, u_d)
         return out
@@ -336,6 +341,11 @@ def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=Tr
 def set_decode_tile(tile):
     """Tasks per workgroup of the decode kernels (8: two workgroups per CU; 16: one)."""
     _lib.call("dpt_tuning_set", _lib.TUNE_DECODE_TILE, int(tile))
+
+
+def set_darkroom_memo(on):
+    """DarkRoom rollout: one window forward per distinct query state per episode (default) or per step."""
+    _lib.call("dpt_tuning_set", _lib.TUNE_DARKROOM_MEMO, int(bool(on)))
 
 
 def set_prefill(on):

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdpt_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 DPT_OK = 0
 DPT_EINVAL = -1
@@ -147,6 +147,7 @@ SIGNATURES.update({
 
 TUNE_DECODE_TILE = 1
 TUNE_PREFILL = 2
+TUNE_DARKROOM_MEMO = 3
 SIGNATURES["dpt_tuning_set"] = (_i32, [_i32, _i64])
 
 
@@ -154,7 +155,8 @@ class DarkroomRolloutArgs(ctypes.Structure):
     _fields_ = [("N", _i32), ("Heps", _i32), ("horizon", _i32), ("ctx_episodes", _i32), ("dim", _i32),
                 ("sample", _i32), ("first_task", _i64), ("seed", _u64), ("counter", _u64), ("temp", _f32),
                 ("reserved0", _i32), ("goals", _c_void_p), ("perms", _c_void_p), ("uniforms", _c_void_p),
-                ("returns_out", _c_void_p), ("actions_out", _c_void_p), ("logits_out", _c_void_p)]
+                ("returns_out", _c_void_p), ("actions_out", _c_void_p), ("logits_out", _c_void_p),
+                ("forwards_out", _c_void_p)]
 
 
 SIGNATURES["dpt_prefill_max_window"] = (_i32, [_c_void_p, ctypes.POINTER(_i32)])

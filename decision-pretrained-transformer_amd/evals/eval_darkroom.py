@@ -54,7 +54,8 @@ def _fused_ok(vec_env, controller, H):
             and 1 + H <= _FUSED_MAX_WINDOW and vec_env.dim <= 255)
 
 
-def rollout_fused(vec_env, controller, Heps, H, horizon, want_actions=False, want_logits=False):
+def rollout_fused(vec_env, controller, Heps, H, horizon, want_actions=False, want_logits=False,
+                  want_forwards=False):
     """The whole deploy_online_vec loop as one dpt_rollout_darkroom launch.
 
     Selection draws are the controller's own stream: the counters this loop
@@ -72,7 +73,7 @@ def rollout_fused(vec_env, controller, Heps, H, horizon, want_actions=False, wan
     return dm.rollout_darkroom(vec_env.goals_device, Heps, horizon, H // horizon, dim=vec_env.dim,
                                perms=vec_env.perms_device, sample=controller.sample, temp=controller.temp,
                                seed=seed, counter=ctr0, uniforms=u, want_actions=want_actions,
-                               want_logits=want_logits)
+                               want_logits=want_logits, want_forwards=want_forwards)
 
 
 def deploy_online_vec(vec_env, controller, Heps, H, horizon, fused=True):

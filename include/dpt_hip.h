@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 1
+#define DPT_ABI_VERSION 2
 
 /* error codes (mapped to the reference's Python exceptions by dpt_hip/_lib.py) */
 #define DPT_OK 0
@@ -67,9 +67,14 @@ const char* dpt_last_error(void);
  * two workgroups per CU) or 16.
  * DPT_TUNE_PREFILL = 1 (default): dpt_forward_window runs windows of up to
  * dpt_prefill_max_window() tokens as one MFMA prefill; 0: always position by
- * position through the K/V workspace.  */
+ * position through the K/V workspace.
+ * DPT_TUNE_DARKROOM_MEMO = 1 (default): dpt_rollout_darkroom runs one window
+ * forward per distinct query state per episode (the window is fixed within an
+ * episode, so a repeated state's logits are the same pure function of the same
+ * inputs: results are bit-identical); 0: one forward per step.  */
 #define DPT_TUNE_DECODE_TILE 1
 #define DPT_TUNE_PREFILL 2
+#define DPT_TUNE_DARKROOM_MEMO 3
 int dpt_tuning_set(int32_t key, int64_t value);
 /* number of visible gfx950 devices (0 on a CPU-only host; never faults) */
 int dpt_device_count(int* count_out_host);
@@ -300,6 +305,7 @@ typedef struct dpt_darkroom_rollout_args {
     int32_t* returns_out;       /* (N, Heps) sum of rewards per episode */
     int32_t* actions_out;       /* (N, Heps*horizon) or NULL */
     float* logits_out;          /* (Heps*horizon, N, 5) or NULL */
+    int32_t* forwards_out;      /* (N, Heps) window forwards run per task and episode, or NULL */
 } dpt_darkroom_rollout_args;
 
 int dpt_rollout_darkroom(const dpt_model* model, const dpt_darkroom_rollout_args* args_host,

@@ -312,6 +312,41 @@ def test_rollout_darkroom_large_properties():
         st = ns
 
 
+def test_rollout_darkroom_memo_bit_identical():
+    """The per-episode logits memo (one window forward per distinct query state) changes nothing:
+    actions, per-step logits and returns are bit-identical to one forward per step, and the
+    forward counter equals the number of distinct (episode, state) pairs the trajectory visits."""
+    import dpt_hip
+    _, m, _ = model_from_golden("darkroom")
+    rs = np.random.RandomState(5)
+    N, Heps, horizon, R = 512, 3, 100, 1
+    goals = rs.randint(0, 10, (N, 2))
+    outs = []
+    try:
+        for memo in (False, True):
+            dpt_hip.set_darkroom_memo(memo)
+            o = m.rollout_darkroom(goals, Heps, horizon, R, seed=21, want_actions=True, want_logits=True,
+                                   want_forwards=True)
+            outs.append({k: o[k].cpu().numpy() for k in ("actions", "logits", "returns", "forwards")})
+    finally:
+        dpt_hip.set_darkroom_memo(True)  # the library default
+    off, on = outs
+    for k in ("actions", "logits", "returns"):
+        assert np.array_equal(off[k], on[k]), k
+    assert (off["forwards"] == horizon).all()
+    acts = on["actions"].reshape(N, Heps, horizon)
+    distinct = np.zeros((N, Heps), np.int64)
+    for e in range(Heps):
+        st = np.zeros((N, 2), np.int64)
+        seen = np.zeros((N, 100), bool)
+        for t in range(horizon):
+            seen[np.arange(N), st[:, 0] * 10 + st[:, 1]] = True
+            st, _ = O.darkroom_transit(st, acts[:, e, t], goals)
+        distinct[:, e] = seen.sum(1)
+    assert np.array_equal(on["forwards"], distinct)
+    assert on["forwards"].sum() < off["forwards"].sum()
+
+
 def test_prefill_equals_positionwise_window():
     """The MFMA prefill (4/8/16 waves: windows of 128/256/512 tokens) and the position-by-position K/V path give the
     same logits (out_mode 0 and 1) on random contexts of every model; both within the bar
