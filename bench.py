@@ -49,13 +49,14 @@ def synthetic_state_dict(n_layer, state_dim, action_dim, horizon, seed=0):
 
 def algorithmic_bytes(N, H, n_layer, E=32):
     """Minimal HBM bytes of one fused rollout launch (rollout_bandit_kernel's
-    algorithm): at step h, blocks 1..L-1 stream the K/V rows of positions < h
-    (2*(L-1)*E*4 B each) and block 0 reads the 8-B (action, reward) record of
-    each position < h (its attention is recomputed from the tokens, DESIGN.md);
-    the new K/V rows and record are written, and means[a] (8 B) is read +
-    action (4 B), reward and arm value (8 B each) are written.  wpe and the
-    weights are shared by every task and served from L2 (not counted)."""
-    per_pos = 2 * (n_layer - 1) * E * 4 + 8
+    algorithm): at step h, blocks 1..L-1 stream the cached LayerNorm output y_p
+    of positions < h (E*4 B each; y serves as both key and value on folded
+    weights) and block 0 reads the 8-B (action, reward) record of
+    each position < h (its attention is recomputed from the tokens); the new y
+    rows and record are written, and means[a] (8 B) is read + action (4 B),
+    reward and arm value (8 B each) are written.  wpe and the weights are shared
+    by every task and served from L2 (not counted)."""
+    per_pos = (n_layer - 1) * E * 4 + 8
     per_task = per_pos * H * (H - 1) // 2 + (per_pos + 28) * H
     return N * per_task
 

@@ -52,7 +52,7 @@ int launch_rollout_policy(const dpt_policy_rollout_args&, hipStream_t);
 int launch_pack_fragments(const ModelView&, float*, hipStream_t);
 int64_t fragments_numel(int n_layer);
 int launch_derive_l0(const ModelView&, float*, hipStream_t);
-int64_t l0_numel();
+int64_t l0_numel(int n_layer);
 int launch_rollout_darkroom(const ModelView&, const float*, const dpt_darkroom_rollout_args&, hipStream_t);
 int darkroom_max_window();
 int prefill_max_window(const ModelView&);
@@ -158,7 +158,7 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
     float* frag = nullptr;
     float* l0 = nullptr;
     const size_t frag_bytes = (size_t)fragments_numel(d->n_layer) * sizeof(float);
-    const size_t l0_bytes = (size_t)l0_numel() * sizeof(float);
+    const size_t l0_bytes = (size_t)l0_numel(d->n_layer) * sizeof(float);
     if (hipMalloc(&frag, frag_bytes) != hipSuccess || hipMalloc(&l0, l0_bytes) != hipSuccess) {
         (void)hipFree(blob);
         (void)hipFree(frag);

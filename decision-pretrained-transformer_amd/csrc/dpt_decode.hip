@@ -100,8 +100,9 @@ __host__ inline size_t decode_smem_bytes(const ModelView& M) {
     return sizeof(Smem) + sizeof(float) * (size_t)ParamLDS::make(M.F, M.n_layer, M.A).total;
 }
 
-// Block 0 folded for the K/V-free bandit rollout (ModelView::l0, derived at model
-// creation by derive_l0_kernel).  All matrices [in][out], E x E.
+// Every block folded for the K/V-free bandit rollout (ModelView::l0, one L0Off
+// block per layer, derived at model creation by derive_l0_kernel).  All
+// matrices [in][out], E x E.
 struct L0Off {
     static constexpr int G = 0;                 // Wq Wk^T: u = xn G + g0 = Wk q
     static constexpr int g0 = G + kE * kE;      // Wk bq
@@ -112,21 +113,22 @@ struct L0Off {
 
 // LDS block of the rollout after ParamLDS (offsets in floats): the embedding of
 // every bandit token up to its reward term, base[k] = ((w_s + w_a=k) + w_s') + emb_b
-// for k < A and base[A] = w_s + emb_b (the query token), then g0 and bvp.
+// for k < A and base[A] = w_s + emb_b (the query token), then g0 and bvp of
+// every layer (kE floats per layer each).
 struct RolloutLDS {
     int base, g0, bvp, total;
-    __host__ __device__ static RolloutLDS make(int A) {
+    __host__ __device__ static RolloutLDS make(int A, int L) {
         RolloutLDS r;
         r.base = 0;
         r.g0 = (A + 1) * kE;
-        r.bvp = r.g0 + kE;
-        r.total = r.bvp + kE;
+        r.bvp = r.g0 + L * kE;
+        r.total = r.bvp + L * kE;
         return r;
     }
 };
 
 __host__ inline size_t rollout_smem_bytes(const ModelView& M) {
-    return decode_smem_bytes(M) + sizeof(float) * (size_t)RolloutLDS::make(M.A).total;
+    return decode_smem_bytes(M) + sizeof(float) * (size_t)RolloutLDS::make(M.A, M.n_layer).total;
 }
 
 template <int NT>
@@ -190,6 +192,9 @@ __device__ inline float dpp_sum8(float d) {
 
 // Flash-decoding attention of one task (one wave): positions 0..pos-1 from the
 // cache (global), position pos from LDS.  Writes o = softmax(qK^T/sqrt(E)) V.
+// KV_SAME (the rollout's blocks >= 1): keys and values are one stream (the
+// LayerNorm outputs y_p, see attend_l0 for the algebra), read once.
+template <bool KV_SAME = false>
 __device__ inline void attend_one(const float* __restrict__ kc, const float* __restrict__ vc, int pos,
                                   const float* q, const float* kcur, const float* vcur, float* o,
                                   int lane) {
@@ -207,9 +212,14 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
                 // non-temporal: each K/V row is read once per step by this CU only, so it
                 // must not evict the weights every workgroup re-reads from L2
                 const floatx4 k4 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kc + (size_t)p * kE) + c);
-                const floatx4 v4 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vc + (size_t)p * kE) + c);
                 kk[r] = make_float4(k4[0], k4[1], k4[2], k4[3]);
-                vv[r] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+                if (KV_SAME) {
+                    vv[r] = kk[r];
+                } else {
+                    const floatx4 v4 =
+                        __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vc + (size_t)p * kE) + c);
+                    vv[r] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+                }
             } else {
                 kk[r] = make_float4(0.f, 0.f, 0.f, 0.f);
                 vv[r] = kk[r];
@@ -421,9 +431,12 @@ __device__ inline void zero_smem(Smem& S) {
 //   split-K reduce + residual + next LayerNorm (half-wave per task)
 // `wpe_j` is wpe[pos][tid & 31] (prefetched by the caller); P is the LDS
 // parameter block.
-// L0R (bandit rollout only): block 0 runs K/V-free (attend_l0); layer 0's K slot
-// of each task holds its (a_p, r_p) token records instead, and D is the
-// RolloutLDS block.
+// L0R (bandit rollout only): every block runs on folded weights (L0Off) without
+// K/V.  Block 0 recomputes its inputs from the (a_p, r_p) token records held in
+// layer 0's K slot (attend_l0); block l >= 1 caches y_p = LN1(h_p) (128 B per
+// position, layer l's K slot) instead of K and V (256 B): q . k_p = y_p . u +
+// const with u = Wk q = xn G + g0, and sum_p P_p v_p = (sum_p P_p y_p) Wv + bv, so
+// the same y stream serves as keys and values.  D is the RolloutLDS block.
 template <int TILE, bool L0R = false>
 __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, const ModelView& M,
                                 float* __restrict__ kv, int N, int max_pos, int tile0, int pos, float wpe_j,
@@ -457,10 +470,12 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         const float* W = M.layers + (size_t)li * LayerOff::size;
         const float* PL = P + pl.layers + li * PLay::size;
         const bool l0 = L0R && li == 0;
-        if (l0) {
-            // u = xn G + g0 (= Wk q), two 16-column tiles; block 0 stores no K/V
+        const float* LF = L0R ? M.l0 + (size_t)li * L0Off::size : nullptr;  // this block's folded weights
+        if (L0R) {
+            // u = xn G + g0 (= Wk q), two 16-column tiles; no block stores K/V (block 0
+            // keeps token records, blocks >= 1 their LayerNorm outputs y, stored below)
             if (wave < 2) {
-                const float* B = M.l0 + L0Off::G + wave * 16;
+                const float* B = LF + L0Off::G + wave * 16;
                 float w[8];
 #pragma unroll
                 for (int s = 0; s < 8; ++s) w[s] = __ldg(B + (size_t)(4 * s + kq) * kE + i16);
@@ -469,7 +484,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 for (int s = 0; s < 8; ++s)
                     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(S.xn[i16][4 * s + kq], w[s], acc, 0, 0, 0);
                 const int col = wave * 16 + i16;
-                const float bias = D[RolloutLDS::make(M.A).g0 + col];
+                const float bias = D[RolloutLDS::make(M.A, M.n_layer).g0 + li * kE + col];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int t = kq * 4 + r;
@@ -519,8 +534,10 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 const float* vc = kv + vhalf + li * lstride + (size_t)task * max_pos * kE;
                 if (l0)
                     attend_l0(reinterpret_cast<const float2*>(kc), M.wpe, pos, S.q[wave], S.x[wave],
-                              D + RolloutLDS::make(M.A).base, P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
-                              PL + PLay::ln1_b, S.o[wave], lane);
+                              D + RolloutLDS::make(M.A, M.n_layer).base, P + pl.emb_w + (2 + M.A) * kE,
+                              PL + PLay::ln1_g, PL + PLay::ln1_b, S.o[wave], lane);
+                else if (L0R)  // scores y_p . u, output sum_p P_p y_p; y_pos is in S.kcur
+                    attend_one<true>(kc, kc, pos, S.q[wave], S.kcur[wave], S.kcur[wave], S.o[wave], lane);
                 else
                     attend_one(kc, vc, pos, S.q[wave], S.kcur[wave], S.vcur[wave], S.o[wave], lane);
             }
@@ -529,7 +546,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         DPT_STAMP(2);
         // c_proj + residual + ln_2, one wave: both 16-column tiles, rows reduced over 16 lanes
         if (wave == kProjWave) {
-            const float* B = l0 ? M.l0 + L0Off::Wvp : W + LayerOff::proj_w;
+            const float* B = L0R ? LF + L0Off::Wvp : W + LayerOff::proj_w;
             float w0[8], w1[8];
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
@@ -544,7 +561,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w1[s], a1, 0, 0, 0);
             }
             const int c0 = i16, c1 = 16 + i16;
-            const float* pb = l0 ? D + RolloutLDS::make(M.A).bvp : PL + PLay::proj_b;
+            const float* pb = L0R ? D + RolloutLDS::make(M.A, M.n_layer).bvp + li * kE : PL + PLay::proj_b;
             const float b0 = pb[c0], b1 = pb[c1];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -614,7 +631,14 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
             const bool last = li + 1 == M.n_layer;
             const float g = last ? P[pl.lnf_g + j] : PL[PLay::size + PLay::ln1_g + j];
             const float b = last ? P[pl.lnf_b + j] : PL[PLay::size + PLay::ln1_b + j];
-            S.xn[t][j] = ln_halfwave(x, g, b);
+            const float y = ln_halfwave(x, g, b);
+            S.xn[t][j] = y;
+            if (L0R && !last) {  // block li+1's y at `pos`: its K/V-cache row (128 B per half-wave)
+                S.kcur[t][j] = y;
+                const int task = tile0 + t;
+                if (task < N)
+                    __builtin_nontemporal_store(y, kv + (li + 1) * lstride + ((size_t)task * max_pos + pos) * kE + j);
+            }
         }
         bar_lds();
         DPT_STAMP(5);
@@ -779,7 +803,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
     }
     // block 0 runs K/V-free (attend_l0): token embedding table and folded biases in LDS
     float* D = P + pl.total;
-    const RolloutLDS rl = RolloutLDS::make(A);
+    const RolloutLDS rl = RolloutLDS::make(A, M.n_layer);
     for (int i = tid; i < (A + 1) * kE; i += TILE * 64) {
         const int k = i / kE, j = i % kE;
         const float* ew = P + pl.emb_w;
@@ -787,9 +811,10 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         const float acc = (k < A) ? (ew[j] + ew[(1 + k) * kE + j]) + ew[(1 + A) * kE + j] : ew[j];
         D[rl.base + i] = acc + P[pl.emb_b + j];
     }
-    for (int j = tid; j < kE; j += TILE * 64) {
-        D[rl.g0 + j] = M.l0[L0Off::g0 + j];
-        D[rl.bvp + j] = M.l0[L0Off::bvp + j];
+    for (int i = tid; i < M.n_layer * kE; i += TILE * 64) {
+        const int li = i / kE, j = i % kE;
+        D[rl.g0 + i] = M.l0[(size_t)li * L0Off::size + L0Off::g0 + j];
+        D[rl.bvp + i] = M.l0[(size_t)li * L0Off::size + L0Off::bvp + j];
     }
     // per task, block 0's K slot holds the (a_p, r_p) record of every position
     auto tokrec = [&](int task) {
@@ -857,9 +882,11 @@ ModelView make_view(const float* blob, const dpt_model_desc& d) {
     return v;
 }
 
-// ModelView::l0 from block 0's weights (fp64 sums, one rounding per element).
-__global__ void derive_l0_kernel(ModelView M, float* __restrict__ l0) {
-    const float* W = M.layers;
+// ModelView::l0 from every block's weights (fp64 sums, one rounding per
+// element); workgroup li derives block li.
+__global__ void derive_l0_kernel(ModelView M, float* __restrict__ l0_all) {
+    const float* W = M.layers + (size_t)blockIdx.x * LayerOff::size;
+    float* l0 = l0_all + (size_t)blockIdx.x * L0Off::size;
     const float* aw = W + LayerOff::attn_w;  // [E][3E]: q | k | v columns
     const float* ab = W + LayerOff::attn_b;
     const float* pw = W + LayerOff::proj_w;  // [E][E]
@@ -883,10 +910,10 @@ __global__ void derive_l0_kernel(ModelView M, float* __restrict__ l0) {
     }
 }
 
-int64_t l0_numel() { return L0Off::size; }
+int64_t l0_numel(int n_layer) { return (int64_t)n_layer * L0Off::size; }
 
 int launch_derive_l0(const ModelView& M, float* l0, hipStream_t st) {
-    hipLaunchKernelGGL(derive_l0_kernel, dim3(1), dim3(256), 0, st, M, l0);
+    hipLaunchKernelGGL(derive_l0_kernel, dim3(M.n_layer), dim3(256), 0, st, M, l0);
     return check_hip(hipGetLastError(), "derive_l0_kernel launch");
 }
 
