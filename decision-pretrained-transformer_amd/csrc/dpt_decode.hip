@@ -51,6 +51,10 @@ namespace dpt {
 constexpr int kM = 16;                    // MFMA rows = task slots in LDS (TILE <= 16 are live)
 constexpr int kLdE = kE + 2;              // padded LDS row strides (conflict-free A reads)
 constexpr int kRows = 4;                  // K/V rows (of 8 positions) in flight per wave
+#ifndef DPT_YROWS
+#define DPT_YROWS 8
+#endif
+constexpr int kYRows = DPT_YROWS;         // y rows in flight per wave (rollout blocks >= 1; 8: -1.5 % vs 4)
 constexpr int kChunks = kFF / 16;         // hidden-unit chunks of the fused c_fc -> mlp.c_proj
 
 // barrier for LDS hand-offs only: does not wait for outstanding global stores
@@ -194,7 +198,7 @@ __device__ inline float dpp_sum8(float d) {
 // cache (global), position pos from LDS.  Writes o = softmax(qK^T/sqrt(E)) V.
 // KV_SAME (the rollout's blocks >= 1): keys and values are one stream (the
 // LayerNorm outputs y_p, see attend_l0 for the algebra), read once.
-template <bool KV_SAME = false>
+template <bool KV_SAME = false, int NR = kRows>
 __device__ inline void attend_one(const float* __restrict__ kc, const float* __restrict__ vc, int pos,
                                   const float* q, const float* kcur, const float* vcur, float* o,
                                   int lane) {
@@ -203,10 +207,10 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
     const float4 q4 = *reinterpret_cast<const float4*>(q + 4 * c);
     float m = -1e30f, l = 0.f;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int base = 0; base < pos; base += 8 * kRows) {
-        float4 kk[kRows], vv[kRows];
+    for (int base = 0; base < pos; base += 8 * NR) {
+        float4 kk[NR], vv[NR];
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
+        for (int r = 0; r < NR; ++r) {
             const int p = base + 8 * r + g;
             if (p < pos) {
                 // non-temporal: each K/V row is read once per step by this CU only, so it
@@ -225,10 +229,10 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
                 vv[r] = kk[r];
             }
         }
-        float s[kRows];
+        float s[NR];
         float mx = -1e30f;
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
+        for (int r = 0; r < NR; ++r) {
             float d = q4.x * kk[r].x;
             d = fmaf(q4.y, kk[r].y, d);
             d = fmaf(q4.z, kk[r].z, d);
@@ -243,7 +247,7 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
         l *= corr;
         acc.x *= corr; acc.y *= corr; acc.z *= corr; acc.w *= corr;
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
+        for (int r = 0; r < NR; ++r) {
             const float pr = __builtin_amdgcn_exp2f(s[r] - mn);
             l += pr;
             acc.x = fmaf(pr, vv[r].x, acc.x);
@@ -537,7 +541,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                               D + RolloutLDS::make(M.A, M.n_layer).base, P + pl.emb_w + (2 + M.A) * kE,
                               PL + PLay::ln1_g, PL + PLay::ln1_b, S.o[wave], lane);
                 else if (L0R)  // scores y_p . u, output sum_p P_p y_p; y_pos is in S.kcur
-                    attend_one<true>(kc, kc, pos, S.q[wave], S.kcur[wave], S.kcur[wave], S.o[wave], lane);
+                    attend_one<true, kYRows>(kc, kc, pos, S.q[wave], S.kcur[wave], S.kcur[wave], S.o[wave], lane);
                 else
                     attend_one(kc, vc, pos, S.q[wave], S.kcur[wave], S.vcur[wave], S.o[wave], lane);
             }

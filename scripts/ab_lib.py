@@ -1,0 +1,58 @@
+"""A/B of library builds (Makefile `variants`): one bandit rollout timing per library,
+each in its own process (python scripts/ab_lib.py libA.so libB.so ...; rounds alternate).
+Env: AB_H, AB_N, AB_A, AB_TILE, AB_ROUNDS."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(lib):
+    sys.path[:0] = [os.path.join(ROOT, "decision-pretrained-transformer_amd"), ROOT]
+    from dpt_hip import _lib
+    _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.__file__), lib)
+    import torch
+    import bench
+    import dpt_hip
+    H, N, A = (int(os.environ.get(k, d)) for k, d in (("AB_H", "500"), ("AB_N", "4096"), ("AB_A", "5")))
+    dpt_hip.set_decode_tile(int(os.environ.get("AB_TILE", "8")))
+    sd, _ = bench.synthetic_state_dict(4, 1, A, H)
+    m = dpt_hip.DeviceModel(sd, 4, 1, A, 4 * (1 + H))
+    means = torch.from_numpy(np.random.RandomState(1).uniform(0, 1, (N, A))).cuda()
+    ts = []
+    for rnd in range(4):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = m.rollout_bandit(means, H, 0.3, True, seed=rnd)
+        b.record()
+        torch.cuda.synchronize()
+        if rnd > 0:
+            ts.append(a.elapsed_time(b))
+    chk = float(out["arm_value"].sum())
+    print(json.dumps({"lib": lib, "ms": ts, "checksum": chk}))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--child":
+        child(sys.argv[2])
+        sys.exit(0)
+    res = {lib: [] for lib in sys.argv[1:]}
+    chk = {}
+    for rnd in range(int(os.environ.get("AB_ROUNDS", "2"))):
+        for lib in sys.argv[1:]:
+            out = subprocess.run([sys.executable, __file__, "--child", lib], check=True, capture_output=True,
+                                 text=True, timeout=300).stdout.strip().splitlines()[-1]
+            d = json.loads(out)
+            res[lib] += d["ms"]
+            chk[lib] = d["checksum"]
+    H, N = int(os.environ.get("AB_H", "500")), int(os.environ.get("AB_N", "4096"))
+    sys.path[:0] = [ROOT]
+    import bench
+    ab = bench.algorithmic_bytes(N, H, 4)
+    print(json.dumps({lib: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)),
+                            "TBps": ab / (np.median(v) * 1e-3) / 1e12, "checksum": chk[lib]}
+                      for lib, v in res.items()}))
