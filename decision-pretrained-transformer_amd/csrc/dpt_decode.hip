@@ -162,27 +162,6 @@ __device__ inline void load_params(float* P, const ParamLDS& pl, const ModelView
     for (int i = tid; i < M.A; i += NT) P[pl.head_b + i] = M.head_b[i];
 }
 
-// LayerNorm of one 32-wide row held by the 32 lanes of a half-wave.
-__device__ inline float ln_halfwave(float v, float g, float b) {
-    float s = v;
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) s += __shfl_xor(s, off, 32);
-    const float mean = s * (1.0f / kE);
-    const float d = v - mean;
-    float s2 = d * d;
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) s2 += __shfl_xor(s2, off, 32);
-    const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
-    return fmaf(d * rstd, g, b);
-}
-
-__device__ inline float gelu_new(float x) {
-    // 0.5*x*(1 + tanh(sqrt(2/pi)*(x + 0.044715*x^3)))  (transformers/activations.py:65)
-    const float k0 = 0.7978845608028654f;
-    float inner = k0 * (x + 0.044715f * (x * x * x));
-    return 0.5f * x * (1.0f + tanhf(inner));
-}
-
 // Sum over the 8 lanes of an aligned lane group with DPP (VALU, no LDS
 // round trip): xor 1 and xor 2 by quad_perm, then row_half_mirror pairs the two
 // quads of the group.  Every lane of the group gets the same value, bit-identical
@@ -192,6 +171,40 @@ __device__ inline float dpp_sum8(float d) {
     d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x4E, 0xF, 0xF, false));
     d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x141, 0xF, 0xF, false));
     return d;
+}
+
+// Sum over the 16 lanes of a DPP row: dpp_sum8, then row_mirror (lane i <-> 15-i)
+// pairs the row's two 8-lane groups (every lane of a group holds its group sum,
+// so this equals the xor-8 step).
+__device__ inline float dpp_sum16(float d) {
+    d = dpp_sum8(d);
+    d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x140, 0xF, 0xF, false));
+    return d;
+}
+
+// lane i <- lane i ^ 8 (row_ror:8 within each 16-lane row)
+__device__ inline float dpp_xor8(float d) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x128, 0xF, 0xF, false));
+}
+
+// LayerNorm of one 32-wide row held by the 32 lanes of a half-wave: the two
+// row sums are 16-lane DPP reductions plus one xor-16 exchange.
+__device__ inline float ln_halfwave(float v, float g, float b) {
+    float s = dpp_sum16(v);
+    s += __shfl_xor(s, 16, 32);
+    const float mean = s * (1.0f / kE);
+    const float d = v - mean;
+    float s2 = dpp_sum16(d * d);
+    s2 += __shfl_xor(s2, 16, 32);
+    const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
+    return fmaf(d * rstd, g, b);
+}
+
+__device__ inline float gelu_new(float x) {
+    // 0.5*x*(1 + tanh(sqrt(2/pi)*(x + 0.044715*x^3)))  (transformers/activations.py:65)
+    const float k0 = 0.7978845608028654f;
+    float inner = k0 * (x + 0.044715f * (x * x * x));
+    return 0.5f * x * (1.0f + tanhf(inner));
 }
 
 // Flash-decoding attention of one task (one wave): positions 0..pos-1 from the
@@ -279,11 +292,12 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
         }
     }
 #pragma unroll
-    for (int off = 8; off <= 32; off <<= 1) {
-        const float mo = __shfl_xor(m, off);
-        const float lo = __shfl_xor(l, off);
-        const float ax = __shfl_xor(acc.x, off), ay = __shfl_xor(acc.y, off);
-        const float az = __shfl_xor(acc.z, off), aw = __shfl_xor(acc.w, off);
+    for (int off = 8; off <= 32; off <<= 1) {  // xor 8 by DPP (row_ror:8), 16 and 32 by ds_bpermute
+        auto xch = [&](float v) { return off == 8 ? dpp_xor8(v) : __shfl_xor(v, off); };
+        const float mo = xch(m);
+        const float lo = xch(l);
+        const float ax = xch(acc.x), ay = xch(acc.y);
+        const float az = xch(acc.z), aw = xch(acc.w);
         const float mn = fmaxf(m, mo);
         const float sa = __builtin_amdgcn_exp2f(m - mn), sb = __builtin_amdgcn_exp2f(mo - mn);
         l = l * sa + lo * sb;
@@ -398,11 +412,12 @@ __device__ inline void attend_l0(const float2* __restrict__ tok, const float* __
         }
     }
 #pragma unroll
-    for (int off = 8; off <= 32; off <<= 1) {
-        const float mo = __shfl_xor(m, off);
-        const float lo = __shfl_xor(l, off);
-        const float ax = __shfl_xor(acc.x, off), ay = __shfl_xor(acc.y, off);
-        const float az = __shfl_xor(acc.z, off), aw = __shfl_xor(acc.w, off);
+    for (int off = 8; off <= 32; off <<= 1) {  // xor 8 by DPP (row_ror:8), 16 and 32 by ds_bpermute
+        auto xch = [&](float v) { return off == 8 ? dpp_xor8(v) : __shfl_xor(v, off); };
+        const float mo = xch(m);
+        const float lo = xch(l);
+        const float ax = xch(acc.x), ay = xch(acc.y);
+        const float az = xch(acc.z), aw = xch(acc.w);
         const float mn = fmaxf(m, mo);
         const float sa = __builtin_amdgcn_exp2f(m - mn), sb = __builtin_amdgcn_exp2f(mo - mn);
         l = l * sa + lo * sb;
@@ -573,13 +588,11 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 const float x0 = (a0[r] + b0) + S.x[t][c0];
                 const float x1 = (a1[r] + b1) + S.x[t][c1];
                 float s = x0 + x1;
-#pragma unroll
-                for (int off = 1; off <= 8; off <<= 1) s += __shfl_xor(s, off);
+                s = dpp_sum16(s);
                 const float mean = s * (1.0f / kE);
                 const float d0 = x0 - mean, d1 = x1 - mean;
                 float s2 = d0 * d0 + d1 * d1;
-#pragma unroll
-                for (int off = 1; off <= 8; off <<= 1) s2 += __shfl_xor(s2, off);
+                s2 = dpp_sum16(s2);
                 const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
                 if (t < TILE) {
                     S.x[t][c0] = x0;
@@ -838,27 +851,32 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         if (h + 1 < Pr.H) wpe_next = M.wpe[(size_t)(h + 1) * kE + (tid & 31)];
         const double2 dr = draws ? draws[h] : make_double2(0.0, 0.0);  // consumed after the forward
         decode_position<TILE, true>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D);
-        if (tid < TILE) {
-            const int t = tid, task = tile0 + t;
-            if (task < Pr.N) {
-                const int a = select_from_logits(S.logits[t], A, Pr.sample, 1.0f, dr.x);
-                const double mean = S.means[t][a];
-                const double r = (Pr.type == DPT_BANDIT_BERNOULLI) ? ((dr.y < mean) ? 1.0 : 0.0)
-                                                                  : gaussian_reward(mean, Pr.var, dr.y);
-                Pr.actions_out[(size_t)task * Pr.H + h] = a;
-                Pr.rewards_out[(size_t)task * Pr.H + h] = r;
-                Pr.arm_value_out[(size_t)task * Pr.H + h] = mean;
-                if (Pr.logits_out)
-                    for (int k = 0; k < A; ++k) Pr.logits_out[((size_t)h * Pr.N + task) * A + k] = S.logits[t][k];
-                // next token = transition h: [s=1, onehot(a), s'=1, float(r)] (eval_bandit.py:83-86)
-                S.tok[t][0] = 1.f;
-                for (int k = 0; k < A; ++k) S.tok[t][1 + k] = (k == a) ? 1.f : 0.f;
-                S.tok[t][1 + A] = 1.f;
-                S.tok[t][2 + A] = (float)r;
-                if (h + 1 < Pr.H) tokrec(task)[h + 1] = make_float2(__int_as_float(a * kE), (float)r);
-            }
+        // selection + env step; the outputs are stored after the barrier so that it
+        // waits only for the y rows (issued phases earlier), not for these stores
+        const int t = tid, task = tile0 + t;
+        const bool live = tid < TILE && task < Pr.N;
+        int a = 0;
+        double mean = 0.0, r = 0.0;
+        if (live) {
+            a = select_from_logits(S.logits[t], A, Pr.sample, 1.0f, dr.x);
+            mean = S.means[t][a];
+            r = (Pr.type == DPT_BANDIT_BERNOULLI) ? ((dr.y < mean) ? 1.0 : 0.0) : gaussian_reward(mean, Pr.var, dr.y);
+            // next token = transition h: [s=1, onehot(a), s'=1, float(r)] (eval_bandit.py:83-86)
+            S.tok[t][0] = 1.f;
+            for (int k = 0; k < A; ++k) S.tok[t][1 + k] = (k == a) ? 1.f : 0.f;
+            S.tok[t][1 + A] = 1.f;
+            S.tok[t][2 + A] = (float)r;
         }
-        __syncthreads();  // K/V stores of step h visible before step h+1 reads them
+        __syncthreads();  // y rows of step h visible before step h+1 reads them
+        if (live) {
+            Pr.actions_out[(size_t)task * Pr.H + h] = a;
+            Pr.rewards_out[(size_t)task * Pr.H + h] = r;
+            Pr.arm_value_out[(size_t)task * Pr.H + h] = mean;
+            if (Pr.logits_out)  // S.logits is next rewritten by step h+1's head phase
+                for (int k = 0; k < A; ++k) Pr.logits_out[((size_t)h * Pr.N + task) * A + k] = S.logits[t][k];
+            // first read from memory by step h+2 (positions < h+2), so it may land during step h+1
+            if (h + 1 < Pr.H) tokrec(task)[h + 1] = make_float2(__int_as_float(a * kE), (float)r);
+        }
         DPT_STAMP(7);
     }
 }
