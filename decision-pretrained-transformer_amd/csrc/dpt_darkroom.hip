@@ -128,41 +128,6 @@ __device__ inline int2 pack_tr(int x, int y, int a, int nx, int ny, int r) {
     return make_int2(x | (y << 8) | (a << 16) | (r << 24), nx | (ny << 8));
 }
 
-// Fixed-A twin of select_from_logits (dpt_common.h): same arithmetic, the
-// logits stay in registers.
-template <int NA>
-__device__ inline int select_fixed(const float (&lg)[NA], int sample, float temp, double u) {
-    if (!sample) {
-        int best = 0;
-        float bv = lg[0];
-#pragma unroll
-        for (int k = 1; k < NA; ++k)
-            if (lg[k] > bv) { bv = lg[k]; best = k; }
-        return best;
-    }
-    float xk[NA], ek[NA];
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < NA; ++k) {
-        xk[k] = (temp == 1.0f) ? lg[k] : lg[k] / temp;
-        m = fmaxf(m, xk[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < NA; ++k) ek[k] = expf(xk[k] - m);
-    const float s = np_pairwise_sum_f32([&](int k) { return ek[k]; }, NA);
-    double total = 0.0;
-#pragma unroll
-    for (int k = 0; k < NA; ++k) total += (double)(ek[k] / s);
-    double c = 0.0;
-    int idx = 0;
-#pragma unroll
-    for (int k = 0; k < NA; ++k) {
-        c += (double)(ek[k] / s);
-        idx += (c / total <= u) ? 1 : 0;
-    }
-    return idx < NA ? idx : NA - 1;
-}
-
 struct DarkroomParams {
     int N, Heps, horizon, R, dim, sample;
     int64_t first_task;

@@ -120,13 +120,14 @@ struct L0Off {
 // for k < A and base[A] = w_s + emb_b (the query token), then g0 and bvp of
 // every layer (kE floats per layer each).
 struct RolloutLDS {
-    int base, g0, bvp, total;
+    int base, g0, bvp, wvp, total;
     __host__ __device__ static RolloutLDS make(int A, int L) {
         RolloutLDS r;
         r.base = 0;
         r.g0 = (A + 1) * kE;
         r.bvp = r.g0 + L * kE;
-        r.total = r.bvp + L * kE;
+        r.wvp = r.bvp + L * kE;  // Wv Wproj of every layer (c_proj's B operand, read from LDS)
+        r.total = r.wvp + L * kE * kE;
         return r;
     }
 };
@@ -565,12 +566,12 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         DPT_STAMP(2);
         // c_proj + residual + ln_2, one wave: both 16-column tiles, rows reduced over 16 lanes
         if (wave == kProjWave) {
-            const float* B = L0R ? LF + L0Off::Wvp : W + LayerOff::proj_w;
+            const float* B = L0R ? D + RolloutLDS::make(M.A, M.n_layer).wvp + li * kE * kE : W + LayerOff::proj_w;
             float w0[8], w1[8];
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
-                w0[s] = __ldg(B + (size_t)(4 * s + kq) * kE + i16);
-                w1[s] = __ldg(B + (size_t)(4 * s + kq) * kE + 16 + i16);
+                w0[s] = L0R ? B[(4 * s + kq) * kE + i16] : __ldg(B + (size_t)(4 * s + kq) * kE + i16);
+                w1[s] = L0R ? B[(4 * s + kq) * kE + 16 + i16] : __ldg(B + (size_t)(4 * s + kq) * kE + 16 + i16);
             }
             floatx4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -806,6 +807,21 @@ __global__ void rollout_draws_kernel(BanditRolloutParams Pr) {
     draw_pairs(Pr, task)[h] = make_double2(u, g);
 }
 
+// select_from_logits with the logits in registers for the configured arm counts
+// (5: the bandit configs, 20: the linear-bandit config).
+__device__ inline int select_rollout(const float* logits, int A, int sample, double u) {
+    auto fixed = [&](auto na) {
+        constexpr int NA = decltype(na)::value;
+        float lg[NA];
+#pragma unroll
+        for (int k = 0; k < NA; ++k) lg[k] = logits[k];
+        return select_fixed<NA>(lg, sample, 1.0f, u);
+    };
+    if (A == 5) return fixed(std::integral_constant<int, 5>{});
+    if (A == 20) return fixed(std::integral_constant<int, 20>{});
+    return select_from_logits(logits, A, sample, 1.0f, u);
+}
+
 // The bandit online loop (evals/eval_bandit.py:70-89) for one tile of tasks,
 // all H steps: decode -> select -> env step -> append transition.
 template <int TILE>
@@ -833,6 +849,10 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         D[rl.g0 + i] = M.l0[(size_t)li * L0Off::size + L0Off::g0 + j];
         D[rl.bvp + i] = M.l0[(size_t)li * L0Off::size + L0Off::bvp + j];
     }
+    for (int i = tid; i < M.n_layer * kE * kE; i += TILE * 64) {
+        const int li = i / (kE * kE), j = i % (kE * kE);
+        D[rl.wvp + i] = M.l0[(size_t)li * L0Off::size + L0Off::Wvp + j];
+    }
     // per task, block 0's K slot holds the (a_p, r_p) record of every position
     auto tokrec = [&](int task) {
         return reinterpret_cast<float2*>(Pr.kv + (size_t)task * Pr.H * kE);
@@ -858,7 +878,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         int a = 0;
         double mean = 0.0, r = 0.0;
         if (live) {
-            a = select_from_logits(S.logits[t], A, Pr.sample, 1.0f, dr.x);
+            a = select_rollout(S.logits[t], A, Pr.sample, dr.x);
             mean = S.means[t][a];
             r = (Pr.type == DPT_BANDIT_BERNOULLI) ? ((dr.y < mean) ? 1.0 : 0.0) : gaussian_reward(mean, Pr.var, dr.y);
             // next token = transition h: [s=1, onehot(a), s'=1, float(r)] (eval_bandit.py:83-86)
