@@ -74,7 +74,6 @@ struct Smem {
     float part[kChunks][kM][kE]; // mlp.c_proj partial sums, one per 16-unit hidden chunk
     float logits[kM][kMaxA];
     float tok[kM][kMaxF];        // packed token features of the current position
-    double means[kM][kMaxA];     // the tile's arm means (rollout)
 };
 static_assert(sizeof(Smem) % 16 == 0, "parameter block must start 16-B aligned");
 
@@ -118,22 +117,24 @@ struct L0Off {
 // LDS block of the rollout after ParamLDS (offsets in floats): the embedding of
 // every bandit token up to its reward term, base[k] = ((w_s + w_a=k) + w_s') + emb_b
 // for k < A and base[A] = w_s + emb_b (the query token), then g0 and bvp of
-// every layer (kE floats per layer each).
+// every layer (kE floats per layer each) and the folded matrices Wvp and G.
 struct RolloutLDS {
-    int base, g0, bvp, wvp, total;
-    __host__ __device__ static RolloutLDS make(int A, int L) {
+    int means, base, g0, bvp, wvp, G, total;
+    __host__ __device__ static RolloutLDS make(int A, int L, bool with_G = true) {
         RolloutLDS r;
-        r.base = 0;
-        r.g0 = (A + 1) * kE;
+        r.means = 0;               // the tile's arm means, double [kM][A]
+        r.base = 2 * kM * A;
+        r.g0 = r.base + (A + 1) * kE;
         r.bvp = r.g0 + L * kE;
         r.wvp = r.bvp + L * kE;  // Wv Wproj of every layer (c_proj's B operand, read from LDS)
-        r.total = r.wvp + L * kE * kE;
+        r.G = r.wvp + L * kE * kE;  // Wq Wk^T of every layer (the u projection's B operand)
+        r.total = r.G + (with_G ? L * kE * kE : 0);
         return r;
     }
 };
 
-__host__ inline size_t rollout_smem_bytes(const ModelView& M) {
-    return decode_smem_bytes(M) + sizeof(float) * (size_t)RolloutLDS::make(M.A, M.n_layer).total;
+__host__ inline size_t rollout_smem_bytes(const ModelView& M, bool with_G) {
+    return decode_smem_bytes(M) + sizeof(float) * (size_t)RolloutLDS::make(M.A, M.n_layer, with_G).total;
 }
 
 template <int NT>
@@ -457,7 +458,7 @@ __device__ inline void zero_smem(Smem& S) {
 // position, layer l's K slot) instead of K and V (256 B): q . k_p = y_p . u +
 // const with u = Wk q = xn G + g0, and sum_p P_p v_p = (sum_p P_p y_p) Wv + bv, so
 // the same y stream serves as keys and values.  D is the RolloutLDS block.
-template <int TILE, bool L0R = false>
+template <int TILE, bool L0R = false, bool GL = false>
 __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, const ModelView& M,
                                 float* __restrict__ kv, int N, int max_pos, int tile0, int pos, float wpe_j,
                                 const float* D = nullptr) {
@@ -490,15 +491,16 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         const float* W = M.layers + (size_t)li * LayerOff::size;
         const float* PL = P + pl.layers + li * PLay::size;
         const bool l0 = L0R && li == 0;
-        const float* LF = L0R ? M.l0 + (size_t)li * L0Off::size : nullptr;  // this block's folded weights
         if (L0R) {
             // u = xn G + g0 (= Wk q), two 16-column tiles; no block stores K/V (block 0
             // keeps token records, blocks >= 1 their LayerNorm outputs y, stored below)
             if (wave < 2) {
-                const float* B = LF + L0Off::G + wave * 16;
+                // G from LDS (GL: the rollout's LDS block has room for it) or from L2
+                const float* B = GL ? D + RolloutLDS::make(M.A, M.n_layer).G + li * kE * kE + wave * 16
+                                    : M.l0 + (size_t)li * L0Off::size + L0Off::G + wave * 16;
                 float w[8];
 #pragma unroll
-                for (int s = 0; s < 8; ++s) w[s] = __ldg(B + (size_t)(4 * s + kq) * kE + i16);
+                for (int s = 0; s < 8; ++s) w[s] = GL ? B[(4 * s + kq) * kE + i16] : __ldg(B + (4 * s + kq) * kE + i16);
                 floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < 8; ++s)
@@ -824,19 +826,20 @@ __device__ inline int select_rollout(const float* logits, int A, int sample, dou
 
 // The bandit online loop (evals/eval_bandit.py:70-89) for one tile of tasks,
 // all H steps: decode -> select -> env step -> append transition.
-template <int TILE>
+template <int TILE, bool GL>
 __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView M, BanditRolloutParams Pr) {
     DPT_SMEM_SETUP(TILE)
     const int tile0 = blockIdx.x * TILE;
     const int tid = threadIdx.x;
     const int A = Pr.A;
+    // block 0 runs K/V-free (attend_l0): token embedding table and folded weights in LDS
+    float* D = P + pl.total;
+    const RolloutLDS rl = RolloutLDS::make(A, M.n_layer, GL);
+    double* means = reinterpret_cast<double*>(D + rl.means);
     for (int i = tid; i < TILE * A; i += TILE * 64) {
         const int t = i / A, k = i % A;
-        S.means[t][k] = (tile0 + t < Pr.N) ? Pr.means[(size_t)(tile0 + t) * A + k] : 0.0;
+        means[i] = (tile0 + t < Pr.N) ? Pr.means[(size_t)(tile0 + t) * A + k] : 0.0;
     }
-    // block 0 runs K/V-free (attend_l0): token embedding table and folded biases in LDS
-    float* D = P + pl.total;
-    const RolloutLDS rl = RolloutLDS::make(A, M.n_layer);
     for (int i = tid; i < (A + 1) * kE; i += TILE * 64) {
         const int k = i / kE, j = i % kE;
         const float* ew = P + pl.emb_w;
@@ -852,6 +855,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
     for (int i = tid; i < M.n_layer * kE * kE; i += TILE * 64) {
         const int li = i / (kE * kE), j = i % (kE * kE);
         D[rl.wvp + i] = M.l0[(size_t)li * L0Off::size + L0Off::Wvp + j];
+        if (GL) D[rl.G + i] = M.l0[(size_t)li * L0Off::size + L0Off::G + j];
     }
     // per task, block 0's K slot holds the (a_p, r_p) record of every position
     auto tokrec = [&](int task) {
@@ -870,7 +874,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         const float wpe_j = wpe_next;
         if (h + 1 < Pr.H) wpe_next = M.wpe[(size_t)(h + 1) * kE + (tid & 31)];
         const double2 dr = draws ? draws[h] : make_double2(0.0, 0.0);  // consumed after the forward
-        decode_position<TILE, true>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D);
+        decode_position<TILE, true, GL>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D);
         // selection + env step; the outputs are stored after the barrier so that it
         // waits only for the y rows (issued phases earlier), not for these stores
         const int t = tid, task = tile0 + t;
@@ -879,7 +883,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         double mean = 0.0, r = 0.0;
         if (live) {
             a = select_rollout(S.logits[t], A, Pr.sample, dr.x);
-            mean = S.means[t][a];
+            mean = means[t * A + a];
             r = (Pr.type == DPT_BANDIT_BERNOULLI) ? ((dr.y < mean) ? 1.0 : 0.0) : gaussian_reward(mean, Pr.var, dr.y);
             // next token = transition h: [s=1, onehot(a), s'=1, float(r)] (eval_bandit.py:83-86)
             S.tok[t][0] = 1.f;
@@ -1039,7 +1043,11 @@ int launch_window_decode(const ModelView& M, float* kv, int N, int C, const floa
 int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, hipStream_t st) {
     size_t sm;
     if (int rc = check_smem(M, &sm)) return rc;
-    sm = rollout_smem_bytes(M);
+    // G in LDS when the block still lets the tile's workgroups share a CU (two at
+    // tile 8, one at tile 16); otherwise the u projection reads it from L2
+    const size_t per_cu = 160 * 1024 / (g_decode_tile == 8 ? 2 : 1);
+    const bool gl = rollout_smem_bytes(M, true) <= per_cu;
+    sm = rollout_smem_bytes(M, gl);
     if (sm > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "rollout LDS %zu B > 160 KiB (n_layer=%d, action_dim=%d)", sm, M.n_layer, M.A);
         return DPT_EUNSUPPORTED;
@@ -1057,12 +1065,14 @@ int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, 
     P.n_layer = M.n_layer;
     const int64_t nd = (int64_t)a.N * a.H;
     hipLaunchKernelGGL(rollout_draws_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st, P);
-    allow_smem(rollout_bandit_kernel<8>, sm);
-    allow_smem(rollout_bandit_kernel<16>, sm);
+    auto launch = [&](auto kernel, int tile) {
+        allow_smem(kernel, sm);
+        hipLaunchKernelGGL(kernel, dim3((a.N + tile - 1) / tile), dim3(tile * 64), sm, st, M, P);
+    };
     if (g_decode_tile == 8)
-        hipLaunchKernelGGL(rollout_bandit_kernel<8>, tiles<8>(a.N), dim3(512), sm, st, M, P);
+        gl ? launch(rollout_bandit_kernel<8, true>, 8) : launch(rollout_bandit_kernel<8, false>, 8);
     else
-        hipLaunchKernelGGL(rollout_bandit_kernel<16>, tiles<16>(a.N), dim3(1024), sm, st, M, P);
+        gl ? launch(rollout_bandit_kernel<16, true>, 16) : launch(rollout_bandit_kernel<16, false>, 16);
     return check_hip(hipGetLastError(), "rollout_bandit_kernel launch");
 }
 
