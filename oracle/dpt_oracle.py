@@ -282,7 +282,7 @@ def darkroom_online_rollout(W, goals, Heps, H, horizon, u, sample=True, perm=Non
     cn = np.zeros((N, R, horizon, 2))
     cr = np.zeros((N, R, horizon, 1))
     rets = np.zeros((N, Heps), np.int64)
-    logs = []
+    logs, acts = [], []
     for ep in range(Heps):
         nctx = min(ep, R)
         if ep < R:
@@ -297,6 +297,7 @@ def darkroom_online_rollout(W, goals, Heps, H, horizon, u, sample=True, perm=Non
             a = select_actions(lg, u[ep, t] if sample else None, sample,
                                temp=1.0 if sample else None)
             ns, r = darkroom_transit(s, a, goals, dim, perm)
+            acts.append(a)
             es.append(s.copy())
             ea.append(np.eye(5)[a])
             en.append(ns.copy())
@@ -312,7 +313,7 @@ def darkroom_online_rollout(W, goals, Heps, H, horizon, u, sample=True, perm=Non
             for buf, v in zip((cs, ca, cn, cr), new):
                 buf[:, :-1] = buf[:, 1:].copy()
                 buf[:, -1] = v
-    return dict(returns=rets, logits=np.stack(logs))
+    return dict(returns=rets, logits=np.stack(logs), actions=np.stack(acts, 1))
 
 
 def regret_curves(opt, lnr):

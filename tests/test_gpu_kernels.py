@@ -396,3 +396,76 @@ def test_rollout_bernoulli_philox_vs_oracle():
         assert np.array_equal(out["actions"].cpu().numpy(), ref["actions"])
         assert np.array_equal(out["rewards"].cpu().numpy(), ref["rewards"])
         assert set(np.unique(out["rewards"].cpu().numpy())) <= {0.0, 1.0}
+
+
+@pytest.mark.parametrize("A,H,var", [(5, 500, 0.3), (20, 1000, 0.3)])
+def test_rollout_full_config_sampled_tasks(A, H, var):
+    """BASELINE configs 2 (5 arms, H=500) and 4 (20 arms, H=1000; one GPU's 4096-task shard) at full
+    size: the fused rollout over 4096 tasks agrees, on sampled tasks spread over the tiles, with the C
+    oracle fed the same Philox draws -- logits within 1e-5 at every step and actions / arm values
+    exactly, each task up to its first near-tie draw (a uniform within 1e-5 of a cdf edge)."""
+    import bench
+    import dpt_hip
+    from oracle import c_oracle
+    dh()
+    N, seed, L = 4096, 31337, 4
+    sd, _ = bench.synthetic_state_dict(L, 1, A, H)
+    m = dpt_hip.DeviceModel(sd, L, 1, A, 4 * (1 + H))
+    if A == 5:
+        means = np.random.RandomState(1).uniform(0, 1, (N, A))
+    else:  # collect_data.py:230-231 arms, theta ~ N(0,1)/sqrt(d)
+        arms = np.random.RandomState(1234).normal(size=(A, 2)) / np.sqrt(2)
+        means = np.random.RandomState(2).normal(0, 1, (N, 2)) / np.sqrt(2) @ arms.T
+    out = m.rollout_bandit(means, H, var, True, seed=seed, want_logits=True)
+    acts = out["actions"].cpu().numpy()
+    av = out["arm_value"].cpu().numpy()
+    assert np.array_equal(av, means[np.arange(N)[:, None], acts])
+    tasks = np.array([0, 7, 8, 2049, 4095])
+    u = np.stack([philox_np.uniform(seed, h, tasks, dpt_hip.STREAM_SELECT) for h in range(H)])
+    g = np.stack([philox_np.normal(seed, h, tasks, dpt_hip.STREAM_REWARD) for h in range(H)])
+    blob = dpt_hip.pack_weights(sd, L).numpy()
+    ref = c_oracle.bandit_rollout(blob, L, A, 4 * (1 + H), means[tasks], H, var, u, g, True, False, 4,
+                                  want_logits=True)
+    lg = out["logits"].cpu().numpy()[:, tasks]
+    margin = O.boundary_margin(O.softmax_f32(ref["logits"], 1.0), u)  # (H, n)
+    for j, t in enumerate(tasks):
+        tie = np.nonzero(margin[:, j] < 1e-5)[0]
+        k = int(tie[0]) if tie.size else H - 1  # steps 0..k agree; a near-tie may flip step k's action
+        assert_logits(lg[:k + 1, j], ref["logits"][:k + 1, j])
+        n = k if tie.size else H
+        assert np.array_equal(acts[t, :n], ref["actions"][j, :n]), t
+        assert np.array_equal(av[t, :n], ref["arm_value"][j, :n]), t
+
+
+def test_rollout_darkroom_full_config3_sampled_tasks():
+    """BASELINE config 3 at full size (4096 tasks, Heps=40, horizon=100, goals in collect_data.py's
+    shuffled order, logits memo on): sampled tasks agree with the float64 numpy oracle fed the same
+    Philox draws -- logits within 1e-5, actions and per-episode returns exactly, each task up to its
+    first near-tie draw."""
+    import bench
+    import dpt_hip
+    d = dh()
+    N, Heps, horizon, seed, ctr, L = 4096, 40, 100, 99, 3, 4
+    sd, _ = bench.synthetic_state_dict(L, 2, 5, horizon)
+    m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + horizon))
+    goals = np.array([(j, i) for j in range(10) for i in range(10)])
+    np.random.RandomState(0).shuffle(goals)
+    goals = goals[np.arange(N) % 100]
+    out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, counter=ctr, want_actions=True, want_logits=True)
+    tasks = np.array([0, 1337, 4095])
+    steps = Heps * horizon
+    u = np.stack([philox_np.uniform(seed, ctr + k, tasks, d.STREAM_SELECT) for k in range(steps)])
+    W = O.split_weights({k: v.numpy() for k, v in sd.items()}, L)
+    ref = O.darkroom_online_rollout(W, goals[tasks], Heps, horizon, horizon, u.reshape(Heps, horizon, -1), True)
+    lg = out["logits"].cpu().numpy()[:, tasks]
+    acts = out["actions"].cpu().numpy()[tasks]
+    rets = out["returns"].cpu().numpy()[tasks]
+    margin = O.boundary_margin(O.softmax_f32(ref["logits"], 1.0), u)  # (steps, n)
+    for j in range(len(tasks)):
+        tie = np.nonzero(margin[:, j] < 1e-5)[0]
+        k = int(tie[0]) if tie.size else steps - 1
+        assert_logits(lg[:k + 1, j], ref["logits"][:k + 1, j])
+        n = k if tie.size else steps
+        assert np.array_equal(acts[j, :n], ref["actions"][j, :n])
+        full_eps = (k // horizon) if tie.size else Heps
+        assert np.array_equal(rets[j, :full_eps], ref["returns"][j, :full_eps])
