@@ -68,8 +68,8 @@ using namespace dpt;
 struct dpt_model {
     dpt_model_desc desc;
     float* blob;
-    float* frag;  // the blocks' weights in MFMA fragment order (dpt_darkroom.hip FragOff)
-    float* l0;    // block 0 folded for the K/V-free bandit rollout (dpt_decode.hip L0Off)
+    float* frag;  // the blocks' weights in MFMA fragment order, attention folded (dpt_mfma_fwd.h FragOff)
+    float* l0;    // every block's attention folded (dpt_common.h L0Off)
     ModelView view;
 };
 
@@ -165,8 +165,9 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
         set_error(DPT_ENOMEM, "hipMalloc(%zu + %zu) for the derived weights failed", frag_bytes, l0_bytes);
         return DPT_ENOMEM;
     }
-    rc = launch_pack_fragments(view, frag, nullptr);
-    if (!rc) rc = launch_derive_l0(view, l0, nullptr);
+    rc = launch_derive_l0(view, l0, nullptr);
+    view.l0 = l0;  // the fragments pack the folded attention (dpt_mfma_fwd.h FragOff)
+    if (!rc) rc = launch_pack_fragments(view, frag, nullptr);
     if (!rc) rc = check_hip(hipDeviceSynchronize(), "weight derivation");
     if (rc) {
         (void)hipFree(blob);
@@ -174,7 +175,6 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
         (void)hipFree(l0);
         return rc;
     }
-    view.l0 = l0;
     dpt_model* m = new dpt_model;
     m->desc = *d;
     m->blob = blob;
@@ -189,7 +189,7 @@ int dpt_model_free(dpt_model* m) {
     if (!m) return DPT_OK;
     int rc = check_hip(hipFree(m->blob), "hipFree weight blob");
     int rc2 = check_hip(hipFree(m->frag), "hipFree fragment weights");
-    const int rc3 = check_hip(hipFree(m->l0), "hipFree derived block-0 weights");
+    const int rc3 = check_hip(hipFree(m->l0), "hipFree folded attention weights");
     if (!rc2) rc2 = rc3;
     delete m;
     if (!rc) rc = rc2;

@@ -54,8 +54,8 @@ struct ModelView {
     const float* lnf_b;
     const float* head_w;  // [E][A]
     const float* head_b;  // [A]
-    // block 0's attention folded into the K/V-free form the bandit rollout uses
-    // (dpt_decode.hip L0Off): G = Wq Wk^T, g0 = Wk bq, Wvp = Wv Wproj, bvp = bv Wproj + bproj
+    // every block's attention folded (L0Off, one block per layer): G = Wq Wk^T,
+    // g0 = Wk bq, Wvp = Wv Wproj, bvp = bv Wproj + bproj
     const float* l0;
     int n_layer, sd, A, F, n_positions;
 };
@@ -194,6 +194,20 @@ __device__ inline int select_fixed(const float (&lg)[NA], int sample, float temp
     }
     return idx < NA ? idx : NA - 1;
 }
+
+// Every block's attention folded (ModelView::l0, one L0Off block per layer,
+// derived at model creation by derive_l0_kernel): with y = LN1(h), q.k_s =
+// y_s . u + (terms constant over the keys s) for u = Wk q = y G + g0, and
+// sum_s P_s v_s = (sum_s P_s y_s) Wv + bv.  Used by the bandit rollout
+// (dpt_decode.hip) and the MFMA window forwards (dpt_mfma_fwd.h).  All
+// matrices [in][out], E x E.
+struct L0Off {
+    static constexpr int G = 0;                 // Wq Wk^T: u = xn G + g0 = Wk q
+    static constexpr int g0 = G + kE * kE;      // Wk bq
+    static constexpr int Wvp = g0 + kE;         // Wv Wproj
+    static constexpr int bvp = Wvp + kE * kE;   // bv Wproj + bproj
+    static constexpr int size = bvp + kE;
+};
 
 // ----------------------------------------------------------------------------- env arithmetic
 // envs/bandit_env.py:59: means[a] + np.random.normal(0, var) == means[a] + (0.0 + var*g).

@@ -58,18 +58,27 @@ constexpr int kMemoStates = 128;            // logits memo rows (grids up to 11 
 // A-operand fragment of W^T for a k=32 input (W is [in][out], Conv1D layout):
 // lane l, k-step s reads W[16*(s>>2) + 4*(l>>4) + (s&3)][ob*16 + (l&15)];
 // mlp.c_proj ([128][32]): chunk j, step s reads hidden 16j + 4*(l>>4) + s.
+// The attention is folded (FragOff): the attn region packs G ([E][E], tiles 0-1;
+// tiles 2-5 are zero) and the proj region Wvp, both from ModelView::l0.
 __global__ void pack_fragments_kernel(ModelView M, float* __restrict__ frag) {
     const int total = M.n_layer * FragOff::size;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
         const int layer = i / FragOff::size;
         int o = i % FragOff::size;
         const float* W = M.layers + (size_t)layer * LayerOff::size;
+        const float* F = M.l0 + (size_t)layer * L0Off::size;
         const float* src;
         int n_out, in, out;
         if (o < FragOff::mp) {
             int base;
-            if (o < FragOff::proj) { base = FragOff::attn; src = W + LayerOff::attn_w; n_out = 3 * kE; }
-            else if (o < FragOff::fc) { base = FragOff::proj; src = W + LayerOff::proj_w; n_out = kE; }
+            if (o < FragOff::proj) {
+                if (o >= FragOff::attn + 2 * 512) {  // tiles 2-5: unused in the folded form
+                    frag[i] = 0.f;
+                    continue;
+                }
+                base = FragOff::attn; src = F + L0Off::G; n_out = kE;
+            }
+            else if (o < FragOff::fc) { base = FragOff::proj; src = F + L0Off::Wvp; n_out = kE; }
             else { base = FragOff::fc; src = W + LayerOff::fc_w; n_out = kFF; }
             o -= base;
             const int s4 = o & 3, lane = (o >> 2) & 63, q = (o >> 8) & 1, ob = o >> 9;
@@ -221,7 +230,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             for (int j = 0; j < 2; ++j)
                 if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
             DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                           c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 6)));
+                           c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 2), kv_from_y<NB>(S.kv, qb, xn)));
             bar_lds();
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -293,8 +302,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     float xn[2][8];
                     DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
                                    c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 2)));
-                    if (wave == 0) {  // block 0 (slot 0 of wave 0): key/value of the query token
-                        c_attn_n<1>(S.kv, P, frag0, qb, xn, q, 2, 6);
+                    if (wave == 0) {  // block 0 (slot 0 of wave 0): key/value (= y) of the query token
+                        kv_from_y<1>(S.kv, qb, xn);
                         const int lane = lane_id();
                         if ((lane & 15) == 0) {
 #pragma unroll
@@ -353,11 +362,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     float xn[2][8];
                     if (!last) {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       c_attn_n<NB>(S.kv, W, fs, qb, xn, q, 0, 6)));
+                                       c_attn_n<NB>(S.kv, W, fs, qb, xn, q, 0, 2), kv_from_y<NB>(S.kv, qb, xn)));
                     } else {
                         // the last layer needs q only for token T-1 (block qlast)
-                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       c_attn_n<NB>(S.kv, W, fs, qb, xn, q, 2, 6)));
+                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(S.kv, qb, xn)));
 #pragma unroll
                         for (int j = 0; j < 2; ++j) {
                             if (j < nb && qb[j] == qlast) {

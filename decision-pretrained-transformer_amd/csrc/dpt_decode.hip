@@ -103,17 +103,6 @@ __host__ inline size_t decode_smem_bytes(const ModelView& M) {
     return sizeof(Smem) + sizeof(float) * (size_t)ParamLDS::make(M.F, M.n_layer, M.A).total;
 }
 
-// Every block folded for the K/V-free bandit rollout (ModelView::l0, one L0Off
-// block per layer, derived at model creation by derive_l0_kernel).  All
-// matrices [in][out], E x E.
-struct L0Off {
-    static constexpr int G = 0;                 // Wq Wk^T: u = xn G + g0 = Wk q
-    static constexpr int g0 = G + kE * kE;      // Wk bq
-    static constexpr int Wvp = g0 + kE;         // Wv Wproj
-    static constexpr int bvp = Wvp + kE * kE;   // bv Wproj + bproj
-    static constexpr int size = bvp + kE;
-};
-
 // LDS block of the rollout after ParamLDS (offsets in floats): the embedding of
 // every bandit token up to its reward term, base[k] = ((w_s + w_a=k) + w_s') + emb_b
 // for k < A and base[A] = w_s + emb_b (the query token), then g0 and bvp of

@@ -19,6 +19,9 @@ constexpr int kKStride = kE + 4;            // K[token][feature]
 constexpr int kVStride = kFwdT + 4;          // Vt[feature][token] (128-token buffer)
 
 // Fragment-packed weights of one block (floats), see pack_fragments_kernel.
+// The attention is folded (L0Off): the attn region's tiles 0-1 hold G (the u =
+// y G + g0 projection; tiles 2-5 are unused: keys and values are y itself) and
+// the proj region holds Wvp = Wv Wproj.
 struct FragOff {
     static constexpr int attn = 0;            // [6 ob][2 q][64 lanes][4]
     static constexpr int proj = attn + 3072;  // [2 ob][2 q][64][4]
@@ -241,8 +244,28 @@ __device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn
         }
 }
 
+// Folded attention input of the NB blocks qb[]: keys and values are the
+// LayerNorm output y itself (K <- y token-major, Vt <- y feature-major, the
+// C-layout of xn is the layout c_attn's K / V tiles had).
+template <int NB, class KV>
+__device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2][8]) {
+    const int lane = lane_id(), g = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int tok = qb[j] * 16 + (lane & 15);
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+            *reinterpret_cast<floatx4*>(&S.K[tok][16 * blk + 4 * g]) =
+                floatx4{xn[j][4 * blk], xn[j][4 * blk + 1], xn[j][4 * blk + 2], xn[j][4 * blk + 3]};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S.Vt[16 * blk + 4 * g + r][tok] = xn[j][4 * blk + r];
+        }
+    }
+}
+
 // c_attn output blocks [ob0, ob1) of (Q0 Q1 K0 K1 V0 V1) for the NB blocks qb[]:
-// Q stays in registers, K -> LDS token-major, V -> LDS feature-major.
+// Q stays in registers, K -> LDS token-major, V -> LDS feature-major.  With the
+// folded fragments only [0, 2) is used: "Q" is then u = y G + g0.
 template <int NB, class KV>
 __device__ inline void c_attn_n(KV& S, const float* W, const FragSrc& fs, const int (&qb)[2],
                                 const float (&xn)[2][8], float (&q)[2][8], int ob0, int ob1) {
@@ -337,7 +360,8 @@ __device__ inline int blocks_of_wave(int w, int nqb, int (&qb)[2]) {
     return 0;
 }
 
-// Copy the small per-layer parameters of n_layer blocks into LDS (layout PL).
+// Copy the small per-layer parameters of n_layer blocks into LDS (layout PL;
+// attention biases in the folded form: attn_b[0, E) = g0, proj_b = bvp).
 __device__ inline void load_layer_params(float* P, const ModelView& M, int tid, int nthreads) {
     for (int i = tid; i < M.n_layer * PL::size; i += nthreads) {
         const int l = i / PL::size, k = i % PL::size;
@@ -345,8 +369,9 @@ __device__ inline void load_layer_params(float* P, const ModelView& M, int tid, 
         float v;
         if (k < PL::ln1_b) v = Wg[LayerOff::ln1_g + k];
         else if (k < PL::attn_b) v = Wg[LayerOff::ln1_b + k - PL::ln1_b];
-        else if (k < PL::proj_b) v = Wg[LayerOff::attn_b + k - PL::attn_b];
-        else if (k < PL::ln2_g) v = Wg[LayerOff::proj_b + k - PL::proj_b];
+        else if (k < PL::attn_b + kE) v = M.l0[(size_t)l * L0Off::size + L0Off::g0 + k - PL::attn_b];  // folded
+        else if (k < PL::proj_b) v = 0.f;                                                            // unused
+        else if (k < PL::ln2_g) v = M.l0[(size_t)l * L0Off::size + L0Off::bvp + k - PL::proj_b];     // folded
         else if (k < PL::ln2_b) v = Wg[LayerOff::ln2_g + k - PL::ln2_g];
         else if (k < PL::fc_b) v = Wg[LayerOff::ln2_b + k - PL::ln2_b];
         else if (k < PL::mp_b) v = Wg[LayerOff::fc_b + k - PL::fc_b];

@@ -113,7 +113,8 @@ prefill_kernel(ModelView M, PrefillArgs a) {
         float q[2][8];
         {
             float xn[2][8];
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), c_attn_n<NB>(S, W, fs, qb, xn, q, 0, 6)));
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), c_attn_n<NB>(S, W, fs, qb, xn, q, 0, 2),
+                            kv_from_y<NB>(S, qb, xn)));
         }
         bar_lds();
         if (nb > 0) {
