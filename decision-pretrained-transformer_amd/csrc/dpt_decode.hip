@@ -187,15 +187,17 @@ __device__ inline float ln_halfwave(float v, float g, float b) {
     const float d = v - mean;
     float s2 = dpp_sum16(d * d);
     s2 += __shfl_xor(s2, 16, 32);
-    const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
+    const float rstd = __builtin_amdgcn_rsqf(s2 * (1.0f / kE) + 1e-5f);
     return fmaf(d * rstd, g, b);
 }
 
 __device__ inline float gelu_new(float x) {
-    // 0.5*x*(1 + tanh(sqrt(2/pi)*(x + 0.044715*x^3)))  (transformers/activations.py:65)
-    const float k0 = 0.7978845608028654f;
-    float inner = k0 * (x + 0.044715f * (x * x * x));
-    return 0.5f * x * (1.0f + tanhf(inner));
+    // 0.5*x*(1 + tanh(z)), z = sqrt(2/pi)*(x + 0.044715*x^3) (transformers/activations.py:65),
+    // evaluated as x * sigmoid(2z) = x / (1 + 2^(-2z log2 e)) with v_exp_f32 / v_rcp_f32
+    const float c1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+    const float c2 = c1 * 0.044715f;
+    const float e = __builtin_amdgcn_exp2f(x * fmaf(x * x, c2, c1));
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 // Flash-decoding attention of one task (one wave): positions 0..pos-1 from the
@@ -585,7 +587,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 const float d0 = x0 - mean, d1 = x1 - mean;
                 float s2 = d0 * d0 + d1 * d1;
                 s2 = dpp_sum16(s2);
-                const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
+                const float rstd = __builtin_amdgcn_rsqf(s2 * (1.0f / kE) + 1e-5f);
                 if (t < TILE) {
                     S.x[t][c0] = x0;
                     S.x[t][c1] = x1;
