@@ -133,11 +133,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # one rank per GPU; DPT_BENCH_BACKEND=gloo (ranks may then share a GPU) rehearses the
+    # multi-rank path on a one-GPU box -- the measured runs use RCCL ("nccl")
+    backend = os.environ.get("DPT_BENCH_BACKEND", "nccl")
+    dev = local % torch.cuda.device_count() if backend == "gloo" else local
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     import dpt_hip
     from dpt_hip.distributed import gather_rows, shard
 
@@ -180,7 +187,7 @@ def main():
         np.random.RandomState(0).shuffle(goals)   # collect_data.py:408-409 order, cycled to N
         goals_all = goals[np.arange(n_total) % 100]
         envs = [DarkroomEnv(10, g, H) for g in goals_all[first:first + count]]
-        vec = DarkroomEnvVec(envs)
+        vec = DarkroomEnvVec(envs, first_task=first)
 
         def one(step_idx):
             np.random.seed(step_idx)
@@ -213,7 +220,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 

@@ -25,10 +25,11 @@ def gather_rows(local, n_total, group=None):
     pad = torch.zeros((width,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
     out = torch.empty((world * width,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    if dist.get_backend(group) == "gloo":
-        parts = list(out.chunk(world))
-        dist.all_gather(parts, pad, group=group)
-        out = torch.cat(parts)
+    if dist.get_backend(group) == "gloo":  # CPU tests / one-GPU rehearsal: gather on the host
+        host = pad.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        out = torch.cat(parts).to(local.device)
     else:
         dist.all_gather_into_tensor(out, pad, group=group)
     return torch.cat([out[r * width: r * width + counts[r]] for r in range(world)])

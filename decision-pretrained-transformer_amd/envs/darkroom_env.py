@@ -87,11 +87,14 @@ class DarkroomEnvPermuted(DarkroomEnv):
 class DarkroomEnvVec(BaseEnv):
     """Vectorized DarkRoom (envs/darkroom_env.py:114-175); goals / permutations live on the device."""
 
-    def __init__(self, envs):
+    def __init__(self, envs, first_task=0):
         self._envs = envs
         self._num_envs = len(envs)
         self._goals_d = None
         self._perms_d = None
+        # global id of envs[0] when the tasks are sharded over ranks: the fused rollout
+        # keys its Philox draws by global task id (dpt_hip.distributed)
+        self.first_task = int(first_task)
 
     @property
     def goals_device(self):

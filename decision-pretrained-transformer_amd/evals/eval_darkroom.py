@@ -72,8 +72,8 @@ def rollout_fused(vec_env, controller, Heps, H, horizon, want_actions=False, wan
                          for k in range(steps)])
     return dm.rollout_darkroom(vec_env.goals_device, Heps, horizon, H // horizon, dim=vec_env.dim,
                                perms=vec_env.perms_device, sample=controller.sample, temp=controller.temp,
-                               seed=seed, counter=ctr0, uniforms=u, want_actions=want_actions,
-                               want_logits=want_logits, want_forwards=want_forwards)
+                               seed=seed, counter=ctr0, first_task=getattr(vec_env, "first_task", 0), uniforms=u,
+                               want_actions=want_actions, want_logits=want_logits, want_forwards=want_forwards)
 
 
 def deploy_online_vec(vec_env, controller, Heps, H, horizon, fused=True):
