@@ -205,9 +205,9 @@ __device__ inline float gelu_new(float x) {
 // KV_SAME (the rollout's blocks >= 1): keys and values are one stream (the
 // LayerNorm outputs y_p, see attend_l0 for the algebra), read once.
 template <bool KV_SAME = false, int NR = kRows>
-__device__ inline void attend_one(const float* __restrict__ kc, const float* __restrict__ vc, int pos,
-                                  const float* q, const float* kcur, const float* vcur, float* o,
-                                  int lane) {
+__device__ inline float4 attend_one(const float* __restrict__ kc, const float* __restrict__ vc, int pos,
+                                    const float* q, const float* kcur, const float* vcur, float* o,
+                                    int lane) {
     const int g = lane >> 3, c = lane & 7;
     const float scale = 0.17677669529663687f * 1.4426950408889634f;  // 32 ** -0.5 * log2(e): exp2 domain
     const float4 q4 = *reinterpret_cast<const float4*>(q + 4 * c);
@@ -300,13 +300,11 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
         acc.w = acc.w * sa + aw * sb;
         m = mn;
     }
-    if (lane < 8) {
-        const float inv = 1.0f / l;
-        o[4 * c + 0] = acc.x * inv;
-        o[4 * c + 1] = acc.y * inv;
-        o[4 * c + 2] = acc.z * inv;
-        o[4 * c + 3] = acc.w * inv;
-    }
+    // every lane holds dims 4c..4c+3 of the result after the butterfly
+    const float inv = 1.0f / l;
+    const float4 res = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    if (o && lane < 8) *reinterpret_cast<float4*>(o + 4 * c) = res;
+    return res;
 }
 
 // Block-0 attention of one bandit task (one wave) without a K/V cache.  Every
@@ -320,7 +318,7 @@ __device__ inline void attend_one(const float* __restrict__ kc, const float* __r
 // folded into c_proj (L0Off::Wvp, bvp).  Writes o = sum_p P_p y_p.  The current
 // position's x is xcur (the residual row, before attention).  A record is
 // (a_p * E as int bits, r_p); scores are kept in the log2 domain (v_exp_f32).
-__device__ inline void attend_l0(const float2* __restrict__ tok, const float* __restrict__ wpe, int pos,
+__device__ inline float4 attend_l0(const float2* __restrict__ tok, const float* __restrict__ wpe, int pos,
                                  const float* u, const float* xcur, const float* baseT, const float* wr,
                                  const float* lng, const float* lnb, float* o, int lane) {
     const int g = lane >> 3, c = lane & 7;
@@ -420,13 +418,60 @@ __device__ inline void attend_l0(const float2* __restrict__ tok, const float* __
         acc.w = acc.w * sa + aw * sb;
         m = mn;
     }
-    if (lane < 8) {  // sum_p P_p y_p = g * (sum_p P_p rstd_p d_p) + b   (sum_p P_p = 1)
-        const float inv = 1.0f / l;
-        const float4 b4 = *reinterpret_cast<const float4*>(lnb + 4 * c);
-        o[4 * c + 0] = fmaf(g4.x, acc.x * inv, b4.x);
-        o[4 * c + 1] = fmaf(g4.y, acc.y * inv, b4.y);
-        o[4 * c + 2] = fmaf(g4.z, acc.z * inv, b4.z);
-        o[4 * c + 3] = fmaf(g4.w, acc.w * inv, b4.w);
+    // sum_p P_p y_p = g * (sum_p P_p rstd_p d_p) + b   (sum_p P_p = 1); every lane holds dims 4c..4c+3
+    const float inv = 1.0f / l;
+    const float4 b4 = *reinterpret_cast<const float4*>(lnb + 4 * c);
+    const float4 res = make_float4(fmaf(g4.x, acc.x * inv, b4.x), fmaf(g4.y, acc.y * inv, b4.y),
+                                   fmaf(g4.z, acc.z * inv, b4.z), fmaf(g4.w, acc.w * inv, b4.w));
+    if (o && lane < 8) *reinterpret_cast<float4*>(o + 4 * c) = res;
+    return res;
+}
+
+// The rollout's c_proj + residual + ln_2 for one task inside its attention wave (no
+// extra phase or barrier): lane (c = l & 7, g = l >> 3) holds attention dims
+// o4 = o[4c..4c+3] and forms the partial outputs j = 4g..4g+3 over them from the
+// folded Wvp ([k][j], LDS); an 8-lane DPP sum over c completes them.  Then
+// x += out + bvp and LayerNorm ln_2 over the 32 j (groups g combined by xor 8 / 16
+// / 32); lane c == 0 of each group writes x[4g..] and xn[4g..].
+__device__ inline void proj_ln_task(float4 o4, const float* Wvp, const float* bvp, const float* lng,
+                                    const float* lnb, float* xrow, float* xnrow, int lane) {
+    const int c = lane & 7, g = lane >> 3;
+    const float ov[4] = {o4.x, o4.y, o4.z, o4.w};
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float4 w = *reinterpret_cast<const float4*>(Wvp + (4 * c + i) * kE + 4 * g);
+        acc.x = fmaf(ov[i], w.x, acc.x);
+        acc.y = fmaf(ov[i], w.y, acc.y);
+        acc.z = fmaf(ov[i], w.z, acc.z);
+        acc.w = fmaf(ov[i], w.w, acc.w);
+    }
+    acc.x = dpp_sum8(acc.x);
+    acc.y = dpp_sum8(acc.y);
+    acc.z = dpp_sum8(acc.z);
+    acc.w = dpp_sum8(acc.w);
+    const float4 bv = *reinterpret_cast<const float4*>(bvp + 4 * g);
+    const float4 xv = *reinterpret_cast<const float4*>(xrow + 4 * g);
+    const float x0 = (acc.x + bv.x) + xv.x, x1 = (acc.y + bv.y) + xv.y;
+    const float x2 = (acc.z + bv.z) + xv.z, x3 = (acc.w + bv.w) + xv.w;
+    auto sum_groups = [](float v) {  // over the 8 groups g: lanes l ^ 8, l ^ 16, l ^ 32
+        v += dpp_xor8(v);
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        return v;
+    };
+    const float mean = sum_groups((x0 + x1) + (x2 + x3)) * (1.0f / kE);
+    const float d0 = x0 - mean, d1 = x1 - mean, d2 = x2 - mean, d3 = x3 - mean;
+    const float var = sum_groups((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3)) * (1.0f / kE);
+    const float rstd = __builtin_amdgcn_rsqf(var + 1e-5f);
+    if (c == 0) {
+        const float4 gv = *reinterpret_cast<const float4*>(lng + 4 * g);
+        const float4 bb = *reinterpret_cast<const float4*>(lnb + 4 * g);
+        *reinterpret_cast<float4*>(xrow + 4 * g) = make_float4(x0, x1, x2, x3);
+        // xn rows are padded to kLdE floats: 8-B aligned stores
+        *reinterpret_cast<float2*>(xnrow + 4 * g) = make_float2(fmaf(d0 * rstd, gv.x, bb.x), fmaf(d1 * rstd, gv.y, bb.y));
+        *reinterpret_cast<float2*>(xnrow + 4 * g + 2) =
+            make_float2(fmaf(d2 * rstd, gv.z, bb.z), fmaf(d3 * rstd, gv.w, bb.w));
     }
 }
 
@@ -545,20 +590,28 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
             if (task < N) {
                 const float* kc = kv + li * lstride + (size_t)task * max_pos * kE;
                 const float* vc = kv + vhalf + li * lstride + (size_t)task * max_pos * kE;
-                if (l0)
-                    attend_l0(reinterpret_cast<const float2*>(kc), M.wpe, pos, S.q[wave], S.x[wave],
-                              D + RolloutLDS::make(M.A, M.n_layer).base, P + pl.emb_w + (2 + M.A) * kE,
-                              PL + PLay::ln1_g, PL + PLay::ln1_b, S.o[wave], lane);
-                else if (L0R)  // scores y_p . u, output sum_p P_p y_p; y_pos is in S.kcur
-                    attend_one<true, kYRows>(kc, kc, pos, S.q[wave], S.kcur[wave], S.kcur[wave], S.o[wave], lane);
-                else
+                if (L0R) {
+                    const RolloutLDS rl = RolloutLDS::make(M.A, M.n_layer);
+                    const float4 o4 =
+                        l0 ? attend_l0(reinterpret_cast<const float2*>(kc), M.wpe, pos, S.q[wave], S.x[wave],
+                                       D + rl.base, P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
+                                       PL + PLay::ln1_b, nullptr, lane)
+                           // scores y_p . u, output sum_p P_p y_p; y_pos is in S.kcur
+                           : attend_one<true, kYRows>(kc, kc, pos, S.q[wave], S.kcur[wave], S.kcur[wave], nullptr,
+                                                      lane);
+                    // c_proj (folded Wvp) + residual + ln_2 of this task, in this wave
+                    proj_ln_task(o4, D + rl.wvp + li * kE * kE, D + rl.bvp + li * kE, PL + PLay::ln2_g,
+                                 PL + PLay::ln2_b, S.x[wave], S.xn[wave], lane);
+                } else {
                     attend_one(kc, vc, pos, S.q[wave], S.kcur[wave], S.vcur[wave], S.o[wave], lane);
+                }
             }
         }
         bar_lds();
         DPT_STAMP(2);
         // c_proj + residual + ln_2, one wave: both 16-column tiles, rows reduced over 16 lanes
-        if (wave == kProjWave) {
+        // (the rollout did this per task in the attention phase)
+        if (!L0R && wave == kProjWave) {
             const float* B = L0R ? D + RolloutLDS::make(M.A, M.n_layer).wvp + li * kE * kE : W + LayerOff::proj_w;
             float w0[8], w1[8];
 #pragma unroll
@@ -596,7 +649,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 }
             }
         }
-        bar_lds();
+        if (!L0R) bar_lds();
         DPT_STAMP(3);
         // c_fc (computed transposed: hidden units on the MFMA rows) -> gelu_new -> mlp.c_proj
         // partial over this wave's 16 hidden units; the accumulator is the A operand
