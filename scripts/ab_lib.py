@@ -20,6 +20,21 @@ def child(lib):
     import dpt_hip
     H, N, A = (int(os.environ.get(k, d)) for k, d in (("AB_H", "500"), ("AB_N", "4096"), ("AB_A", "5")))
     dpt_hip.set_decode_tile(int(os.environ.get("AB_TILE", "8")))
+    if os.environ.get("AB_WL") == "darkroom":  # config 3: 4096 tasks x 40 episodes x 100 steps
+        sd, _ = bench.synthetic_state_dict(4, 2, 5, 100)
+        m = dpt_hip.DeviceModel(sd, 4, 2, 5, 404)
+        goals = np.stack(np.unravel_index(np.arange(N) % 100, (10, 10)), 1)
+        ts = []
+        for rnd in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            out = m.rollout_darkroom(goals, 40, 100, 1, seed=rnd)
+            b.record()
+            torch.cuda.synchronize()
+            if rnd > 0:
+                ts.append(a.elapsed_time(b))
+        print(json.dumps({"lib": lib, "ms": ts, "checksum": float(out["returns"].sum())}))
+        return
     sd, _ = bench.synthetic_state_dict(4, 1, A, H)
     m = dpt_hip.DeviceModel(sd, 4, 1, A, 4 * (1 + H))
     means = torch.from_numpy(np.random.RandomState(1).uniform(0, 1, (N, A))).cuda()

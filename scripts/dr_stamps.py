@@ -23,6 +23,7 @@ import dpt_hip  # noqa: E402
 L = 4
 sd, _ = bench.synthetic_state_dict(L, 2, 5, 100)
 m = dpt_hip.DeviceModel(sd, L, 2, 5, 404)
+dpt_hip.set_darkroom_memo(bool(int(os.environ.get("DR_MEMO", "0"))))  # per-forward costs: memo off
 Heps = 11  # episode 0 (window 1) is 1/11 of the steps
 names = ["L0:embed+query k/v", "L0:merge+c_proj+mlp (wave 0 view)"]
 for layer in range(1, L - 1):
