@@ -124,6 +124,8 @@ class DeviceModel:
             cs_ = ca_ = cn_ = cr_ = None
         out = torch.empty((N, self.action_dim) if out_mode == 0 else (N, C, self.action_dim),
                           dtype=torch.float32, device=dev)
+        if N == 0 or (out_mode == 1 and C == 0):  # empty batch / no context rows: nothing to run
+            return out
         ws = (None if C + 1 <= self.prefill_max_window()
               else torch.empty(self.kv_numel(N, C + 1), dtype=torch.float32, device=dev))
         _lib.call("dpt_forward_window", self._h, _p(q), _p(cs_), _p(ca_), _p(cn_), _p(cr_), N, C,
@@ -155,11 +157,13 @@ class DeviceModel:
         means_d = _dev(means, torch.float64, dev)
         N, A = means_d.shape
         H = int(H)
-        kv = torch.empty(self.kv_numel(N, H), dtype=torch.float32, device=dev)
         out = dict(actions=torch.empty((N, H), dtype=torch.int32, device=dev),
                    rewards=torch.empty((N, H), dtype=torch.float64, device=dev),
                    arm_value=torch.empty((N, H), dtype=torch.float64, device=dev))
         out["logits"] = (torch.empty((H, N, A), dtype=torch.float32, device=dev) if want_logits else None)
+        if N == 0 or H == 0:  # no tasks or no steps: empty curves, nothing to run
+            return out
+        kv = torch.empty(self.kv_numel(N, H), dtype=torch.float32, device=dev)
         u_d = None if uniforms is None else _dev(uniforms, torch.float64, dev)
         g_d = None if noise is None else _dev(noise, torch.float64, dev)
         args = _lib.BanditRolloutArgs(
@@ -192,6 +196,11 @@ class DeviceModel:
         out["actions"] = torch.empty((N, steps), dtype=torch.int32, device=dev) if want_actions else None
         out["logits"] = torch.empty((steps, N, 5), dtype=torch.float32, device=dev) if want_logits else None
         out["forwards"] = torch.empty((N, int(Heps)), dtype=torch.int32, device=dev) if want_forwards else None
+        if N == 0 or steps == 0:  # no tasks or no steps: empty returns, nothing to run
+            for k in ("returns", "forwards"):
+                if out[k] is not None:
+                    out[k].zero_()
+            return out
         args = _lib.DarkroomRolloutArgs(
             N, int(Heps), int(horizon), int(ctx_episodes), int(dim), int(bool(sample)), int(first_task),
             int(seed) & (2 ** 64 - 1), int(counter), float(temp), 0, _p(goals_d).value,

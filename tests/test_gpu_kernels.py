@@ -469,3 +469,16 @@ def test_rollout_darkroom_full_config3_sampled_tasks():
         assert np.array_equal(acts[j, :n], ref["actions"][j, :n])
         full_eps = (k // horizon) if tie.size else Heps
         assert np.array_equal(rets[j, :full_eps], ref["returns"][j, :full_eps])
+
+
+def test_empty_batches():
+    """No tasks or no steps: empty outputs of the right shapes, no launch (the ABI rejects N=0)."""
+    _, m, _ = model_from_golden("bandit5")
+    o = m.rollout_bandit(np.zeros((0, 5)), 10, 0.3, True, want_logits=True)
+    assert o["actions"].shape == (0, 10) and o["logits"].shape == (10, 0, 5)
+    o = m.rollout_bandit(np.random.RandomState(0).uniform(0, 1, (4, 5)), 0, 0.3, True)
+    assert o["arm_value"].shape == (4, 0)
+    assert m.forward_window(np.zeros((0, 1), np.float32)).shape == (0, 5)
+    _, md, _ = model_from_golden("darkroom")
+    o = md.rollout_darkroom(np.zeros((0, 2), np.int64), 3, 10, 1, want_forwards=True)
+    assert o["returns"].shape == (0, 3) and o["forwards"].shape == (0, 3)
