@@ -254,8 +254,12 @@ def main():
                                  (Heps - 1) * window_flops(1 + H, L, F, 5, folded=False))
         flops = int(fw[0]) * window_flops(1, L, F, 5) + int(fw[1:].sum()) * window_flops(1 + H, L, F, 5)
         achieved = flops / (kern_ms * 1e-3) / 1e12
+        traffic = None  # HBM bytes read per launch (rocprofv3 FETCH_SIZE x2, scripts/profile_darkroom.sh)
+        pmc = os.path.join(ROOT, "profiles", "pmc_rollout_darkroom.json")
+        if os.path.exists(pmc) and count == 4096 and H == 100:
+            traffic = json.load(open(pmc)).get("hbm_fetch_bytes_corrected")
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": achieved / FP32_MFMA_PEAK_TF, "traffic": None,
+                "frac": achieved / FP32_MFMA_PEAK_TF, "traffic": traffic,
                 "kernel": "rollout_darkroom_kernel (one launch = one whole online eval)",
                 "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
                 "window_forwards_per_launch": int(fw.sum()),
