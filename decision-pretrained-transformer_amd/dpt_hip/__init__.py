@@ -352,9 +352,19 @@ def set_decode_tile(tile):
     _lib.call("dpt_tuning_set", _lib.TUNE_DECODE_TILE, int(tile))
 
 
+_darkroom_memo = True
+
+
 def set_darkroom_memo(on):
-    """DarkRoom rollout: one window forward per distinct query state per episode (default) or per step."""
+    """DarkRoom rollout: one window forward per distinct query state per episode (default) or per step.
+    Applies to the fused kernel and to the per-step device loop (evals/eval_darkroom.py)."""
+    global _darkroom_memo
     _lib.call("dpt_tuning_set", _lib.TUNE_DARKROOM_MEMO, int(bool(on)))
+    _darkroom_memo = bool(on)
+
+
+def darkroom_memo():
+    return _darkroom_memo
 
 
 def set_prefill(on):

@@ -27,7 +27,12 @@ def _device_ok(vec_env, controller):
 
 
 def _episode_device(dm, ctrl, vec_env, ctx, horizon):
-    """One DarkroomEnvVec.deploy_eval episode on device: returns (states, actions, next, rewards)."""
+    """One DarkroomEnvVec.deploy_eval episode on device: returns (states, actions, next, rewards).
+
+    The context is fixed for the episode, so a task's logits are a pure function of its
+    query state: with dpt_hip.darkroom_memo() (default) a step forwards only the tasks
+    whose current state is new in this episode and reuses the stored logits of the
+    others (each task's forward is independent, so the logits are bit-identical)."""
     dev = dpt_hip.device()
     N = vec_env.num_envs
     state = torch.zeros((N, 2), dtype=torch.int32, device=dev)   # DarkroomEnv.reset -> (0, 0)
@@ -35,8 +40,22 @@ def _episode_device(dm, ctrl, vec_env, ctx, horizon):
     ea = torch.empty((N, horizon), dtype=torch.int64, device=dev)
     er = torch.empty((N, horizon), dtype=torch.int32, device=dev)
     goals, perms, dim = vec_env.goals_device, vec_env.perms_device, vec_env.dim
+    memo = None
+    if dpt_hip.darkroom_memo():
+        memo = torch.empty((N, dim * dim, vec_env.action_dim), dtype=torch.float32, device=dev)
+        seen = torch.zeros((N, dim * dim), dtype=torch.bool, device=dev)
+        rows = torch.arange(N, device=dev)
     for t in range(horizon):
-        logits = dm.forward_window(state.float(), *ctx)
+        if memo is None:
+            logits = dm.forward_window(state.float(), *ctx)
+        else:
+            cell = state[:, 0].long() * dim + state[:, 1].long()
+            need = (~seen[rows, cell]).nonzero().squeeze(1)
+            if need.numel():
+                lg = dm.forward_window(state.index_select(0, need).float(), *(c.index_select(0, need) for c in ctx))
+                memo[need, cell[need]] = lg
+                seen[need, cell[need]] = True
+            logits = memo[rows, cell]
         a = ctrl.select(logits)
         es[:, t] = state
         ea[:, t] = a

@@ -183,6 +183,30 @@ def test_eval_darkroom_device_loop_matches_reference(fused):
         assert np.array_equal(ret, r["returns"]), tag
 
 
+def test_eval_darkroom_per_step_memo_bit_identical():
+    """The per-step device loop (window 1 + 2*70 = 141 > 128 tokens, so not fused) forwards only
+    the tasks whose state is new in the episode; returns are identical with the memo off."""
+    import dpt_hip
+    from ctrls.ctrl_darkroom import DarkroomTransformerController
+    from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec
+    from evals import eval_darkroom
+    _, m = ref_model("darkroom")
+    rs = np.random.RandomState(8)
+    envs = [DarkroomEnv(10, rs.randint(0, 10, 2), 70) for _ in range(48)]
+    outs = []
+    try:
+        for memo in (False, True):
+            dpt_hip.set_darkroom_memo(memo)
+            np.random.seed(5)
+            ctrl = DarkroomTransformerController(m, batch_size=48, sample=True)
+            vec = DarkroomEnvVec(envs)
+            assert not eval_darkroom._fused_ok(vec, ctrl, 140)
+            outs.append(eval_darkroom.deploy_online_vec(vec, ctrl, 4, 140, 70))
+    finally:
+        dpt_hip.set_darkroom_memo(True)
+    assert np.array_equal(outs[0], outs[1])
+
+
 def test_rollin_kernels_match_oracle():
     import dpt_hip
     g = golden("rollin.npz")
