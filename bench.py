@@ -151,7 +151,6 @@ def main():
     N, L, wl = args.tasks, args.layers, args.workload
     n_total = N * world
     first, count = shard(n_total, world, rank)
-    extra = {}
     if wl in ("bandit", "linear"):
         A, H = (5, args.H or 500) if wl == "bandit" else (20, args.H or 1000)
         sd, _ = synthetic_state_dict(L, 1, A, H, seed=0)
