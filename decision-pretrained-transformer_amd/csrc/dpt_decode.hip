@@ -584,6 +584,9 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         }
         bar_lds();
         DPT_STAMP(1);
+        // the streaming phase yields issue slots to the other workgroup's latency-bound dense
+        // phases (s_setprio; -0.5 % at config 2, -1 % on the linear config)
+        if (L0R) __builtin_amdgcn_s_setprio(0);
         // causal self-attention, one wave per task
         if (wave < TILE) {
             const int task = tile0 + wave;
@@ -609,6 +612,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         }
         bar_lds();
         DPT_STAMP(2);
+        if (L0R) __builtin_amdgcn_s_setprio(2);
         // c_proj + residual + ln_2, one wave: both 16-column tiles, rows reduced over 16 lanes
         // (the rollout did this per task in the attention phase)
         if (!L0R && wave == kProjWave) {
