@@ -17,6 +17,11 @@
 //    coalesced), online softmax per lane-group of 8, combined across the 8
 //    groups by a 3-step butterfly; the new position's K/V come from LDS;
 //  * LayerNorm / gelu / residual: one half-wave per task in LDS.
+// The bandit rollout (decode_position<TILE, true>) runs every block on folded
+// attention weights (dpt_common.h L0Off): block 0 recomputes its inputs from
+// 8-B token records, blocks >= 1 cache y = LN1(h) (128 B per position) as both
+// key and value, the u = y G + g0 projection replaces c_attn, and c_proj +
+// ln_2 run per task inside the attention wave (proj_ln_task).
 // Small parameters (embedding, LayerNorm, biases, head) and the tile's bandit
 // means live in LDS for the whole launch.  Phases inside one position are
 // separated by LDS-only barriers (lgkmcnt + s_barrier: the K/V stores of the
