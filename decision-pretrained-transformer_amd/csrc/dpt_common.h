@@ -195,6 +195,40 @@ __device__ inline int select_fixed(const float (&lg)[NA], int sample, float temp
     return idx < NA ? idx : NA - 1;
 }
 
+// select_fixed split at its cdf: q[k] = c_k / total (the values select_fixed
+// compares with u), so a caller that meets the same logits again selects with
+// select_from_cdf alone -- bit-identical to select_fixed on those logits.
+template <int NA>
+__device__ inline void cdf_fixed(const float (&lg)[NA], float temp, double (&q)[NA]) {
+    float xk[NA], ek[NA];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        xk[k] = (temp == 1.0f) ? lg[k] : lg[k] / temp;
+        m = fmaxf(m, xk[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) ek[k] = expf(xk[k] - m);
+    const float s = np_pairwise_sum_f32([&](int k) { return ek[k]; }, NA);
+    double total = 0.0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) total += (double)(ek[k] / s);
+    double c = 0.0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        c += (double)(ek[k] / s);
+        q[k] = c / total;
+    }
+}
+
+template <int NA>
+__device__ inline int select_from_cdf(const double* q, double u) {
+    int idx = 0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) idx += (q[k] <= u) ? 1 : 0;
+    return idx < NA ? idx : NA - 1;
+}
+
 // Every block's attention folded (ModelView::l0, one L0Off block per layer,
 // derived at model creation by derive_l0_kernel): with y = LN1(h), q.k_s =
 // y_s . u + (terms constant over the keys s) for u = Wk q = y G + g0, and

@@ -129,6 +129,7 @@ struct DrSmem {
     float part_y[kFF / 16][kE];       // last layer: per-hidden-chunk MLP partials
     // per-episode logits memo, one row per grid state (dim * dim <= kMemoStates)
     float memo_lg[kMemoStates][kDrA];
+    double memo_q[kMemoStates][kDrA];  // and their selection cdf (cdf_fixed), so a hit selects by 5 compares
     int memo_ok[kMemoStates];
     int sx, sy, ret, nfwd;
 };
@@ -251,13 +252,15 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         // the policy's logits are a pure function of (window, query state) and the
         // window is fixed for the whole episode: a state queried before in this
         // episode reuses that forward's logits (bit-identical to re-running it)
-        auto finish_step = [&](const float (&lg)[kDrA], int t, int sx, int sy) {
+        // q: the selection cdf of lg (cdf_fixed) when sampling; select_from_cdf(q, u)
+        // equals select_fixed(lg, u) bit for bit
+        auto finish_step = [&](const float (&lg)[kDrA], const double* q, int t, int sx, int sy) {
             const int step = ep * p.horizon + t;
             double u = 0.0;
             if (p.sample)
                 u = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
                                : philox_uniform(p.seed, p.counter + step, p.first_task + task, DPT_STREAM_SELECT);
-            const int a = select_fixed<kDrA>(lg, p.sample, p.temp, u);
+            const int a = p.sample ? select_from_cdf<kDrA>(q, u) : select_fixed<kDrA>(lg, 0, p.temp, u);
             const int ea = p.perms ? p.perms[(size_t)task * kDrA + a] : a;
             int nx = sx + (ea == 0) - (ea == 1);
             int ny = sy + (ea == 2) - (ea == 3);
@@ -283,7 +286,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         float lg[kDrA];
 #pragma unroll
                         for (int k = 0; k < kDrA; ++k) lg[k] = S.memo_lg[sidx][k];
-                        finish_step(lg, t, S.sx, S.sy);
+                        finish_step(lg, S.memo_q[sidx], t, S.sx, S.sy);
                     }
                     bar_lds();
                     continue;
@@ -568,14 +571,19 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         lg[a] = sum_cols(part) + P[pt.head_b + a];
                     }
                     if (lane == 0) {
+                        double q[kDrA] = {0.0, 0.0, 0.0, 0.0, 0.0};
+                        if (p.sample) cdf_fixed<kDrA>(lg, p.temp, q);
                         if (p.memo) {
                             const int sidx = sx * p.dim + sy;
 #pragma unroll
-                            for (int k = 0; k < kDrA; ++k) S.memo_lg[sidx][k] = lg[k];
+                            for (int k = 0; k < kDrA; ++k) {
+                                S.memo_lg[sidx][k] = lg[k];
+                                S.memo_q[sidx][k] = q[k];
+                            }
                             S.memo_ok[sidx] = 1;
                         }
                         S.nfwd += 1;
-                        finish_step(lg, t, sx, sy);
+                        finish_step(lg, q, t, sx, sy);
                     }
                 }
             }
