@@ -114,7 +114,8 @@ struct PTop {
     }
 };
 
-struct DrSmem {
+// 16-B multiple: the dynamic parameter block P follows it and is read with 16-B loads
+struct alignas(16) DrSmem {
     KVLds kv;
     int2 ctx[kFwdT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
     int2 cur[kFwdT];   // this episode's transitions
@@ -131,7 +132,7 @@ struct DrSmem {
     float memo_lg[kMemoStates][kDrA];
     double memo_q[kMemoStates][kDrA];  // and their selection cdf (cdf_fixed), so a hit selects by 5 compares
     int memo_ok[kMemoStates];
-    int sx, sy, ret, nfwd;
+    int sx, sy, ret, nfwd, tnext;
 };
 
 __device__ inline int2 pack_tr(int x, int y, int a, int nx, int ny, int r) {
@@ -280,17 +281,25 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         };
         for (int t = 0; t < p.horizon; ++t) {
             if (p.memo) {
-                const int sidx = S.sx * p.dim + S.sy;  // same value in every lane (LDS, after a barrier)
-                if (S.memo_ok[sidx]) {
-                    if (tid == 0) {
+                // thread 0 runs consecutive steps whose state was already queried this
+                // episode (a memo hit needs no forward); the other threads wait at one
+                // barrier for the first state that needs one
+                if (tid == 0) {
+                    int tt = t;
+                    while (tt < p.horizon) {
+                        const int sidx = S.sx * p.dim + S.sy;
+                        if (!S.memo_ok[sidx]) break;
                         float lg[kDrA];
 #pragma unroll
                         for (int k = 0; k < kDrA; ++k) lg[k] = S.memo_lg[sidx][k];
-                        finish_step(lg, S.memo_q[sidx], t, S.sx, S.sy);
+                        finish_step(lg, S.memo_q[sidx], tt, S.sx, S.sy);
+                        ++tt;
                     }
-                    bar_lds();
-                    continue;
+                    S.tnext = tt;
                 }
+                bar_lds();
+                t = S.tnext;
+                if (t >= p.horizon) break;
             }
             float x[2][8];
 #pragma unroll
