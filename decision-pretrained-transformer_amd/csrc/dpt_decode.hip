@@ -824,7 +824,7 @@ struct BanditRolloutParams {
     int N, H, A, type, sample, n_layer;
     int64_t first_task;
     double var;
-    uint64_t seed;
+    uint64_t seed, counter;
     const double* means;
     const double* uniforms;
     const double* noise;
@@ -851,14 +851,15 @@ __global__ void rollout_draws_kernel(BanditRolloutParams Pr) {
     const int task = (int)(i / Pr.H), h = (int)(i % Pr.H);
     const int64_t gtask = Pr.first_task + task;
     double u = 0.0, g;
+    const uint64_t ctr = Pr.counter + (uint64_t)h;
     if (Pr.sample)
-        u = Pr.uniforms ? Pr.uniforms[(size_t)h * Pr.N + task] : philox_uniform(Pr.seed, h, gtask, DPT_STREAM_SELECT);
+        u = Pr.uniforms ? Pr.uniforms[(size_t)h * Pr.N + task] : philox_uniform(Pr.seed, ctr, gtask, DPT_STREAM_SELECT);
     if (Pr.noise)
         g = Pr.noise[(size_t)h * Pr.N + task];
     else if (Pr.type == DPT_BANDIT_BERNOULLI)
-        g = philox_uniform(Pr.seed, h, gtask, DPT_STREAM_REWARD);
+        g = philox_uniform(Pr.seed, ctr, gtask, DPT_STREAM_REWARD);
     else
-        g = philox_normal(Pr.seed, h, gtask, DPT_STREAM_REWARD);
+        g = philox_normal(Pr.seed, ctr, gtask, DPT_STREAM_REWARD);
     draw_pairs(Pr, task)[h] = make_double2(u, g);
 }
 
@@ -1111,7 +1112,7 @@ int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, 
     }
     BanditRolloutParams P;
     P.N = a.N; P.H = a.H; P.A = a.A; P.type = a.type; P.sample = a.sample;
-    P.first_task = a.first_task; P.var = a.var; P.seed = a.seed;
+    P.first_task = a.first_task; P.var = a.var; P.seed = a.seed; P.counter = a.counter;
     P.means = a.means; P.uniforms = a.uniforms; P.noise = a.noise; P.kv = a.kvcache;
     P.actions_out = a.actions_out; P.rewards_out = a.rewards_out; P.arm_value_out = a.arm_value_out;
     P.logits_out = a.logits_out;

@@ -39,11 +39,14 @@ class DarkroomTransformerController(Controller):
         self._stream = _SelectStream()
         self.uniforms = None
 
-    def select(self, logits):
-        """Device action indices for (B, A) logits (ctrl_darkroom.py:48-59)."""
+    def select(self, logits, first_task=0):
+        """Device action indices for (B, A) logits (ctrl_darkroom.py:48-59).  Philox draws are
+        keyed by the global task id (``first_task`` + row), as in the fused rollout, so a
+        sharded env's tasks draw the same uniforms on any rank layout."""
         seed, ctr = self._stream.next()
         u = self.uniforms(ctr) if (self.sample and self.uniforms is not None) else None
-        return dpt_hip.select_action(logits, self.sample, self.temp, uniforms=u, seed=seed, counter=ctr)
+        return dpt_hip.select_action(logits, self.sample, self.temp, uniforms=u, seed=seed, counter=ctr,
+                                     first_task=first_task)
 
     def act(self, state):
         self.batch["zeros"] = self.zeros

@@ -147,8 +147,11 @@ class DeviceModel:
         return logits
 
     def rollout_bandit(self, means, H, var, sample=True, bandit_type=BANDIT_GAUSSIAN, seed=0,
-                       first_task=0, uniforms=None, noise=None, want_logits=False):
+                       first_task=0, uniforms=None, noise=None, want_logits=False, counter=0):
         """Fused online bandit rollout (evals/eval_bandit.py:56-103) on device.
+
+        Step h draws at Philox counter ``counter + h`` (global task id first_task + i),
+        the counters the per-step path's selects would consume from ``counter`` on.
 
         Returns dict of device tensors: actions (N,H) int32, rewards (N,H) f64,
         arm_value (N,H) f64 (= cum_means.T), logits (H,N,A) f32 if requested.
@@ -170,7 +173,7 @@ class DeviceModel:
             N, H, A, int(bandit_type), int(bool(sample)), 0, int(first_task), float(var), int(seed) & (2 ** 64 - 1),
             _p(means_d).value, None if u_d is None else _p(u_d).value, None if g_d is None else _p(g_d).value,
             _p(kv).value, _p(out["actions"]).value, _p(out["rewards"]).value, _p(out["arm_value"]).value,
-            None if out["logits"] is None else _p(out["logits"]).value)
+            None if out["logits"] is None else _p(out["logits"]).value, int(counter) & (2 ** 64 - 1))
         _lib.call("dpt_rollout_bandit", self._h, ctypes.byref(args), _stream())
         out["_keep"] = (kv, means_d, u_d, g_d)
         return out
@@ -181,9 +184,9 @@ class DeviceModel:
         """Fused DarkRoom online evaluation (evals/eval_darkroom.py:20-84) on device.
 
         Returns dict of device tensors: returns (N, Heps) int32, actions (N, Heps*horizon)
-        int32, logits (Heps*horizon, N, 5) f32 and forwards (N,) int32 (window forwards
-        run per task: one per distinct state per episode under set_darkroom_memo) if
-        requested.  Raises
+        int32, logits (Heps*horizon, N, 5) f32 and forwards (N, Heps) int32 (window
+        forwards run per task and episode: one per distinct state per episode under
+        set_darkroom_memo) if requested.  Raises
         NotImplementedError outside sd=2 / A=5 / window <= 128 (use the per-step path).
         """
         dev = device()

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdpt_hip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 DPT_OK = 0
 DPT_EINVAL = -1
@@ -48,7 +48,7 @@ class BanditRolloutArgs(ctypes.Structure):
                 ("reserved0", _i32), ("first_task", _i64), ("var", _f64), ("seed", _u64),
                 ("means", _c_void_p), ("uniforms", _c_void_p), ("noise", _c_void_p),
                 ("kvcache", _c_void_p), ("actions_out", _c_void_p), ("rewards_out", _c_void_p),
-                ("arm_value_out", _c_void_p), ("logits_out", _c_void_p)]
+                ("arm_value_out", _c_void_p), ("logits_out", _c_void_p), ("counter", _u64)]
 
 
 # name -> (restype, argtypes); mirrors include/dpt_hip.h exactly

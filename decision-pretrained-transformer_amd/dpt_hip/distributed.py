@@ -48,21 +48,21 @@ def sharded_online(rollout_fn, means_all, group=None):
 def regret_stats_allreduce(opt_local, lnr_local, n_total, group=None):
     """Suboptimality and cumulative-regret mean / SEM curves over ALL tasks of all ranks
     (evals/eval_bandit.py:169-178: diff = opt - lnr, cumsum over steps, mean and
-    scipy.stats.sem with ddof=1 over tasks) from one all_reduce of per-step moments
-    (4 x H fp64) instead of gathering every task's curve.  Same values as the gathered
-    computation up to fp64 summation order (sum-of-squares form of the variance).
+    scipy.stats.sem with ddof=1 over tasks) without gathering every task's curve.
+
+    Two all_reduces of 2 x H fp64: the per-step sums give the global means, then each
+    rank sums its squared deviations from those means (the centred two-pass form
+    scipy uses, so a large mean relative to the spread loses nothing to cancellation,
+    as the sum-of-squares form would).  Equal to scipy.stats.sem over the gathered
+    curves up to fp64 summation order.
     opt_local / lnr_local: (count, H) arm-value curves of this rank's tasks."""
     diff = opt_local.to(torch.float64) - lnr_local.to(torch.float64)
     cr = torch.cumsum(diff, dim=1)
-    mom = torch.stack([diff.sum(0), (diff * diff).sum(0), cr.sum(0), (cr * cr).sum(0)])
-    dist.all_reduce(mom, group=group)
     n = float(n_total)
-
-    def mean_sem(s1, s2):
-        mean = s1 / n
-        var = (s2 - s1 * mean) / (n - 1.0)
-        return mean, torch.sqrt(torch.clamp(var, min=0.0) / n)
-
-    sm, ss = mean_sem(mom[0], mom[1])
-    rm, rsem = mean_sem(mom[2], mom[3])
-    return dict(subopt_mean=sm, subopt_sem=ss, regret_mean=rm, regret_sem=rsem)
+    s1 = torch.stack([diff.sum(0), cr.sum(0)])
+    dist.all_reduce(s1, group=group)
+    mean = s1 / n
+    m2 = torch.stack([((diff - mean[0]) ** 2).sum(0), ((cr - mean[1]) ** 2).sum(0)])
+    dist.all_reduce(m2, group=group)
+    sem = torch.sqrt(m2 / (n - 1.0) / n)
+    return dict(subopt_mean=mean[0], subopt_sem=sem[0], regret_mean=mean[1], regret_sem=sem[1])

@@ -48,12 +48,27 @@ def _fused_ok(vec_env, controller, horizon):
             and controller.batch_size == vec_env.num_envs and horizon <= controller.model.n_positions)
 
 
-def rollout_fused(vec_env, controller, horizon, uniforms=None, noise=None, seed=None, first_task=0):
-    """One-launch online rollout; returns the device result dict of DeviceModel.rollout_bandit."""
+def rollout_fused(vec_env, controller, horizon, uniforms=None, noise=None, seed=None, first_task=None):
+    """One-launch online rollout; returns the device result dict of DeviceModel.rollout_bandit.
+
+    Selection draws are the controller's own stream, as in the per-step path
+    (BanditTransformerController._select): the H counters that loop would consume
+    one per step are consumed here in one go, so both paths act on the same
+    Philox draws, and uniforms injected on the controller (``controller.uniforms``)
+    are used unless ``uniforms`` is given explicitly.  Draws are keyed by the
+    global task id (``vec_env.first_task`` for a shard).
+    """
     dm = controller.model.device_model()
-    seed = dpt_hip.next_seed() if seed is None else seed
+    s0, ctr0 = controller._stream.next()
+    controller._stream.counter = ctr0 + horizon
+    seed = s0 if seed is None else seed
+    if uniforms is None and controller.sample and controller.uniforms is not None:
+        uniforms = np.stack([np.asarray(controller.uniforms(ctr0 + h), dtype=np.float64).reshape(-1)
+                             for h in range(horizon)])
+    if first_task is None:
+        first_task = getattr(vec_env, "first_task", 0)
     return dm.rollout_bandit(vec_env.means_device, horizon, vec_env.var, controller.sample, vec_env.type_code,
-                             seed=seed, first_task=first_task, uniforms=uniforms, noise=noise)
+                             seed=seed, first_task=first_task, uniforms=uniforms, noise=noise, counter=ctr0)
 
 
 def _policy_ok(vec_env, controller):

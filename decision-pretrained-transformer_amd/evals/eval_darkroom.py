@@ -40,6 +40,7 @@ def _episode_device(dm, ctrl, vec_env, ctx, horizon):
     ea = torch.empty((N, horizon), dtype=torch.int64, device=dev)
     er = torch.empty((N, horizon), dtype=torch.int32, device=dev)
     goals, perms, dim = vec_env.goals_device, vec_env.perms_device, vec_env.dim
+    first_task = getattr(vec_env, "first_task", 0)  # draws keyed by global task id, as in rollout_fused
     memo = None
     if dpt_hip.darkroom_memo():
         memo = torch.empty((N, dim * dim, vec_env.action_dim), dtype=torch.float32, device=dev)
@@ -56,7 +57,7 @@ def _episode_device(dm, ctrl, vec_env, ctx, horizon):
                 memo[need, cell[need]] = lg
                 seen[need, cell[need]] = True
             logits = memo[rows, cell]
-        a = ctrl.select(logits)
+        a = ctrl.select(logits, first_task=first_task)
         es[:, t] = state
         ea[:, t] = a
         state, r = dpt_hip.darkroom_step(state, a, goals, perms, dim)

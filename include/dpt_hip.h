@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 2
+#define DPT_ABI_VERSION 3
 
 /* error codes (mapped to the reference's Python exceptions by dpt_hip/_lib.py) */
 #define DPT_OK 0
@@ -230,6 +230,9 @@ typedef struct dpt_bandit_rollout_args {
     double* rewards_out;    /* (N, H)                                       */
     double* arm_value_out;  /* (N, H)  = cum_means.T                         */
     float* logits_out;      /* (H, N, A) or NULL                             */
+    uint64_t counter;       /* Philox counter of step 0: step h draws at
+                             * counter + h, as the per-step path's selects
+                             * (dpt_select_action) numbered from `counter` */
 } dpt_bandit_rollout_args;
 
 int dpt_rollout_bandit(const dpt_model* model, const dpt_bandit_rollout_args* args_host,

@@ -95,3 +95,46 @@ def test_gloo_world2_sharded_equals_single():
     ref = O.regret_curves(opt, single)
     for k, v in ref.items():
         assert np.allclose(stats[k], v, rtol=1e-9, atol=1e-12), k
+
+
+def _stats_worker(rank, port, opt, lnr, q):
+    import sys
+    sys.path[:0] = [PKG, ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    from dpt_hip.distributed import regret_stats_allreduce, shard
+    first, count = shard(opt.shape[0], WORLD, rank)
+    sl = slice(first, first + count)
+    stats = regret_stats_allreduce(torch.from_numpy(opt[sl]), torch.from_numpy(lnr[sl]), opt.shape[0])
+    if rank == 0:
+        q.put({k: v.numpy() for k, v in stats.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_regret_sem_matches_scipy():
+    """regret_stats_allreduce at H=1000 (the linear-bandit horizon) on curves whose cumulative
+    regret has a large mean relative to its spread: mean and SEM equal scipy.stats.sem over the
+    gathered curves (evals/eval_bandit.py:169-178) to fp64 summation order."""
+    import scipy.stats
+    rs = np.random.RandomState(6)
+    N, H = 301, 1000
+    opt = np.repeat(rs.uniform(0.9, 1.0, (N, 1)), H, axis=1)
+    lnr = opt - 0.25 - 1e-6 * rs.standard_normal((N, H))  # regret ~0.25 per step, tiny spread
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, port, opt, lnr, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    stats = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    diff = opt - lnr
+    cr = np.cumsum(diff, axis=1)
+    for key, x in (("subopt", diff), ("regret", cr)):
+        assert np.allclose(stats[f"{key}_mean"], x.mean(0), rtol=1e-12, atol=0), key
+        ref_sem = scipy.stats.sem(x, axis=0)
+        assert np.allclose(stats[f"{key}_sem"], ref_sem, rtol=1e-6, atol=0), key

@@ -93,6 +93,41 @@ def test_generic_loop_equals_fused():
         assert np.array_equal(a, b)
 
 
+def test_fused_bandit_uses_controller_stream():
+    """The fused bandit rollout draws its selection uniforms from the controller's own stream:
+    fused and per-step loops act on the same Philox draws (var=0: no env noise), the stream
+    advances by H either way, and uniforms injected on the controller are used by both."""
+    from ctrls.ctrl_bandit import BanditTransformerController
+    from envs.bandit_env import BanditEnv, BanditEnvVec
+    from evals import eval_bandit
+    _, m = ref_model("bandit5")
+    rs = np.random.RandomState(12)
+    n, H = 24, 16
+    envs = [BanditEnv(rs.uniform(0, 1, 5), H, var=0.0) for _ in range(n)]
+    vec = BanditEnvVec(envs)
+
+    def ctrl(counter=0, uniforms=None):
+        c = BanditTransformerController(m, sample=True, batch_size=n)
+        c._stream.seed, c._stream.counter = 4242, counter
+        c.uniforms = uniforms
+        return c
+
+    for counter in (0, 37):
+        cf, cg = ctrl(counter), ctrl(counter)
+        a_f = eval_bandit.deploy_online_vec(vec, cf, H, include_meta=True)[1]["context_actions"]
+        a_g = eval_bandit.deploy_online_vec(vec, cg, H, include_meta=True, fused=False)[1]["context_actions"]
+        assert np.array_equal(a_f, a_g), counter
+        assert cf._stream.counter == cg._stream.counter == counter + H
+    u = rs.uniform(size=(100, n))
+    cf, cg = ctrl(5, lambda k: u[k]), ctrl(5, lambda k: u[k])
+    a_f = eval_bandit.deploy_online_vec(vec, cf, H, include_meta=True)[1]["context_actions"]
+    a_g = eval_bandit.deploy_online_vec(vec, cg, H, include_meta=True, fused=False)[1]["context_actions"]
+    assert np.array_equal(a_f, a_g)
+    # explicit uniforms override the controller's; counters 5..5+H of u are the ones used
+    out = eval_bandit.rollout_fused(vec, ctrl(0), H, uniforms=u[5:5 + H])
+    assert np.array_equal(np.eye(5)[out["actions"].cpu().numpy()], a_f)
+
+
 def test_offline_greedy_matches_reference():
     from ctrls.ctrl_bandit import BanditTransformerController
     from envs.bandit_env import BanditEnv, BanditEnvVec
@@ -205,6 +240,29 @@ def test_eval_darkroom_per_step_memo_bit_identical():
     finally:
         dpt_hip.set_darkroom_memo(True)
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_eval_darkroom_per_step_shard_invariant():
+    """The per-step device loop (window 1 + 2*70 = 141 > 128 tokens, so not fused) keys its
+    selection draws by the GLOBAL task id (DarkroomEnvVec.first_task), like the fused kernel:
+    two shards of the tasks, each with the same controller seed, give the unsharded returns."""
+    from ctrls.ctrl_darkroom import DarkroomTransformerController
+    from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec
+    from evals import eval_darkroom
+    _, m = ref_model("darkroom")
+    rs = np.random.RandomState(9)
+    goals = [rs.randint(0, 10, 2) for _ in range(40)]
+
+    def run(lo, hi):
+        envs = [DarkroomEnv(10, g_, 70) for g_ in goals[lo:hi]]
+        ctrl = DarkroomTransformerController(m, batch_size=hi - lo, sample=True)
+        ctrl._stream.seed = 31337
+        vec = DarkroomEnvVec(envs, first_task=lo)
+        assert not eval_darkroom._fused_ok(vec, ctrl, 140)
+        return eval_darkroom.deploy_online_vec(vec, ctrl, 3, 140, 70)
+
+    full = run(0, 40)
+    assert np.array_equal(np.concatenate([run(0, 17), run(17, 40)]), full)
 
 
 def test_rollin_kernels_match_oracle():

@@ -312,21 +312,30 @@ def test_rollout_darkroom_large_properties():
         st = ns
 
 
-def test_rollout_darkroom_memo_bit_identical():
+@pytest.mark.parametrize("sample", [1, 0])
+@pytest.mark.parametrize("permuted", [False, True])
+def test_rollout_darkroom_memo_bit_identical(sample, permuted):
     """The per-episode logits memo (one window forward per distinct query state) changes nothing:
     actions, per-step logits and returns are bit-identical to one forward per step, and the
-    forward counter equals the number of distinct (episode, state) pairs the trajectory visits."""
+    forward counter equals the number of distinct (episode, state) pairs the trajectory visits.
+    Greedy selection (sample=0) is where the memo-hit runs are longest; permuted actions go
+    through the per-task action permutation of DarkroomEnvPermuted."""
     import dpt_hip
+    import itertools
     _, m, _ = model_from_golden("darkroom")
-    rs = np.random.RandomState(5)
+    rs = np.random.RandomState(5 + 2 * sample + permuted)
     N, Heps, horizon, R = 512, 3, 100, 1
     goals = rs.randint(0, 10, (N, 2))
+    perms = None
+    if permuted:
+        table = np.array(list(itertools.permutations(range(5))), np.int32)
+        perms = table[rs.randint(0, len(table), N)]
     outs = []
     try:
         for memo in (False, True):
             dpt_hip.set_darkroom_memo(memo)
-            o = m.rollout_darkroom(goals, Heps, horizon, R, seed=21, want_actions=True, want_logits=True,
-                                   want_forwards=True)
+            o = m.rollout_darkroom(goals, Heps, horizon, R, perms=perms, sample=bool(sample), seed=21,
+                                   want_actions=True, want_logits=True, want_forwards=True)
             outs.append({k: o[k].cpu().numpy() for k in ("actions", "logits", "returns", "forwards")})
     finally:
         dpt_hip.set_darkroom_memo(True)  # the library default
@@ -341,7 +350,7 @@ def test_rollout_darkroom_memo_bit_identical():
         seen = np.zeros((N, 100), bool)
         for t in range(horizon):
             seen[np.arange(N), st[:, 0] * 10 + st[:, 1]] = True
-            st, _ = O.darkroom_transit(st, acts[:, e, t], goals)
+            st, _ = O.darkroom_transit(st, acts[:, e, t], goals, perm=perms)
         distinct[:, e] = seen.sum(1)
     assert np.array_equal(on["forwards"], distinct)
     assert on["forwards"].sum() < off["forwards"].sum()
