@@ -60,6 +60,7 @@ int launch_prefill(const ModelView&, const float*, const float*, const float*, c
                    const float*, int, int, int, float*, hipStream_t);
 int set_decode_tile(int);
 int set_darkroom_memo(int);
+int set_cache_budget(int64_t);
 
 }  // namespace dpt
 
@@ -117,6 +118,10 @@ int dpt_tuning_set(int32_t key, int64_t value) {
     }
     if (key == DPT_TUNE_DARKROOM_MEMO) {
         REQUIRE(set_darkroom_memo((int)value) == DPT_OK, "darkroom memo %lld: 0 or 1", (long long)value);
+        return DPT_OK;
+    }
+    if (key == DPT_TUNE_CACHE_BUDGET) {
+        REQUIRE(set_cache_budget(value) == DPT_OK, "cache budget %lld B: >= 0", (long long)value);
         return DPT_OK;
     }
     set_error(DPT_EINVAL, "unknown tuning key %d", key);

@@ -20,6 +20,7 @@ constexpr int kMaxA = 32;       // action_dim limit of the selection / head tile
 constexpr int kMaxF = 64;       // token feature limit (2*sd + A + 1)
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef double doublex2 __attribute__((ext_vector_type(2)));
 
 // ----------------------------------------------------------------------------- error plumbing
 void set_error(int code, const char* fmt, ...);

@@ -61,6 +61,9 @@ constexpr int kRows = 4;                  // K/V rows (of 8 positions) in flight
 #endif
 constexpr int kYRows = DPT_YROWS;         // y rows in flight per wave (rollout blocks >= 1; 8: -1.5 % vs 4)
 constexpr int kChunks = kFF / 16;         // hidden-unit chunks of the fused c_fc -> mlp.c_proj
+#ifndef DPT_DEFAULT_CACHE_BUDGET
+#define DPT_DEFAULT_CACHE_BUDGET (224ll << 20)
+#endif
 
 // barrier for LDS hand-offs only: does not wait for outstanding global stores
 __device__ inline void bar_lds() {
@@ -209,16 +212,20 @@ __device__ inline float gelu_new(float x) {
 // cache (global), position pos from LDS.  Writes o = softmax(qK^T/sqrt(E)) V.
 // KV_SAME (the rollout's blocks >= 1): keys and values are one stream (the
 // LayerNorm outputs y_p, see attend_l0 for the algebra), read once.
+// Cached rows of positions < pin (wave-uniform, a multiple of 8 * NR) are read with
+// the default cache policy, later ones non-temporally (see BanditRolloutParams::pin).
 template <bool KV_SAME = false, int NR = kRows>
 __device__ inline float4 attend_one(const float* __restrict__ kc, const float* __restrict__ vc, int pos,
                                     const float* q, const float* kcur, const float* vcur, float* o,
-                                    int lane) {
+                                    int lane, int pin = 0) {
     const int g = lane >> 3, c = lane & 7;
     const float scale = 0.17677669529663687f * 1.4426950408889634f;  // 32 ** -0.5 * log2(e): exp2 domain
     const float4 q4 = *reinterpret_cast<const float4*>(q + 4 * c);
     float m = -1e30f, l = 0.f;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int base = 0; base < pos; base += 8 * NR) {
+    // one chunk of 8 * NR positions; NT: non-temporal loads
+    auto chunk = [&](int base, auto ntc) {
+        constexpr bool NT = decltype(ntc)::value;
         float4 kk[NR], vv[NR];
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
@@ -226,13 +233,14 @@ __device__ inline float4 attend_one(const float* __restrict__ kc, const float* _
             if (p < pos) {
                 // non-temporal: each K/V row is read once per step by this CU only, so it
                 // must not evict the weights every workgroup re-reads from L2
-                const floatx4 k4 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kc + (size_t)p * kE) + c);
+                const floatx4* ks = reinterpret_cast<const floatx4*>(kc + (size_t)p * kE) + c;
+                const floatx4 k4 = NT ? __builtin_nontemporal_load(ks) : *ks;
                 kk[r] = make_float4(k4[0], k4[1], k4[2], k4[3]);
                 if (KV_SAME) {
                     vv[r] = kk[r];
                 } else {
-                    const floatx4 v4 =
-                        __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vc + (size_t)p * kE) + c);
+                    const floatx4* vs = reinterpret_cast<const floatx4*>(vc + (size_t)p * kE) + c;
+                    const floatx4 v4 = NT ? __builtin_nontemporal_load(vs) : *vs;
                     vv[r] = make_float4(v4[0], v4[1], v4[2], v4[3]);
                 }
             } else {
@@ -267,7 +275,12 @@ __device__ inline float4 attend_one(const float* __restrict__ kc, const float* _
             acc.w = fmaf(pr, vv[r].w, acc.w);
         }
         m = mn;
-    }
+    };
+    int base = 0;
+#pragma unroll 1
+    for (const int pe = min(pos, pin); base < pe; base += 8 * NR) chunk(base, std::false_type{});
+#pragma unroll 1
+    for (; base < pos; base += 8 * NR) chunk(base, std::true_type{});
     {   // the new position (group 0 only; all lanes run the shuffles)
         const float4 k4 = *reinterpret_cast<const float4*>(kcur + 4 * c);
         const float4 v4 = *reinterpret_cast<const float4*>(vcur + 4 * c);
@@ -502,7 +515,7 @@ __device__ inline void zero_smem(Smem& S) {
 template <int TILE, bool L0R = false, bool GL = false>
 __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, const ModelView& M,
                                 float* __restrict__ kv, int N, int max_pos, int tile0, int pos, float wpe_j,
-                                const float* D = nullptr) {
+                                const float* D = nullptr, int pin = 0, int pin_x = 0) {
     constexpr int kProjWave = TILE - 1;  // a wave with no c_attn tile (TILE >= 8)
     // opaque copy of the thread id: every lane-derived address is recomputed per call
     // instead of being hoisted out of the caller's step loop (128-VGPR budget, no spills)
@@ -526,6 +539,8 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
     bar_lds();
     DPT_STAMP(0);
 
+    // block l's y rows of positions < lpin(l) use the default cache policy (rollout_pin)
+    auto lpin = [&](int l) { return pin + (l <= pin_x ? 8 * kYRows : 0); };
     for (int li = 0; li < M.n_layer; ++li) {
         asm volatile("" : "+v"(tid_));  // and per layer (see above)
         const int lane = tid_ & 63, i16 = lane & 15, kq = lane >> 4;
@@ -606,7 +621,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                                        PL + PLay::ln1_b, nullptr, lane)
                            // scores y_p . u, output sum_p P_p y_p; y_pos is in S.kcur
                            : attend_one<true, kYRows>(kc, kc, pos, S.q[wave], S.kcur[wave], S.kcur[wave], nullptr,
-                                                      lane);
+                                                      lane, lpin(li));
                     // c_proj (folded Wvp) + residual + ln_2 of this task, in this wave
                     proj_ln_task(o4, D + rl.wvp + li * kE * kE, D + rl.bvp + li * kE, PL + PLay::ln2_g,
                                  PL + PLay::ln2_b, S.x[wave], S.xn[wave], lane);
@@ -709,8 +724,11 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
             if (L0R && !last) {  // block li+1's y at `pos`: its K/V-cache row (128 B per half-wave)
                 S.kcur[t][j] = y;
                 const int task = tile0 + t;
-                if (task < N)
-                    __builtin_nontemporal_store(y, kv + (li + 1) * lstride + ((size_t)task * max_pos + pos) * kE + j);
+                float* yd = kv + (li + 1) * lstride + ((size_t)task * max_pos + pos) * kE + j;
+                if (task < N) {
+                    if (pos < lpin(li + 1)) *yd = y;
+                    else __builtin_nontemporal_store(y, yd);
+                }
             }
         }
         bar_lds();
@@ -822,6 +840,9 @@ __global__ __launch_bounds__(TILE * 64, 4) void window_decode_kernel(
 
 struct BanditRolloutParams {
     int N, H, A, type, sample, n_layer;
+    // y rows of positions < pin (+ 8 kYRows for blocks 1..pin_x) use the default cache
+    // policy (Infinity-Cache resident), later ones non-temporal (rollout_pin)
+    int pin, pin_x;
     int64_t first_task;
     double var;
     uint64_t seed, counter;
@@ -927,8 +948,13 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
     for (int h = 0; h < Pr.H; ++h) {
         const float wpe_j = wpe_next;
         if (h + 1 < Pr.H) wpe_next = M.wpe[(size_t)(h + 1) * kE + (tid & 31)];
-        const double2 dr = draws ? draws[h] : make_double2(0.0, 0.0);  // consumed after the forward
-        decode_position<TILE, true, GL>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D);
+        // consumed after the forward; read once, so non-temporal (keeps the pinned rows resident)
+        double2 dr = make_double2(0.0, 0.0);
+        if (draws) {
+            const doublex2 d2 = __builtin_nontemporal_load(reinterpret_cast<const doublex2*>(draws + h));
+            dr = make_double2(d2[0], d2[1]);
+        }
+        decode_position<TILE, true, GL>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D, Pr.pin, Pr.pin_x);
         // selection + env step; the outputs are stored after the barrier so that it
         // waits only for the y rows (issued phases earlier), not for these stores
         const int t = tid, task = tile0 + t;
@@ -947,9 +973,9 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         }
         __syncthreads();  // y rows of step h visible before step h+1 reads them
         if (live) {
-            Pr.actions_out[(size_t)task * Pr.H + h] = a;
-            Pr.rewards_out[(size_t)task * Pr.H + h] = r;
-            Pr.arm_value_out[(size_t)task * Pr.H + h] = mean;
+            __builtin_nontemporal_store(a, Pr.actions_out + (size_t)task * Pr.H + h);
+            __builtin_nontemporal_store(r, Pr.rewards_out + (size_t)task * Pr.H + h);
+            __builtin_nontemporal_store(mean, Pr.arm_value_out + (size_t)task * Pr.H + h);
             if (Pr.logits_out)  // S.logits is next rewritten by step h+1's head phase
                 for (int k = 0; k < A; ++k) Pr.logits_out[((size_t)h * Pr.N + task) * A + k] = S.logits[t][k];
             // first read from memory by step h+2 (positions < h+2), so it may land during step h+1
@@ -1036,6 +1062,31 @@ extern "C" int dpt_debug_stamps(unsigned long long* out, int n, int reset) {
 #endif
 
 static int g_decode_tile = 8;  // tuning knob (dpt_tuning_set(DPT_TUNE_DECODE_TILE, 8|16))
+static int64_t g_cache_budget = DPT_DEFAULT_CACHE_BUDGET;  // DPT_TUNE_CACHE_BUDGET
+
+int set_cache_budget(int64_t b) {
+    if (b < 0) return DPT_EINVAL;
+    g_cache_budget = b;
+    return DPT_OK;
+}
+
+// The rollout re-reads every cached y row of a task at every later step, the
+// earliest positions most often.  Rows of positions < pin are stored and read with
+// the default policy and, while they fit the budget, stay in the Infinity Cache
+// across steps; the rest stream non-temporally and do not displace them.  The
+// budget is spent in whole stream chunks (8 kYRows positions of one block): every
+// block gets `pin` positions and blocks 1..pin_x one chunk more.
+static void rollout_pin(int N, int H, int n_layer, int* pin, int* pin_x) {
+    constexpr int chunk = 8 * kYRows;
+    const int64_t row = (int64_t)N * kE * sizeof(float);  // one position of one block, all tasks
+    const int64_t nb = n_layer - 1;                          // blocks with a y cache
+    *pin = 0;
+    *pin_x = 0;
+    if (nb <= 0 || row <= 0) return;
+    const int64_t chunks = g_cache_budget / (row * chunk);
+    *pin = (int)std::min<int64_t>((chunks / nb) * chunk, H);
+    if (*pin < H) *pin_x = (int)(chunks % nb);
+}
 
 int set_decode_tile(int t) {
     if (t != 8 && t != 16) return DPT_EINVAL;
@@ -1117,6 +1168,7 @@ int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, 
     P.actions_out = a.actions_out; P.rewards_out = a.rewards_out; P.arm_value_out = a.arm_value_out;
     P.logits_out = a.logits_out;
     P.n_layer = M.n_layer;
+    rollout_pin(a.N, a.H, M.n_layer, &P.pin, &P.pin_x);
     const int64_t nd = (int64_t)a.N * a.H;
     hipLaunchKernelGGL(rollout_draws_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st, P);
     auto launch = [&](auto kernel, int tile) {

@@ -355,6 +355,13 @@ def set_decode_tile(tile):
     _lib.call("dpt_tuning_set", _lib.TUNE_DECODE_TILE, int(tile))
 
 
+def set_cache_budget(nbytes):
+    """Bytes of the Infinity Cache the bandit rollout may fill with its earliest positions' cached
+    rows (default policy, resident across steps); 0 streams every row non-temporally.  Cache
+    policy only: results are bit-identical for any value."""
+    _lib.call("dpt_tuning_set", _lib.TUNE_CACHE_BUDGET, int(nbytes))
+
+
 _darkroom_memo = True
 
 

@@ -148,6 +148,7 @@ SIGNATURES.update({
 TUNE_DECODE_TILE = 1
 TUNE_PREFILL = 2
 TUNE_DARKROOM_MEMO = 3
+TUNE_CACHE_BUDGET = 4
 SIGNATURES["dpt_tuning_set"] = (_i32, [_i32, _i64])
 
 

@@ -71,10 +71,17 @@ const char* dpt_last_error(void);
  * DPT_TUNE_DARKROOM_MEMO = 1 (default): dpt_rollout_darkroom runs one window
  * forward per distinct query state per episode (the window is fixed within an
  * episode, so a repeated state's logits are the same pure function of the same
- * inputs: results are bit-identical); 0: one forward per step.  */
+ * inputs: results are bit-identical); 0: one forward per step.
+ * DPT_TUNE_CACHE_BUDGET = bytes of the 256 MiB Infinity Cache that
+ * dpt_rollout_bandit may fill with the cached rows of its earliest positions
+ * (stored and streamed with the default cache policy, so they stay resident and
+ * are re-read on-die every step; later positions stream non-temporally and do
+ * not displace them).  0: every row non-temporal.  Cache policy only: results
+ * are bit-identical for any value.  */
 #define DPT_TUNE_DECODE_TILE 1
 #define DPT_TUNE_PREFILL 2
 #define DPT_TUNE_DARKROOM_MEMO 3
+#define DPT_TUNE_CACHE_BUDGET 4
 int dpt_tuning_set(int32_t key, int64_t value);
 /* number of visible gfx950 devices (0 on a CPU-only host; never faults) */
 int dpt_device_count(int* count_out_host);

@@ -241,6 +241,28 @@ def test_decode_tiles_bit_identical():
     assert_logits(outs[1][3], g["T101/preds_train"])
 
 
+def test_rollout_cache_budget_bit_identical():
+    """DPT_TUNE_CACHE_BUDGET only moves the default/non-temporal split of the y stream: budgets of
+    0, one chunk (block 1 only), four chunks (every block 64 positions, block 1 128) and everything
+    give bit-identical rollouts."""
+    import dpt_hip
+    _, m, _ = model_from_golden("bandit5")
+    N, H = 300, 150
+    means = np.random.RandomState(11).uniform(0, 1, (N, 5))
+    chunk = N * 32 * 4 * 64  # one 64-position stream chunk of one block, all tasks
+    outs = []
+    try:
+        for budget in (0, chunk, 4 * chunk, 1 << 40):
+            dpt_hip.set_cache_budget(budget)
+            o = m.rollout_bandit(means, H, 0.3, True, seed=7, want_logits=True)
+            outs.append([o[k].cpu().numpy() for k in ("actions", "rewards", "arm_value", "logits")])
+    finally:
+        dpt_hip.set_cache_budget(224 << 20)  # the library default
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("tag", ["sample", "greedy", "permuted"])
 def test_rollout_darkroom_fused_matches_reference(tag):
     """dpt_rollout_darkroom against the reference's deploy_online_vec recorded with the same draws:
