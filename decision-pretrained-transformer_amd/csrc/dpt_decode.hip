@@ -208,50 +208,68 @@ __device__ inline float gelu_new(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
+// Packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32): two lanes' worth of
+// fp32 work per VALU instruction, each half rounded exactly like the scalar op.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ inline f2 splat2(float s) { return f2{s, s}; }
+__device__ inline f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Calls f(integral_constant<R'>) for the smallest power of two R' <= R with
+// 8 R' >= rem: the last, partial chunk of a stream runs only the rows it needs.
+template <int R, class F>
+__device__ inline void tail_rows(int rem, F&& f) {
+    if constexpr (R == 1) {
+        f(std::integral_constant<int, 1>{});
+    } else {
+        if (rem > 8 * (R / 2)) f(std::integral_constant<int, R>{});
+        else tail_rows<R / 2>(rem, f);
+    }
+}
+
 // Flash-decoding attention of one task (one wave): positions 0..pos-1 from the
 // cache (global), position pos from LDS.  Writes o = softmax(qK^T/sqrt(E)) V.
 // KV_SAME (the rollout's blocks >= 1): keys and values are one stream (the
 // LayerNorm outputs y_p, see attend_l0 for the algebra), read once.
 // Cached rows of positions < pin (wave-uniform, a multiple of 8 * NR) are read with
 // the default cache policy, later ones non-temporally (see BanditRolloutParams::pin).
+// Accumulators are packed pairs (lo = dims 4c, 4c+1; hi = 4c+2, 4c+3).
 template <bool KV_SAME = false, int NR = kRows>
-__device__ inline float4 attend_one(const float* __restrict__ kc, const float* __restrict__ vc, int pos,
+__device__ __attribute__((always_inline)) inline float4 attend_one(const float* __restrict__ kc, const float* __restrict__ vc, int pos,
                                     const float* q, const float* kcur, const float* vcur, float* o,
                                     int lane, int pin = 0) {
     const int g = lane >> 3, c = lane & 7;
     const float scale = 0.17677669529663687f * 1.4426950408889634f;  // 32 ** -0.5 * log2(e): exp2 domain
-    const float4 q4 = *reinterpret_cast<const float4*>(q + 4 * c);
+    const floatx4 q4 = *reinterpret_cast<const floatx4*>(q + 4 * c);
     float m = -1e30f, l = 0.f;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    // one chunk of 8 * NR positions; NT: non-temporal loads
-    auto chunk = [&](int base, auto ntc) {
+    f2 alo = {0.f, 0.f}, ahi = {0.f, 0.f};
+    // one chunk of 8 * R positions; NT: non-temporal loads
+    auto chunk = [&](int base, auto ntc, auto nrc) {
         constexpr bool NT = decltype(ntc)::value;
-        float4 kk[NR], vv[NR];
+        constexpr int R = decltype(nrc)::value;
+        floatx4 kk[R], vv[R];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
+        for (int r = 0; r < R; ++r) {
             const int p = base + 8 * r + g;
             if (p < pos) {
                 // non-temporal: each K/V row is read once per step by this CU only, so it
                 // must not evict the weights every workgroup re-reads from L2
                 const floatx4* ks = reinterpret_cast<const floatx4*>(kc + (size_t)p * kE) + c;
-                const floatx4 k4 = NT ? __builtin_nontemporal_load(ks) : *ks;
-                kk[r] = make_float4(k4[0], k4[1], k4[2], k4[3]);
+                kk[r] = NT ? __builtin_nontemporal_load(ks) : *ks;
                 if (KV_SAME) {
                     vv[r] = kk[r];
                 } else {
                     const floatx4* vs = reinterpret_cast<const floatx4*>(vc + (size_t)p * kE) + c;
-                    const floatx4 v4 = NT ? __builtin_nontemporal_load(vs) : *vs;
-                    vv[r] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+                    vv[r] = NT ? __builtin_nontemporal_load(vs) : *vs;
                 }
             } else {
-                kk[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+                kk[r] = floatx4{0.f, 0.f, 0.f, 0.f};
                 vv[r] = kk[r];
             }
         }
-        float s[NR];
+        float s[R];
         float mx = -1e30f;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
+        for (int r = 0; r < R; ++r) {
             float d = q4.x * kk[r].x;
             d = fmaf(q4.y, kk[r].y, d);
             d = fmaf(q4.z, kk[r].z, d);
@@ -264,26 +282,34 @@ __device__ inline float4 attend_one(const float* __restrict__ kc, const float* _
         const float mn = fmaxf(m, mx);
         const float corr = __builtin_amdgcn_exp2f(m - mn);
         l *= corr;
-        acc.x *= corr; acc.y *= corr; acc.z *= corr; acc.w *= corr;
+        alo *= splat2(corr);
+        ahi *= splat2(corr);
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
+        for (int r = 0; r < R; ++r) {
             const float pr = __builtin_amdgcn_exp2f(s[r] - mn);
             l += pr;
-            acc.x = fmaf(pr, vv[r].x, acc.x);
-            acc.y = fmaf(pr, vv[r].y, acc.y);
-            acc.z = fmaf(pr, vv[r].z, acc.z);
-            acc.w = fmaf(pr, vv[r].w, acc.w);
+            alo = pk_fma(splat2(pr), vv[r].lo, alo);
+            ahi = pk_fma(splat2(pr), vv[r].hi, ahi);
         }
         m = mn;
     };
+    constexpr auto full = std::integral_constant<int, NR>{};
     int base = 0;
+    // whole chunks; the pinned ones (default cache policy) first
 #pragma unroll 1
-    for (const int pe = min(pos, pin); base < pe; base += 8 * NR) chunk(base, std::false_type{});
+    for (const int pe = min(pos, pin) & ~(8 * NR - 1); base < pe; base += 8 * NR) chunk(base, std::false_type{}, full);
 #pragma unroll 1
-    for (; base < pos; base += 8 * NR) chunk(base, std::true_type{});
+    for (const int pe = pos & ~(8 * NR - 1); base < pe; base += 8 * NR) chunk(base, std::true_type{}, full);
+    if (base < pos) {  // the partial last chunk, with only as many rows as it needs
+        const bool pinned = base < pin;
+        tail_rows<NR>(pos - base, [&](auto nrc) {
+            if (pinned) chunk(base, std::false_type{}, nrc);
+            else chunk(base, std::true_type{}, nrc);
+        });
+    }
     {   // the new position (group 0 only; all lanes run the shuffles)
-        const float4 k4 = *reinterpret_cast<const float4*>(kcur + 4 * c);
-        const float4 v4 = *reinterpret_cast<const float4*>(vcur + 4 * c);
+        const floatx4 k4 = *reinterpret_cast<const floatx4*>(kcur + 4 * c);
+        const floatx4 v4 = *reinterpret_cast<const floatx4*>(vcur + 4 * c);
         float d = q4.x * k4.x;
         d = fmaf(q4.y, k4.y, d);
         d = fmaf(q4.z, k4.z, d);
@@ -295,10 +321,8 @@ __device__ inline float4 attend_one(const float* __restrict__ kc, const float* _
             const float corr = __builtin_amdgcn_exp2f(m - mn);
             const float pr = __builtin_amdgcn_exp2f(sc - mn);
             l = l * corr + pr;
-            acc.x = fmaf(pr, v4.x, acc.x * corr);
-            acc.y = fmaf(pr, v4.y, acc.y * corr);
-            acc.z = fmaf(pr, v4.z, acc.z * corr);
-            acc.w = fmaf(pr, v4.w, acc.w * corr);
+            alo = pk_fma(splat2(pr), v4.lo, alo * splat2(corr));
+            ahi = pk_fma(splat2(pr), v4.hi, ahi * splat2(corr));
             m = mn;
         }
     }
@@ -307,20 +331,20 @@ __device__ inline float4 attend_one(const float* __restrict__ kc, const float* _
         auto xch = [&](float v) { return off == 8 ? dpp_xor8(v) : __shfl_xor(v, off); };
         const float mo = xch(m);
         const float lo = xch(l);
-        const float ax = xch(acc.x), ay = xch(acc.y);
-        const float az = xch(acc.z), aw = xch(acc.w);
+        const f2 olo = {xch(alo.x), xch(alo.y)};
+        const f2 ohi = {xch(ahi.x), xch(ahi.y)};
         const float mn = fmaxf(m, mo);
         const float sa = __builtin_amdgcn_exp2f(m - mn), sb = __builtin_amdgcn_exp2f(mo - mn);
         l = l * sa + lo * sb;
-        acc.x = acc.x * sa + ax * sb;
-        acc.y = acc.y * sa + ay * sb;
-        acc.z = acc.z * sa + az * sb;
-        acc.w = acc.w * sa + aw * sb;
+        alo = alo * splat2(sa) + olo * splat2(sb);
+        ahi = ahi * splat2(sa) + ohi * splat2(sb);
         m = mn;
     }
     // every lane holds dims 4c..4c+3 of the result after the butterfly
     const float inv = 1.0f / l;
-    const float4 res = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    alo *= splat2(inv);
+    ahi *= splat2(inv);
+    const float4 res = make_float4(alo.x, alo.y, ahi.x, ahi.y);
     if (o && lane < 8) *reinterpret_cast<float4*>(o + 4 * c) = res;
     return res;
 }
@@ -336,20 +360,21 @@ __device__ inline float4 attend_one(const float* __restrict__ kc, const float* _
 // folded into c_proj (L0Off::Wvp, bvp).  Writes o = sum_p P_p y_p.  The current
 // position's x is xcur (the residual row, before attention).  A record is
 // (a_p * E as int bits, r_p); scores are kept in the log2 domain (v_exp_f32).
-__device__ inline float4 attend_l0(const float2* __restrict__ tok, const float* __restrict__ wpe, int pos,
+__device__ __attribute__((always_inline)) inline float4 attend_l0(const float2* __restrict__ tok, const float* __restrict__ wpe, int pos,
                                  const float* u, const float* xcur, const float* baseT, const float* wr,
                                  const float* lng, const float* lnb, float* o, int lane) {
     const int g = lane >> 3, c = lane & 7;
     const float scale2 = 0.17677669529663687f * 1.4426950408889634f;  // 32 ** -0.5 * log2(e)
-    const float4 u4 = *reinterpret_cast<const float4*>(u + 4 * c);
-    const float4 g4 = *reinterpret_cast<const float4*>(lng + 4 * c);
-    const float4 gu = make_float4(g4.x * u4.x, g4.y * u4.y, g4.z * u4.z, g4.w * u4.w);
-    const float4 wr4 = *reinterpret_cast<const float4*>(wr + 4 * c);
+    const floatx4 u4 = *reinterpret_cast<const floatx4*>(u + 4 * c);
+    const floatx4 g4 = *reinterpret_cast<const floatx4*>(lng + 4 * c);
+    const floatx4 gu = g4 * u4;
+    const floatx4 wr4 = *reinterpret_cast<const floatx4*>(wr + 4 * c);
     const float* bT = baseT + 4 * c;
     // centred row, 1/std and log2-domain score of one position's x (8-lane group sums)
-    auto row = [&](float4 x, float4& d, float& rstd, float& sc) {
+    auto row = [&](floatx4 x, floatx4& d, float& rstd, float& sc) {
         const float mean = dpp_sum8((x.x + x.y) + (x.z + x.w)) * (1.0f / kE);
-        d = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+        d.lo = x.lo - splat2(mean);
+        d.hi = x.hi - splat2(mean);
         float vv = d.x * d.x;
         vv = fmaf(d.y, d.y, vv);
         vv = fmaf(d.z, d.z, vv);
@@ -364,25 +389,28 @@ __device__ inline float4 attend_l0(const float2* __restrict__ tok, const float* 
         sc = (rstd * dg) * scale2;
     };
     float m = -1e30f, l = 0.f;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int base = 0; base < pos; base += 8 * kRows) {
-        float2 tk[kRows];
-        float4 wp[kRows];
+    f2 alo = {0.f, 0.f}, ahi = {0.f, 0.f};
+    // one chunk of 8 * R positions
+    auto chunk = [&](int base, auto nrc) {
+        constexpr int R = decltype(nrc)::value;
+        float2 tk[R];
+        floatx4 wp[R];
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {  // past the end: re-read position pos-1, masked below
+        for (int r = 0; r < R; ++r) {  // past the end: re-read position pos-1, masked below
             const int p = min(base + 8 * r + g, pos - 1);
             tk[r] = tok[p];
-            wp[r] = *reinterpret_cast<const float4*>(wpe + (size_t)p * kE + 4 * c);
+            wp[r] = *reinterpret_cast<const floatx4*>(wpe + (size_t)p * kE + 4 * c);
         }
-        float4 d[kRows];
-        float rs[kRows], s[kRows];
+        floatx4 d[R];
+        float rs[R], s[R];
         float mx = -1e30f;
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            const float4 b4 = *reinterpret_cast<const float4*>(bT + __float_as_int(tk[r].x));
-            const float rr = tk[r].y;
-            const float4 x = make_float4(fmaf(rr, wr4.x, b4.x) + wp[r].x, fmaf(rr, wr4.y, b4.y) + wp[r].y,
-                                         fmaf(rr, wr4.z, b4.z) + wp[r].z, fmaf(rr, wr4.w, b4.w) + wp[r].w);
+        for (int r = 0; r < R; ++r) {
+            const floatx4 b4 = *reinterpret_cast<const floatx4*>(bT + __float_as_int(tk[r].x));
+            const f2 rr = splat2(tk[r].y);
+            floatx4 x;
+            x.lo = pk_fma(rr, wr4.lo, b4.lo) + wp[r].lo;
+            x.hi = pk_fma(rr, wr4.hi, b4.hi) + wp[r].hi;
             row(x, d[r], rs[r], s[r]);
             s[r] = (base + 8 * r + g < pos) ? s[r] : -INFINITY;
             mx = fmaxf(mx, s[r]);
@@ -390,33 +418,35 @@ __device__ inline float4 attend_l0(const float2* __restrict__ tok, const float* 
         const float mn = fmaxf(m, mx);
         const float corr = __builtin_amdgcn_exp2f(m - mn);
         l *= corr;
-        acc.x *= corr; acc.y *= corr; acc.z *= corr; acc.w *= corr;
+        alo *= splat2(corr);
+        ahi *= splat2(corr);
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
+        for (int r = 0; r < R; ++r) {
             const float pr = __builtin_amdgcn_exp2f(s[r] - mn);
             l += pr;
-            const float w = pr * rs[r];
-            acc.x = fmaf(w, d[r].x, acc.x);
-            acc.y = fmaf(w, d[r].y, acc.y);
-            acc.z = fmaf(w, d[r].z, acc.z);
-            acc.w = fmaf(w, d[r].w, acc.w);
+            const f2 w = splat2(pr * rs[r]);
+            alo = pk_fma(w, d[r].lo, alo);
+            ahi = pk_fma(w, d[r].hi, ahi);
         }
         m = mn;
-    }
+    };
+    int base = 0;
+#pragma unroll 1
+    for (const int pe = pos & ~(8 * kRows - 1); base < pe; base += 8 * kRows)
+        chunk(base, std::integral_constant<int, kRows>{});
+    if (base < pos) tail_rows<kRows>(pos - base, [&](auto nrc) { chunk(base, nrc); });
     {   // the current position (group 0 merges it; all lanes run the group sums)
-        float4 dc;
+        floatx4 dc;
         float rc, sc;
-        row(*reinterpret_cast<const float4*>(xcur + 4 * c), dc, rc, sc);
+        row(*reinterpret_cast<const floatx4*>(xcur + 4 * c), dc, rc, sc);
         if (g == 0) {
             const float mn = fmaxf(m, sc);
             const float corr = __builtin_amdgcn_exp2f(m - mn);
             const float pr = __builtin_amdgcn_exp2f(sc - mn);
-            const float w = pr * rc;
+            const f2 w = splat2(pr * rc);
             l = l * corr + pr;
-            acc.x = fmaf(w, dc.x, acc.x * corr);
-            acc.y = fmaf(w, dc.y, acc.y * corr);
-            acc.z = fmaf(w, dc.z, acc.z * corr);
-            acc.w = fmaf(w, dc.w, acc.w * corr);
+            alo = pk_fma(w, dc.lo, alo * splat2(corr));
+            ahi = pk_fma(w, dc.hi, ahi * splat2(corr));
             m = mn;
         }
     }
@@ -425,22 +455,20 @@ __device__ inline float4 attend_l0(const float2* __restrict__ tok, const float* 
         auto xch = [&](float v) { return off == 8 ? dpp_xor8(v) : __shfl_xor(v, off); };
         const float mo = xch(m);
         const float lo = xch(l);
-        const float ax = xch(acc.x), ay = xch(acc.y);
-        const float az = xch(acc.z), aw = xch(acc.w);
+        const f2 olo = {xch(alo.x), xch(alo.y)};
+        const f2 ohi = {xch(ahi.x), xch(ahi.y)};
         const float mn = fmaxf(m, mo);
         const float sa = __builtin_amdgcn_exp2f(m - mn), sb = __builtin_amdgcn_exp2f(mo - mn);
         l = l * sa + lo * sb;
-        acc.x = acc.x * sa + ax * sb;
-        acc.y = acc.y * sa + ay * sb;
-        acc.z = acc.z * sa + az * sb;
-        acc.w = acc.w * sa + aw * sb;
+        alo = alo * splat2(sa) + olo * splat2(sb);
+        ahi = ahi * splat2(sa) + ohi * splat2(sb);
         m = mn;
     }
     // sum_p P_p y_p = g * (sum_p P_p rstd_p d_p) + b   (sum_p P_p = 1); every lane holds dims 4c..4c+3
-    const float inv = 1.0f / l;
-    const float4 b4 = *reinterpret_cast<const float4*>(lnb + 4 * c);
-    const float4 res = make_float4(fmaf(g4.x, acc.x * inv, b4.x), fmaf(g4.y, acc.y * inv, b4.y),
-                                   fmaf(g4.z, acc.z * inv, b4.z), fmaf(g4.w, acc.w * inv, b4.w));
+    const f2 inv = splat2(1.0f / l);
+    const floatx4 b4 = *reinterpret_cast<const floatx4*>(lnb + 4 * c);
+    const f2 rlo = pk_fma(g4.lo, alo * inv, b4.lo), rhi = pk_fma(g4.hi, ahi * inv, b4.hi);
+    const float4 res = make_float4(rlo.x, rlo.y, rhi.x, rhi.y);
     if (o && lane < 8) *reinterpret_cast<float4*>(o + 4 * c) = res;
     return res;
 }
@@ -455,19 +483,18 @@ __device__ inline void proj_ln_task(float4 o4, const float* Wvp, const float* bv
                                     const float* lnb, float* xrow, float* xnrow, int lane) {
     const int c = lane & 7, g = lane >> 3;
     const float ov[4] = {o4.x, o4.y, o4.z, o4.w};
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    f2 alo = {0.f, 0.f}, ahi = {0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const float4 w = *reinterpret_cast<const float4*>(Wvp + (4 * c + i) * kE + 4 * g);
-        acc.x = fmaf(ov[i], w.x, acc.x);
-        acc.y = fmaf(ov[i], w.y, acc.y);
-        acc.z = fmaf(ov[i], w.z, acc.z);
-        acc.w = fmaf(ov[i], w.w, acc.w);
+        const floatx4 w = *reinterpret_cast<const floatx4*>(Wvp + (4 * c + i) * kE + 4 * g);
+        alo = pk_fma(splat2(ov[i]), w.lo, alo);
+        ahi = pk_fma(splat2(ov[i]), w.hi, ahi);
     }
-    acc.x = dpp_sum8(acc.x);
-    acc.y = dpp_sum8(acc.y);
-    acc.z = dpp_sum8(acc.z);
-    acc.w = dpp_sum8(acc.w);
+    float4 acc;
+    acc.x = dpp_sum8(alo.x);
+    acc.y = dpp_sum8(alo.y);
+    acc.z = dpp_sum8(ahi.x);
+    acc.w = dpp_sum8(ahi.y);
     const float4 bv = *reinterpret_cast<const float4*>(bvp + 4 * g);
     const float4 xv = *reinterpret_cast<const float4*>(xrow + 4 * g);
     const float x0 = (acc.x + bv.x) + xv.x, x1 = (acc.y + bv.y) + xv.y;

@@ -25,9 +25,9 @@ m = dpt_hip.DeviceModel(sd, 4, 1, 5, 2004)
 N = 4096
 means = torch.from_numpy(np.random.RandomState(1).uniform(0, 1, (N, 5))).cuda()
 res = {}
-for tile in (16, 8):
+for tile in [int(t) for t in os.environ.get("ST_TILES", "16,8").split(",")]:
     dpt_hip.set_decode_tile(tile)
-    for H in (64, 500):
+    for H in [int(h) for h in os.environ.get("ST_H", "64,500").split(",")]:
         m.rollout_bandit(means, H, 0.3, True, seed=0)
         torch.cuda.synchronize()
         lib.dpt_debug_stamps(None, 0, 1)
