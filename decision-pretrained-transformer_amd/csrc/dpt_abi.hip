@@ -61,6 +61,7 @@ int launch_prefill(const ModelView&, const float*, const float*, const float*, c
 int set_decode_tile(int);
 int set_darkroom_memo(int);
 int set_cache_budget(int64_t);
+int set_block0_mfma(int);
 
 }  // namespace dpt
 
@@ -123,6 +124,10 @@ int dpt_tuning_set(int32_t key, int64_t value) {
     if (key == DPT_TUNE_CACHE_BUDGET) {
         REQUIRE(set_cache_budget(value) == DPT_OK, "cache budget %lld B: >= 0", (long long)value);
         return DPT_OK;
+    }
+    if (key == DPT_TUNE_BLOCK0_MFMA) {
+        REQUIRE(value == 0 || value == 1, "block-0 MFMA %lld: 0 or 1", (long long)value);
+        return set_block0_mfma((int)value);
     }
     set_error(DPT_EINVAL, "unknown tuning key %d", key);
     return DPT_EINVAL;

@@ -61,6 +61,18 @@ constexpr int kRows = 4;                  // K/V rows (of 8 positions) in flight
 #endif
 constexpr int kYRows = DPT_YROWS;         // y rows in flight per wave (rollout blocks >= 1; 8: -1.5 % vs 4)
 constexpr int kChunks = kFF / 16;         // hidden-unit chunks of the fused c_fc -> mlp.c_proj
+// timing-only diagnostics (wrong results; never in the shipped library): drop the
+// cached positions of block 0's attention or of the y streams
+#ifdef DPT_EXP_NOL0
+#define DPT_EXP_L0POS(p) 0
+#else
+#define DPT_EXP_L0POS(p) (p)
+#endif
+#ifdef DPT_EXP_NOSTREAM
+#define DPT_EXP_YPOS(p) 0
+#else
+#define DPT_EXP_YPOS(p) (p)
+#endif
 #ifndef DPT_DEFAULT_CACHE_BUDGET
 #define DPT_DEFAULT_CACHE_BUDGET (224ll << 20)
 #endif
@@ -116,8 +128,10 @@ __host__ inline size_t decode_smem_bytes(const ModelView& M) {
 // for k < A and base[A] = w_s + emb_b (the query token), then g0 and bvp of
 // every layer (kE floats per layer each) and the folded matrices Wvp and G.
 struct RolloutLDS {
-    int means, base, g0, bvp, wvp, G, total;
-    __host__ __device__ static RolloutLDS make(int A, int L, bool with_G = true) {
+    int means, base, g0, bvp, wvp, G, gx, gx0, total;
+    // l0m: block 0 on the matrix cores (l0_tiles) -- its extra u-projection columns
+    // gx [E][16] (alpha, gamma, beta[0..A] of l0_tiles as linear maps of xn) and gx0 [16]
+    __host__ __device__ static RolloutLDS make(int A, int L, bool with_G = true, bool l0m = false) {
         RolloutLDS r;
         r.means = 0;               // the tile's arm means, double [kM][A]
         r.base = 2 * kM * A;
@@ -125,13 +139,15 @@ struct RolloutLDS {
         r.bvp = r.g0 + L * kE;
         r.wvp = r.bvp + L * kE;  // Wv Wproj of every layer (c_proj's B operand, read from LDS)
         r.G = r.wvp + L * kE * kE;  // Wq Wk^T of every layer (the u projection's B operand)
-        r.total = r.G + (with_G ? L * kE * kE : 0);
+        r.gx = r.G + (with_G ? L * kE * kE : 0);
+        r.gx0 = r.gx + kE * 16;
+        r.total = l0m ? r.gx0 + 16 : r.gx;
         return r;
     }
 };
 
-__host__ inline size_t rollout_smem_bytes(const ModelView& M, bool with_G) {
-    return decode_smem_bytes(M) + sizeof(float) * (size_t)RolloutLDS::make(M.A, M.n_layer, with_G).total;
+__host__ inline size_t rollout_smem_bytes(const ModelView& M, bool with_G, bool l0m = false) {
+    return decode_smem_bytes(M) + sizeof(float) * (size_t)RolloutLDS::make(M.A, M.n_layer, with_G, l0m).total;
 }
 
 template <int NT>
@@ -188,7 +204,7 @@ __device__ inline float dpp_xor8(float d) {
 
 // LayerNorm of one 32-wide row held by the 32 lanes of a half-wave: the two
 // row sums are 16-lane DPP reductions plus one xor-16 exchange.
-__device__ inline float ln_halfwave(float v, float g, float b) {
+__device__ inline float ln_halfwave(float v, float g, float b, float* mean_out = nullptr, float* rstd_out = nullptr) {
     float s = dpp_sum16(v);
     s += __shfl_xor(s, 16, 32);
     const float mean = s * (1.0f / kE);
@@ -196,6 +212,10 @@ __device__ inline float ln_halfwave(float v, float g, float b) {
     float s2 = dpp_sum16(d * d);
     s2 += __shfl_xor(s2, 16, 32);
     const float rstd = __builtin_amdgcn_rsqf(s2 * (1.0f / kE) + 1e-5f);
+    if (mean_out) {
+        *mean_out = mean;
+        *rstd_out = rstd;
+    }
     return fmaf(d * rstd, g, b);
 }
 
@@ -351,16 +371,16 @@ __device__ __attribute__((always_inline)) inline float4 attend_one(const float* 
 
 // Block-0 attention of one bandit task (one wave) without a K/V cache.  Every
 // bandit context token is [1, onehot(a), 1, r], so block 0's input at position p
-// is x_p = fma(r_p, w_r, base[a_p]) + wpe[p], rebuilt from the 8-byte (a_p, r_p)
-// record instead of streaming 256 B of K and V.  With y_p = LN1(x_p) =
+// is x_p = fma(r_p, w_r, base[a_p]) + wpe[p], rebuilt from the token record
+// (a_p, r_p, ...; TokRec) instead of streaming 256 B of K and V.  With y_p = LN1(x_p) =
 // rstd_p d_p * g + b (d_p = x_p - mean_p):
 //   q . k_p = y_p . (Wk q) + const = rstd_p d_p . (g * u) + const'   (u = Wk q)
 //   sum_p P_p v_p = (sum_p P_p y_p) Wv + bv
 // The constants shift every score alike and cancel in the softmax; Wv, bv are
 // folded into c_proj (L0Off::Wvp, bvp).  Writes o = sum_p P_p y_p.  The current
-// position's x is xcur (the residual row, before attention).  A record is
-// (a_p * E as int bits, r_p); scores are kept in the log2 domain (v_exp_f32).
-__device__ __attribute__((always_inline)) inline float4 attend_l0(const float2* __restrict__ tok, const float* __restrict__ wpe, int pos,
+// position's x is xcur (the residual row, before attention).  Scores are kept in
+// the log2 domain (v_exp_f32).
+__device__ __attribute__((always_inline)) inline float4 attend_l0(const float4* __restrict__ tok, const float* __restrict__ wpe, int pos,
                                  const float* u, const float* xcur, const float* baseT, const float* wr,
                                  const float* lng, const float* lnb, float* o, int lane) {
     const int g = lane >> 3, c = lane & 7;
@@ -398,7 +418,8 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float2* 
 #pragma unroll
         for (int r = 0; r < R; ++r) {  // past the end: re-read position pos-1, masked below
             const int p = min(base + 8 * r + g, pos - 1);
-            tk[r] = tok[p];
+            const float4 rec = tok[p];
+            tk[r] = make_float2(rec.x, rec.y);
             wp[r] = *reinterpret_cast<const floatx4*>(wpe + (size_t)p * kE + 4 * c);
         }
         floatx4 d[R];
@@ -406,7 +427,7 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float2* 
         float mx = -1e30f;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const floatx4 b4 = *reinterpret_cast<const floatx4*>(bT + __float_as_int(tk[r].x));
+            const floatx4 b4 = *reinterpret_cast<const floatx4*>(bT + __float_as_int(tk[r].x) * kE);
             const f2 rr = splat2(tk[r].y);
             floatx4 x;
             x.lo = pk_fma(rr, wr4.lo, b4.lo) + wp[r].lo;
@@ -471,6 +492,206 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float2* 
     const float4 res = make_float4(rlo.x, rlo.y, rhi.x, rhi.y);
     if (o && lane < 8) *reinterpret_cast<float4*>(o + 4 * c) = res;
     return res;
+}
+
+// Block-0 attention of a whole tile on the matrix cores (L0M: tile of 8 tasks, NA =
+// A + 1 token kinds).  With TokRec (a_p, r_p, mean_p, rstd_p), gu = g * u and
+// x_p = r_p w_r + base[a_p] + wpe[p] (attend_l0):
+//   score_p = rstd_p ((x_p - mean_p) . gu) = rstd_p (r_p alpha + beta[a_p] + wpe[p] . gu - mean_p gamma)
+//   sum_p w_p (x_p - mean_p) = (sum w r) w_r + sum_k (sum_{a_p = k} w_p) base[k] + sum_p w_p wpe[p] - (sum w mean) 1
+// with alpha = w_r . gu, beta[k] = base[k] . gu, gamma = sum gu (per task and step: the
+// u projection's extra columns, kept in S.vcur) and w_p = P_p rstd_p.  The only
+// per-position vector terms involve wpe, which every task shares: the scores are one
+// [16 positions x 32] x [32 x 16 tasks] MFMA product per 16-position tile and the
+// weighted wpe sum one [32 x 16 positions] x [16 x 16 tasks] product; everything else
+// is per-(position, task) scalar work, one element per lane and register.  Wave w
+// takes the tiles w, w + 8, ...; its partial softmax state per task (m, l, the scalar
+// sums, the arm sums and the wpe sum) goes to part[w][task][48] for l0_merge.
+template <int NA>
+__device__ __attribute__((always_inline)) inline void l0_tiles(const float* __restrict__ rec_base, size_t task_stride,
+                                                               int ntask, int pos, const float* __restrict__ wpe,
+                                                               const float* q, const float* cst, const float* lng,
+                                                               float* part, int wave, int lane) {
+    const int n = lane & 15, j = lane >> 4;
+    const bool tv = n < ntask;  // lanes of columns >= the tile's live tasks carry zeros
+    const float scale2 = 0.17677669529663687f * 1.4426950408889634f;  // 32 ** -0.5 * log2(e)
+    // B operand of the score product: gu[task n][dim 8j + s] (k-step s takes dims {8j + s})
+    float gb[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) gb[s] = tv ? lng[8 * j + s] * q[n * kE + 8 * j + s] : 0.f;
+    const float* cn = cst + (tv ? n : 0) * kE;
+    const float alpha = cn[0], gamma = cn[1];
+    const float4* rec = reinterpret_cast<const float4*>(rec_base + (size_t)(tv ? n : 0) * task_stride);
+    float m = -1e30f, l = 0.f, sr = 0.f, sm = 0.f;
+    float W[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) W[k] = 0.f;
+    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0;
+#pragma unroll 1
+    for (int p0 = 16 * wave; p0 < pos; p0 += 16 * 8) {
+        // scores: D[position p0 + 4j + r][task n] = wpe[p] . gu_n
+        const float* wrow = wpe + (size_t)min(p0 + n, pos - 1) * kE + 8 * j;
+        const floatx4 wa0 = *reinterpret_cast<const floatx4*>(wrow);
+        const floatx4 wa1 = *reinterpret_cast<const floatx4*>(wrow + 4);
+        floatx4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa0[s], gb[s], sacc, 0, 0, 0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa1[s], gb[4 + s], sacc, 0, 0, 0);
+        float sc[4], rr[4], mu[4], rs[4];
+        int ak[4];
+        float mx = -1e30f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int p = p0 + 4 * j + r;
+            const float4 R = rec[min(p, pos - 1)];
+            ak[r] = __float_as_int(R.x);
+            rr[r] = R.y;
+            mu[r] = R.z;
+            rs[r] = R.w;
+            float t = fmaf(rr[r], alpha, cn[2 + ak[r]]) + sacc[r];
+            t = fmaf(-mu[r], gamma, t);
+            sc[r] = (tv && p < pos) ? (rs[r] * t) * scale2 : -INFINITY;
+            mx = fmaxf(mx, sc[r]);
+        }
+        // one running max per task: over the 4 lane groups holding its positions
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mn = fmaxf(m, mx);
+        const float corr = __builtin_amdgcn_exp2f(m - mn);
+        l *= corr;
+        sr *= corr;
+        sm *= corr;
+#pragma unroll
+        for (int k = 0; k < NA; ++k) W[k] *= corr;
+        o0 *= corr;
+        o1 *= corr;
+        m = mn;
+        float wv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float pr = __builtin_amdgcn_exp2f(sc[r] - mn);
+            l += pr;
+            const float w = pr * rs[r];
+            wv[r] = w;
+            sr = fmaf(w, rr[r], sr);
+            sm = fmaf(w, mu[r], sm);
+#pragma unroll
+            for (int k = 0; k < NA; ++k) W[k] += (ak[r] == k) ? w : 0.f;
+        }
+        // D2[dim 16 dt + 4j + i][task n] += sum over the tile's positions of wpe[p][dim] w[p][n]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float* wr = wpe + (size_t)min(p0 + 4 * j + r, pos - 1) * kE + n;
+            o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[0], wv[r], o0, 0, 0, 0);
+            o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[16], wv[r], o1, 0, 0, 0);
+        }
+    }
+    // the scalar sums over the 4 lane groups of each task
+    auto red = [](float v) {
+        v += __shfl_xor(v, 16);
+        return v + __shfl_xor(v, 32);
+    };
+    l = red(l);
+    sr = red(sr);
+    sm = red(sm);
+#pragma unroll
+    for (int k = 0; k < NA; ++k) W[k] = red(W[k]);
+    if (n < 8) {
+        float* pp = part + (wave * 8 + n) * 48;
+        *reinterpret_cast<floatx4*>(pp + 4 * j) = o0;
+        *reinterpret_cast<floatx4*>(pp + 16 + 4 * j) = o1;
+        if (j == 0) {
+            pp[32] = m;
+            pp[33] = l;
+            pp[34] = sr;
+            pp[35] = sm;
+#pragma unroll
+            for (int k = 0; k < NA; ++k) pp[36 + k] = W[k];
+        }
+    }
+}
+
+// Combines the 8 waves' l0_tiles partials of one task (one wave, lane (g, c) forms
+// dims 4c..4c+3), adds the current position (its x is xcur) and returns
+// o = g * (sum_p P_p rstd_p (x_p - mean_p)) + b, as attend_l0.
+template <int NA>
+__device__ __attribute__((always_inline)) inline float4 l0_merge(const float* part, int t, const float* u,
+                                                                 const float* xcur, const float* baseT,
+                                                                 const float* wr, const float* lng, const float* lnb,
+                                                                 int lane) {
+    const int g = lane >> 3, c = lane & 7;
+    const float scale2 = 0.17677669529663687f * 1.4426950408889634f;
+    float mw[8];
+    float M = -1e30f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        mw[w] = part[(w * 8 + t) * 48 + 32];
+        M = fmaxf(M, mw[w]);
+    }
+    float L = 0.f, SR = 0.f, SM = 0.f;
+    float Wk[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) Wk[k] = 0.f;
+    f2 olo = {0.f, 0.f}, ohi = {0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const float* pp = part + (w * 8 + t) * 48;
+        const float sw = __builtin_amdgcn_exp2f(mw[w] - M);
+        L = fmaf(sw, pp[33], L);
+        SR = fmaf(sw, pp[34], SR);
+        SM = fmaf(sw, pp[35], SM);
+#pragma unroll
+        for (int k = 0; k < NA; ++k) Wk[k] = fmaf(sw, pp[36 + k], Wk[k]);
+        const floatx4 o4 = *reinterpret_cast<const floatx4*>(pp + 4 * c);
+        olo = pk_fma(splat2(sw), o4.lo, olo);
+        ohi = pk_fma(splat2(sw), o4.hi, ohi);
+    }
+    // V = sum_p w_p (x_p - mean_p) over the cached positions, dims 4c..4c+3
+    const floatx4 wr4 = *reinterpret_cast<const floatx4*>(wr + 4 * c);
+    olo = pk_fma(splat2(SR), wr4.lo, olo);
+    ohi = pk_fma(splat2(SR), wr4.hi, ohi);
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        const floatx4 b4 = *reinterpret_cast<const floatx4*>(baseT + k * kE + 4 * c);
+        olo = pk_fma(splat2(Wk[k]), b4.lo, olo);
+        ohi = pk_fma(splat2(Wk[k]), b4.hi, ohi);
+    }
+    olo -= splat2(SM);
+    ohi -= splat2(SM);
+    // the current position (every lane computes it; its group sums are 8-lane DPP)
+    const floatx4 u4 = *reinterpret_cast<const floatx4*>(u + 4 * c);
+    const floatx4 g4 = *reinterpret_cast<const floatx4*>(lng + 4 * c);
+    const floatx4 gu = g4 * u4;
+    const floatx4 x = *reinterpret_cast<const floatx4*>(xcur + 4 * c);
+    const float mean = dpp_sum8((x.x + x.y) + (x.z + x.w)) * (1.0f / kE);
+    floatx4 d;
+    d.lo = x.lo - splat2(mean);
+    d.hi = x.hi - splat2(mean);
+    float vv = d.x * d.x;
+    vv = fmaf(d.y, d.y, vv);
+    vv = fmaf(d.z, d.z, vv);
+    vv = fmaf(d.w, d.w, vv);
+    float dg = d.x * gu.x;
+    dg = fmaf(d.y, gu.y, dg);
+    dg = fmaf(d.z, gu.z, dg);
+    dg = fmaf(d.w, gu.w, dg);
+    vv = dpp_sum8(vv);
+    dg = dpp_sum8(dg);
+    const float rc = __builtin_amdgcn_rsqf(vv * (1.0f / kE) + 1e-5f);
+    const float sc = (rc * dg) * scale2;
+    const float mn = fmaxf(M, sc);
+    const float corr = __builtin_amdgcn_exp2f(M - mn);
+    const float pr = __builtin_amdgcn_exp2f(sc - mn);
+    L = L * corr + pr;
+    const f2 wc = splat2(pr * rc);
+    olo = pk_fma(wc, d.lo, olo * splat2(corr));
+    ohi = pk_fma(wc, d.hi, ohi * splat2(corr));
+    const f2 inv = splat2(1.0f / L);
+    const floatx4 b4 = *reinterpret_cast<const floatx4*>(lnb + 4 * c);
+    const f2 rlo = pk_fma(g4.lo, olo * inv, b4.lo), rhi = pk_fma(g4.hi, ohi * inv, b4.hi);
+    (void)g;
+    return make_float4(rlo.x, rlo.y, rhi.x, rhi.y);
 }
 
 // The rollout's c_proj + residual + ln_2 for one task inside its attention wave (no
@@ -539,7 +760,9 @@ __device__ inline void zero_smem(Smem& S) {
 // position, layer l's K slot) instead of K and V (256 B): q . k_p = y_p . u +
 // const with u = Wk q = xn G + g0, and sum_p P_p v_p = (sum_p P_p y_p) Wv + bv, so
 // the same y stream serves as keys and values.  D is the RolloutLDS block.
-template <int TILE, bool L0R = false, bool GL = false>
+// L0M (bandit rollout, tile 8): block 0's attention on the matrix cores for NA = L0M
+// token kinds (l0_tiles + l0_merge) instead of one wave per task (attend_l0).
+template <int TILE, bool L0R = false, bool GL = false, int L0M = 0>
 __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, const ModelView& M,
                                 float* __restrict__ kv, int N, int max_pos, int tile0, int pos, float wpe_j,
                                 const float* D = nullptr, int pin = 0, int pin_x = 0) {
@@ -561,7 +784,11 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         for (int f = 0; f < M.F; ++f) acc = fmaf(S.tok[t][f], P[pl.emb_w + f * kE + j], acc);
         const float x = (acc + P[pl.emb_b + j]) + wpe_j;
         S.x[t][j] = x;
-        S.xn[t][j] = ln_halfwave(x, P[pl.layers + PLay::ln1_g + j], P[pl.layers + PLay::ln1_b + j]);
+        float mean, rstd;
+        S.xn[t][j] = ln_halfwave(x, P[pl.layers + PLay::ln1_g + j], P[pl.layers + PLay::ln1_b + j], &mean, &rstd);
+        const int task = tile0 + t;
+        if (L0R && j == 0 && task < N)  // the LayerNorm statistics of this position's TokRec
+            *reinterpret_cast<float2*>(kv + (size_t)task * max_pos * kE + 4 * pos + 2) = make_float2(mean, rstd);
     }
     bar_lds();
     DPT_STAMP(0);
@@ -594,6 +821,20 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 for (int r = 0; r < 4; ++r) {
                     const int t = kq * 4 + r;
                     if (t < TILE) S.q[t][col] = acc[r] + bias;
+                }
+            } else if (L0M && li == 0 && wave == 2) {
+                // l0_tiles' per-task constants (alpha, gamma, beta[k]) = xn gx + gx0 -> S.vcur
+                const RolloutLDS rl = RolloutLDS::make(M.A, M.n_layer, GL, true);
+                floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(S.xn[i16][4 * s + kq], D[rl.gx + (4 * s + kq) * 16 + i16],
+                                                               acc, 0, 0, 0);
+                const float bias = D[rl.gx0 + i16];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int t = kq * 4 + r;
+                    if (t < TILE) S.vcur[t][i16] = acc[r] + bias;
                 }
             }
         } else if (wave < 6) {
@@ -631,6 +872,14 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         }
         bar_lds();
         DPT_STAMP(1);
+        if constexpr (L0M > 0) {
+            if (li == 0) {  // block 0: every wave takes a share of the tile's cached positions
+                l0_tiles<L0M>(kv + (size_t)tile0 * max_pos * kE, (size_t)max_pos * kE, min(TILE, N - tile0),
+                              DPT_EXP_L0POS(pos), M.wpe, &S.q[0][0], &S.vcur[0][0], PL + PLay::ln1_g,
+                              &S.part[0][0][0], wave, lane);
+                bar_lds();
+            }
+        }
         // the streaming phase yields issue slots to the other workgroup's latency-bound dense
         // phases (s_setprio; -0.5 % at config 2, -1 % on the linear config)
         if (L0R) __builtin_amdgcn_s_setprio(0);
@@ -643,11 +892,14 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 if (L0R) {
                     const RolloutLDS rl = RolloutLDS::make(M.A, M.n_layer);
                     const float4 o4 =
-                        l0 ? attend_l0(reinterpret_cast<const float2*>(kc), M.wpe, pos, S.q[wave], S.x[wave],
+                        (L0M > 0 && l0) ? l0_merge<(L0M > 0 ? L0M : 1)>(&S.part[0][0][0], wave, S.q[wave], S.x[wave], D + rl.base,
+                                                             P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
+                                                             PL + PLay::ln1_b, lane)
+                        : l0 ? attend_l0(reinterpret_cast<const float4*>(kc), M.wpe, DPT_EXP_L0POS(pos), S.q[wave], S.x[wave],
                                        D + rl.base, P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
                                        PL + PLay::ln1_b, nullptr, lane)
                            // scores y_p . u, output sum_p P_p y_p; y_pos is in S.kcur
-                           : attend_one<true, kYRows>(kc, kc, pos, S.q[wave], S.kcur[wave], S.kcur[wave], nullptr,
+                           : attend_one<true, kYRows>(kc, kc, DPT_EXP_YPOS(pos), S.q[wave], S.kcur[wave], S.kcur[wave], nullptr,
                                                       lane, lpin(li));
                     // c_proj (folded Wvp) + residual + ln_2 of this task, in this wave
                     proj_ln_task(o4, D + rl.wvp + li * kE * kE, D + rl.bvp + li * kE, PL + PLay::ln2_g,
@@ -865,6 +1117,10 @@ __global__ __launch_bounds__(TILE * 64, 4) void window_decode_kernel(
     }
 }
 
+// TokRec: the rollout's record of one bandit token, 16 B per position, packed at
+// the start of each task's block-0 K slot: (a_p as int bits, float(r_p)) written
+// after the selection that chose them, (mean_p, rstd_p) of ln_1 of block 0 written
+// by the embedding phase of position p.  Position 0 is the query: (A, 0).
 struct BanditRolloutParams {
     int N, H, A, type, sample, n_layer;
     // y rows of positions < pin (+ 8 kYRows for blocks 1..pin_x) use the default cache
@@ -928,15 +1184,15 @@ __device__ inline int select_rollout(const float* logits, int A, int sample, dou
 
 // The bandit online loop (evals/eval_bandit.py:70-89) for one tile of tasks,
 // all H steps: decode -> select -> env step -> append transition.
-template <int TILE, bool GL>
+template <int TILE, bool GL, int L0M = 0>
 __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView M, BanditRolloutParams Pr) {
     DPT_SMEM_SETUP(TILE)
     const int tile0 = blockIdx.x * TILE;
     const int tid = threadIdx.x;
     const int A = Pr.A;
-    // block 0 runs K/V-free (attend_l0): token embedding table and folded weights in LDS
+    // block 0 runs K/V-free (attend_l0 / l0_tiles): token embedding table and folded weights in LDS
     float* D = P + pl.total;
-    const RolloutLDS rl = RolloutLDS::make(A, M.n_layer, GL);
+    const RolloutLDS rl = RolloutLDS::make(A, M.n_layer, GL, L0M > 0);
     double* means = reinterpret_cast<double*>(D + rl.means);
     for (int i = tid; i < TILE * A; i += TILE * 64) {
         const int t = i / A, k = i % A;
@@ -959,14 +1215,35 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         D[rl.wvp + i] = M.l0[(size_t)li * L0Off::size + L0Off::Wvp + j];
         if (GL) D[rl.G + i] = M.l0[(size_t)li * L0Off::size + L0Off::G + j];
     }
-    // per task, block 0's K slot holds the (a_p, r_p) record of every position
+    if constexpr (L0M > 0) {
+        // l0_tiles' constants as maps of xn: column c of gx is G v_c and gx0[c] = g0 . v_c for
+        // v_0 = g * w_r (alpha), v_1 = g (gamma), v_{2+k} = g * base[k] (beta[k]); fp64 sums
+        __syncthreads();  // base[] complete
+        const float* g = P + pl.layers + PLay::ln1_g;
+        const float* wr = P + pl.emb_w + (2 + A) * kE;
+        auto v = [&](int c, int jj) -> double {
+            if (c == 0) return (double)g[jj] * wr[jj];
+            if (c == 1) return (double)g[jj];
+            if (c < 2 + L0M) return (double)g[jj] * D[rl.base + (c - 2) * kE + jj];
+            return 0.0;
+        };
+        const float* G0 = M.l0 + L0Off::G;
+        const float* g00 = M.l0 + L0Off::g0;
+        for (int i = tid; i < (kE + 1) * 16; i += TILE * 64) {
+            const int row = i / 16, c = i % 16;
+            double acc = 0.0;
+            for (int jj = 0; jj < kE; ++jj) acc += (row < kE ? (double)G0[row * kE + jj] : (double)g00[jj]) * v(c, jj);
+            D[rl.gx + i] = (float)acc;  // row kE lands in gx0 (= gx + kE * 16)
+        }
+    }
+    // per task, block 0's K slot holds the token record of every position (TokRec)
     auto tokrec = [&](int task) {
         return reinterpret_cast<float2*>(Pr.kv + (size_t)task * Pr.H * kE);
     };
     // position 0: the query token [state=1, 0_A, 0, 0] (BanditEnv.state = [1], ctrl_bandit.py:426)
     if (tid < TILE) {
         S.tok[tid][0] = 1.f;
-        if (tile0 + tid < Pr.N) tokrec(tile0 + tid)[0] = make_float2(__int_as_float(A * kE), 0.f);
+        if (tile0 + tid < Pr.N) tokrec(tile0 + tid)[0] = make_float2(__int_as_float(A), 0.f);
     }
     // this thread's task's (u, g) draw pairs (rollout_draws_kernel), one per step
     const double2* draws = (tid < TILE && tile0 + tid < Pr.N) ? draw_pairs(Pr, tile0 + tid) : nullptr;
@@ -981,7 +1258,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
             const doublex2 d2 = __builtin_nontemporal_load(reinterpret_cast<const doublex2*>(draws + h));
             dr = make_double2(d2[0], d2[1]);
         }
-        decode_position<TILE, true, GL>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D, Pr.pin, Pr.pin_x);
+        decode_position<TILE, true, GL, L0M>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D, Pr.pin, Pr.pin_x);
         // selection + env step; the outputs are stored after the barrier so that it
         // waits only for the y rows (issued phases earlier), not for these stores
         const int t = tid, task = tile0 + t;
@@ -1006,7 +1283,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
             if (Pr.logits_out)  // S.logits is next rewritten by step h+1's head phase
                 for (int k = 0; k < A; ++k) Pr.logits_out[((size_t)h * Pr.N + task) * A + k] = S.logits[t][k];
             // first read from memory by step h+2 (positions < h+2), so it may land during step h+1
-            if (h + 1 < Pr.H) tokrec(task)[h + 1] = make_float2(__int_as_float(a * kE), (float)r);
+            if (h + 1 < Pr.H) tokrec(task)[2 * (h + 1)] = make_float2(__int_as_float(a), (float)r);
         }
         DPT_STAMP(7);
     }
@@ -1090,6 +1367,12 @@ extern "C" int dpt_debug_stamps(unsigned long long* out, int n, int reset) {
 
 static int g_decode_tile = 8;  // tuning knob (dpt_tuning_set(DPT_TUNE_DECODE_TILE, 8|16))
 static int64_t g_cache_budget = DPT_DEFAULT_CACHE_BUDGET;  // DPT_TUNE_CACHE_BUDGET
+static bool g_block0_mfma = true;                          // DPT_TUNE_BLOCK0_MFMA
+
+int set_block0_mfma(int on) {
+    g_block0_mfma = on != 0;
+    return DPT_OK;
+}
 
 int set_cache_budget(int64_t b) {
     if (b < 0) return DPT_EINVAL;
@@ -1178,8 +1461,10 @@ int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, 
     // G in LDS when the block still lets the tile's workgroups share a CU (two at
     // tile 8, one at tile 16); otherwise the u projection reads it from L2
     const size_t per_cu = 160 * 1024 / (g_decode_tile == 8 ? 2 : 1);
-    const bool gl = rollout_smem_bytes(M, true) <= per_cu;
-    sm = rollout_smem_bytes(M, gl);
+    // block 0 on the matrix cores (l0_tiles) for the 5-arm configs at tile 8
+    const bool l0m = g_block0_mfma && g_decode_tile == 8 && a.A == 5;
+    const bool gl = rollout_smem_bytes(M, true, l0m) <= per_cu;
+    sm = rollout_smem_bytes(M, gl, l0m);
     if (sm > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "rollout LDS %zu B > 160 KiB (n_layer=%d, action_dim=%d)", sm, M.n_layer, M.A);
         return DPT_EUNSUPPORTED;
@@ -1202,7 +1487,9 @@ int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, 
         allow_smem(kernel, sm);
         hipLaunchKernelGGL(kernel, dim3((a.N + tile - 1) / tile), dim3(tile * 64), sm, st, M, P);
     };
-    if (g_decode_tile == 8)
+    if (l0m)
+        gl ? launch(rollout_bandit_kernel<8, true, 6>, 8) : launch(rollout_bandit_kernel<8, false, 6>, 8);
+    else if (g_decode_tile == 8)
         gl ? launch(rollout_bandit_kernel<8, true>, 8) : launch(rollout_bandit_kernel<8, false>, 8);
     else
         gl ? launch(rollout_bandit_kernel<16, true>, 16) : launch(rollout_bandit_kernel<16, false>, 16);

@@ -149,6 +149,7 @@ TUNE_DECODE_TILE = 1
 TUNE_PREFILL = 2
 TUNE_DARKROOM_MEMO = 3
 TUNE_CACHE_BUDGET = 4
+TUNE_BLOCK0_MFMA = 5
 SIGNATURES["dpt_tuning_set"] = (_i32, [_i32, _i64])
 
 

@@ -77,11 +77,17 @@ const char* dpt_last_error(void);
  * (stored and streamed with the default cache policy, so they stay resident and
  * are re-read on-die every step; later positions stream non-temporally and do
  * not displace them).  0: every row non-temporal.  Cache policy only: results
- * are bit-identical for any value.  */
+ * are bit-identical for any value.
+ * DPT_TUNE_BLOCK0_MFMA = 1 (default): dpt_rollout_bandit computes block 0's
+ * attention of a tile of 8 five-arm tasks on the matrix cores (the shared
+ * position-embedding terms as MFMA products, the per-token terms as scalars);
+ * 0: one wave per task on the vector ALUs.  Same algebra, different fp32
+ * summation order.  */
 #define DPT_TUNE_DECODE_TILE 1
 #define DPT_TUNE_PREFILL 2
 #define DPT_TUNE_DARKROOM_MEMO 3
 #define DPT_TUNE_CACHE_BUDGET 4
+#define DPT_TUNE_BLOCK0_MFMA 5
 int dpt_tuning_set(int32_t key, int64_t value);
 /* number of visible gfx950 devices (0 on a CPU-only host; never faults) */
 int dpt_device_count(int* count_out_host);

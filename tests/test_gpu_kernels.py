@@ -219,7 +219,8 @@ def test_rollout_large_properties():
 
 
 def test_decode_tiles_bit_identical():
-    """TILE 8 (two workgroups per CU) and TILE 16 give bit-identical rollouts and windows."""
+    """TILE 8 (two workgroups per CU) and TILE 16 give bit-identical rollouts and windows
+    (block 0 on the vector ALUs at both tiles: the matrix-core block 0 is a tile-8 path)."""
     import dpt_hip
     _, m, _ = model_from_golden("bandit5")
     rs = np.random.RandomState(9)
@@ -228,6 +229,7 @@ def test_decode_tiles_bit_identical():
     g, mw, _ = model_from_golden("darkroom")
     q, cs, ca, cn, cr = (g[f"T101/{k}"] for k in ("query", "cs", "ca", "cn", "cr"))
     try:
+        dpt_hip.set_block0_mfma(False)
         for tile in (16, 8):
             dpt_hip.set_decode_tile(tile)
             o = m.rollout_bandit(means, 40, 0.3, True, seed=5, want_logits=True)
@@ -235,10 +237,38 @@ def test_decode_tiles_bit_identical():
             outs.append([o["actions"].cpu().numpy(), o["rewards"].cpu().numpy(), o["logits"].cpu().numpy(),
                          w.cpu().numpy()])
     finally:
-        dpt_hip.set_decode_tile(8)  # the library default
+        dpt_hip.set_decode_tile(8)  # the library defaults
+        dpt_hip.set_block0_mfma(True)
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
     assert_logits(outs[1][3], g["T101/preds_train"])
+
+
+@pytest.mark.parametrize("N,H", [(100, 40), (1000, 130)])
+def test_rollout_block0_mfma_matches_vector_path(N, H):
+    """Block 0 on the matrix cores (l0_tiles / l0_merge, the default at tile 8 and 5 arms) against
+    the one-wave-per-task vector path: same algebra, another fp32 summation order.  Per task, the
+    per-step logits agree within the 1e-5 bar up to the first step whose sampled action differs
+    (a uniform within rounding of a cdf edge), and such divergences are rare."""
+    import dpt_hip
+    _, m, _ = model_from_golden("bandit5")
+    means = np.random.RandomState(13).uniform(0, 1, (N, 5))
+    outs = []
+    try:
+        for on in (False, True):
+            dpt_hip.set_block0_mfma(on)
+            o = m.rollout_bandit(means, H, 0.3, True, seed=17, want_logits=True)
+            outs.append((o["actions"].cpu().numpy(), o["logits"].cpu().numpy()))
+    finally:
+        dpt_hip.set_block0_mfma(True)
+    (a0, l0), (a1, l1) = outs
+    diff = a0 != a1
+    first = np.where(diff.any(1), diff.argmax(1), H)  # first differing step per task
+    assert (first < H).mean() <= 0.01
+    for t in range(N):
+        f = first[t]
+        # logits of steps <= f were computed on identical contexts
+        assert_logits(l1[: f + 1 if f < H else H, t], l0[: f + 1 if f < H else H, t])
 
 
 def test_rollout_cache_budget_bit_identical():
