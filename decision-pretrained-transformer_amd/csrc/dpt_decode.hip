@@ -529,29 +529,40 @@ __device__ __attribute__((always_inline)) inline void l0_tiles(const float* __re
     floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0;
 #pragma unroll 1
     for (int p0 = 16 * wave; p0 < pos; p0 += 16 * 8) {
-        // scores: D[position p0 + 4j + r][task n] = wpe[p] . gu_n
+        // every global load of the tile first (independent; consumed in issue order):
+        // the score operand rows, the 4 token records, the wpe operand of the output product
         const float* wrow = wpe + (size_t)min(p0 + n, pos - 1) * kE + 8 * j;
         const floatx4 wa0 = *reinterpret_cast<const floatx4*>(wrow);
         const floatx4 wa1 = *reinterpret_cast<const floatx4*>(wrow + 4);
-        floatx4 sacc = {0.f, 0.f, 0.f, 0.f};
+        float4 R[4];
+        float wo0[4], wo1[4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa0[s], gb[s], sacc, 0, 0, 0);
+        for (int r = 0; r < 4; ++r) R[r] = rec[min(p0 + 4 * j + r, pos - 1)];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa1[s], gb[4 + s], sacc, 0, 0, 0);
-        float sc[4], rr[4], mu[4], rs[4];
-        int ak[4];
+        for (int r = 0; r < 4; ++r) {
+            const float* wr = wpe + (size_t)min(p0 + 4 * j + r, pos - 1) * kE + n;
+            wo0[r] = wr[0];
+            wo1[r] = wr[16];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // scores: D[position p0 + 4j + r][task n] = wpe[p] . gu_n (two chains of 4)
+        floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = sa;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            sa = __builtin_amdgcn_mfma_f32_16x16x4f32(wa0[s], gb[s], sa, 0, 0, 0);
+            sb = __builtin_amdgcn_mfma_f32_16x16x4f32(wa1[s], gb[4 + s], sb, 0, 0, 0);
+        }
+        float beta[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) beta[r] = cn[2 + __float_as_int(R[r].x)];
+        float sc[4];
         float mx = -1e30f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int p = p0 + 4 * j + r;
-            const float4 R = rec[min(p, pos - 1)];
-            ak[r] = __float_as_int(R.x);
-            rr[r] = R.y;
-            mu[r] = R.z;
-            rs[r] = R.w;
-            float t = fmaf(rr[r], alpha, cn[2 + ak[r]]) + sacc[r];
-            t = fmaf(-mu[r], gamma, t);
-            sc[r] = (tv && p < pos) ? (rs[r] * t) * scale2 : -INFINITY;
+            float t = fmaf(R[r].y, alpha, beta[r]) + (sa[r] + sb[r]);
+            t = fmaf(-R[r].z, gamma, t);
+            sc[r] = (tv && p < pos) ? (R[r].w * t) * scale2 : -INFINITY;
             mx = fmaxf(mx, sc[r]);
         }
         // one running max per task: over the 4 lane groups holding its positions
@@ -572,19 +583,19 @@ __device__ __attribute__((always_inline)) inline void l0_tiles(const float* __re
         for (int r = 0; r < 4; ++r) {
             const float pr = __builtin_amdgcn_exp2f(sc[r] - mn);
             l += pr;
-            const float w = pr * rs[r];
+            const float w = pr * R[r].w;
             wv[r] = w;
-            sr = fmaf(w, rr[r], sr);
-            sm = fmaf(w, mu[r], sm);
+            sr = fmaf(w, R[r].y, sr);
+            sm = fmaf(w, R[r].z, sm);
+            const int ak = __float_as_int(R[r].x);
 #pragma unroll
-            for (int k = 0; k < NA; ++k) W[k] += (ak[r] == k) ? w : 0.f;
+            for (int k = 0; k < NA; ++k) W[k] += (ak == k) ? w : 0.f;
         }
         // D2[dim 16 dt + 4j + i][task n] += sum over the tile's positions of wpe[p][dim] w[p][n]
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const float* wr = wpe + (size_t)min(p0 + 4 * j + r, pos - 1) * kE + n;
-            o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[0], wv[r], o0, 0, 0, 0);
-            o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[16], wv[r], o1, 0, 0, 0);
+            o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wo0[r], wv[r], o0, 0, 0, 0);
+            o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wo1[r], wv[r], o1, 0, 0, 0);
         }
     }
     // the scalar sums over the 4 lane groups of each task
