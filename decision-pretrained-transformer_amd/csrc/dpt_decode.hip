@@ -96,6 +96,11 @@ struct Smem {
     float tok[kM][kMaxF];        // packed token features of the current position
 };
 static_assert(sizeof(Smem) % 16 == 0, "parameter block must start 16-B aligned");
+static_assert(sizeof(Smem::part) >= 8 * 8 * 64 * sizeof(float), "l0_tiles partials (8 waves x 8 tasks x kL0Part) live in part");
+
+// Columns of l0_tiles' per-task constants (alpha, gamma, beta[0..A]): one or two
+// 16-column MFMA tiles of the u phase.
+__host__ __device__ constexpr int l0_cols(int A) { return A + 3 <= 16 ? 16 : 32; }
 
 // Small parameters copied to LDS once per launch (offsets in floats).
 struct PLay {
@@ -130,7 +135,8 @@ __host__ inline size_t decode_smem_bytes(const ModelView& M) {
 struct RolloutLDS {
     int means, base, g0, bvp, wvp, G, gx, gx0, total;
     // l0m: block 0 on the matrix cores (l0_tiles) -- its extra u-projection columns
-    // gx [E][16] (alpha, gamma, beta[0..A] of l0_tiles as linear maps of xn) and gx0 [16]
+    // gx [E][C] (alpha, gamma, beta[0..A] of l0_tiles as linear maps of xn) and gx0 [C],
+    // C = l0_cols(A)
     __host__ __device__ static RolloutLDS make(int A, int L, bool with_G = true, bool l0m = false) {
         RolloutLDS r;
         r.means = 0;               // the tile's arm means, double [kM][A]
@@ -140,8 +146,8 @@ struct RolloutLDS {
         r.wvp = r.bvp + L * kE;  // Wv Wproj of every layer (c_proj's B operand, read from LDS)
         r.G = r.wvp + L * kE * kE;  // Wq Wk^T of every layer (the u projection's B operand)
         r.gx = r.G + (with_G ? L * kE * kE : 0);
-        r.gx0 = r.gx + kE * 16;
-        r.total = l0m ? r.gx0 + 16 : r.gx;
+        r.gx0 = r.gx + kE * l0_cols(A);
+        r.total = l0m ? r.gx0 + l0_cols(A) : r.gx;
         return r;
     }
 };
@@ -411,29 +417,32 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float4* 
     float m = -1e30f, l = 0.f;
     f2 alo = {0.f, 0.f}, ahi = {0.f, 0.f};
     // one chunk of 8 * R positions
+    // one chunk of 8 * R positions; the ln_1 statistics come with the token record
     auto chunk = [&](int base, auto nrc) {
         constexpr int R = decltype(nrc)::value;
-        float2 tk[R];
+        float4 tk[R];
         floatx4 wp[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {  // past the end: re-read position pos-1, masked below
             const int p = min(base + 8 * r + g, pos - 1);
-            const float4 rec = tok[p];
-            tk[r] = make_float2(rec.x, rec.y);
+            tk[r] = tok[p];
             wp[r] = *reinterpret_cast<const floatx4*>(wpe + (size_t)p * kE + 4 * c);
         }
         floatx4 d[R];
-        float rs[R], s[R];
+        float s[R];
         float mx = -1e30f;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const floatx4 b4 = *reinterpret_cast<const floatx4*>(bT + __float_as_int(tk[r].x) * kE);
-            const f2 rr = splat2(tk[r].y);
-            floatx4 x;
-            x.lo = pk_fma(rr, wr4.lo, b4.lo) + wp[r].lo;
-            x.hi = pk_fma(rr, wr4.hi, b4.hi) + wp[r].hi;
-            row(x, d[r], rs[r], s[r]);
-            s[r] = (base + 8 * r + g < pos) ? s[r] : -INFINITY;
+            const f2 rr = splat2(tk[r].y), mu = splat2(-tk[r].z);
+            d[r].lo = (pk_fma(rr, wr4.lo, b4.lo) + wp[r].lo) + mu;
+            d[r].hi = (pk_fma(rr, wr4.hi, b4.hi) + wp[r].hi) + mu;
+            float dg = d[r].x * gu.x;
+            dg = fmaf(d[r].y, gu.y, dg);
+            dg = fmaf(d[r].z, gu.z, dg);
+            dg = fmaf(d[r].w, gu.w, dg);
+            dg = dpp_sum8(dg);
+            s[r] = (base + 8 * r + g < pos) ? (tk[r].w * dg) * scale2 : -INFINITY;
             mx = fmaxf(mx, s[r]);
         }
         const float mn = fmaxf(m, mx);
@@ -445,7 +454,7 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float4* 
         for (int r = 0; r < R; ++r) {
             const float pr = __builtin_amdgcn_exp2f(s[r] - mn);
             l += pr;
-            const f2 w = splat2(pr * rs[r]);
+            const f2 w = splat2(pr * tk[r].w);
             alo = pk_fma(w, d[r].lo, alo);
             ahi = pk_fma(w, d[r].hi, ahi);
         }
@@ -507,6 +516,8 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float4* 
 // is per-(position, task) scalar work, one element per lane and register.  Wave w
 // takes the tiles w, w + 8, ...; its partial softmax state per task (m, l, the scalar
 // sums, the arm sums and the wpe sum) goes to part[w][task][48] for l0_merge.
+constexpr int kL0Part = 64;  // floats per (wave, task) partial of l0_tiles (36 + NA <= 64)
+
 template <int NA>
 __device__ __attribute__((always_inline)) inline void l0_tiles(const float* __restrict__ rec_base, size_t task_stride,
                                                                int ntask, int pos, const float* __restrict__ wpe,
@@ -609,7 +620,7 @@ __device__ __attribute__((always_inline)) inline void l0_tiles(const float* __re
 #pragma unroll
     for (int k = 0; k < NA; ++k) W[k] = red(W[k]);
     if (n < 8) {
-        float* pp = part + (wave * 8 + n) * 48;
+        float* pp = part + (wave * 8 + n) * kL0Part;
         *reinterpret_cast<floatx4*>(pp + 4 * j) = o0;
         *reinterpret_cast<floatx4*>(pp + 16 + 4 * j) = o1;
         if (j == 0) {
@@ -637,7 +648,7 @@ __device__ __attribute__((always_inline)) inline float4 l0_merge(const float* pa
     float M = -1e30f;
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
-        mw[w] = part[(w * 8 + t) * 48 + 32];
+        mw[w] = part[(w * 8 + t) * kL0Part + 32];
         M = fmaxf(M, mw[w]);
     }
     float L = 0.f, SR = 0.f, SM = 0.f;
@@ -647,7 +658,7 @@ __device__ __attribute__((always_inline)) inline float4 l0_merge(const float* pa
     f2 olo = {0.f, 0.f}, ohi = {0.f, 0.f};
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
-        const float* pp = part + (w * 8 + t) * 48;
+        const float* pp = part + (w * 8 + t) * kL0Part;
         const float sw = __builtin_amdgcn_exp2f(mw[w] - M);
         L = fmaf(sw, pp[33], L);
         SR = fmaf(sw, pp[34], SR);
@@ -833,19 +844,21 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                     const int t = kq * 4 + r;
                     if (t < TILE) S.q[t][col] = acc[r] + bias;
                 }
-            } else if (L0M && li == 0 && wave == 2) {
+            } else if (L0M && li == 0 && wave < 2 + l0_cols(L0M - 1) / 16) {
                 // l0_tiles' per-task constants (alpha, gamma, beta[k]) = xn gx + gx0 -> S.vcur
+                constexpr int C = l0_cols(L0M - 1);
                 const RolloutLDS rl = RolloutLDS::make(M.A, M.n_layer, GL, true);
+                const int col = (wave - 2) * 16 + i16;
                 floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < 8; ++s)
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(S.xn[i16][4 * s + kq], D[rl.gx + (4 * s + kq) * 16 + i16],
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(S.xn[i16][4 * s + kq], D[rl.gx + (4 * s + kq) * C + col],
                                                                acc, 0, 0, 0);
-                const float bias = D[rl.gx0 + i16];
+                const float bias = D[rl.gx0 + col];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int t = kq * 4 + r;
-                    if (t < TILE) S.vcur[t][i16] = acc[r] + bias;
+                    if (t < TILE) S.vcur[t][col] = acc[r] + bias;
                 }
             }
         } else if (wave < 6) {
@@ -1240,11 +1253,12 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         };
         const float* G0 = M.l0 + L0Off::G;
         const float* g00 = M.l0 + L0Off::g0;
-        for (int i = tid; i < (kE + 1) * 16; i += TILE * 64) {
-            const int row = i / 16, c = i % 16;
+        constexpr int C = l0_cols(L0M - 1);
+        for (int i = tid; i < (kE + 1) * C; i += TILE * 64) {
+            const int row = i / C, c = i % C;
             double acc = 0.0;
             for (int jj = 0; jj < kE; ++jj) acc += (row < kE ? (double)G0[row * kE + jj] : (double)g00[jj]) * v(c, jj);
-            D[rl.gx + i] = (float)acc;  // row kE lands in gx0 (= gx + kE * 16)
+            D[rl.gx + i] = (float)acc;  // row kE lands in gx0 (= gx + kE * C)
         }
     }
     // per task, block 0's K slot holds the token record of every position (TokRec)
@@ -1378,7 +1392,7 @@ extern "C" int dpt_debug_stamps(unsigned long long* out, int n, int reset) {
 
 static int g_decode_tile = 8;  // tuning knob (dpt_tuning_set(DPT_TUNE_DECODE_TILE, 8|16))
 static int64_t g_cache_budget = DPT_DEFAULT_CACHE_BUDGET;  // DPT_TUNE_CACHE_BUDGET
-static bool g_block0_mfma = true;                          // DPT_TUNE_BLOCK0_MFMA
+static bool g_block0_mfma = false;                         // DPT_TUNE_BLOCK0_MFMA
 
 int set_block0_mfma(int on) {
     g_block0_mfma = on != 0;
@@ -1473,6 +1487,7 @@ int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, 
     // tile 8, one at tile 16); otherwise the u projection reads it from L2
     const size_t per_cu = 160 * 1024 / (g_decode_tile == 8 ? 2 : 1);
     // block 0 on the matrix cores (l0_tiles) for the 5-arm configs at tile 8
+    // (A = 20 in this form spills at the 128-VGPR cap: its 21 arm sums; measured +17 %)
     const bool l0m = g_block0_mfma && g_decode_tile == 8 && a.A == 5;
     const bool gl = rollout_smem_bytes(M, true, l0m) <= per_cu;
     sm = rollout_smem_bytes(M, gl, l0m);

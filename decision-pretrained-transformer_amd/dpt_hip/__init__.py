@@ -363,8 +363,8 @@ def set_cache_budget(nbytes):
 
 
 def set_block0_mfma(on):
-    """Bandit rollout, 5 arms at tile 8: block 0's attention on the matrix cores (default) or one
-    wave per task on the vector ALUs.  Same algebra; the fp32 summation order differs."""
+    """Bandit rollout, 5 arms at tile 8: block 0's attention on the matrix cores, or one wave per
+    task on the vector ALUs (default).  Same algebra; the fp32 summation order differs."""
     _lib.call("dpt_tuning_set", _lib.TUNE_BLOCK0_MFMA, int(bool(on)))
 
 

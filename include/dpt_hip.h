@@ -78,11 +78,11 @@ const char* dpt_last_error(void);
  * are re-read on-die every step; later positions stream non-temporally and do
  * not displace them).  0: every row non-temporal.  Cache policy only: results
  * are bit-identical for any value.
- * DPT_TUNE_BLOCK0_MFMA = 1 (default): dpt_rollout_bandit computes block 0's
- * attention of a tile of 8 five-arm tasks on the matrix cores (the shared
- * position-embedding terms as MFMA products, the per-token terms as scalars);
- * 0: one wave per task on the vector ALUs.  Same algebra, different fp32
- * summation order.  */
+ * DPT_TUNE_BLOCK0_MFMA = 0 (default): dpt_rollout_bandit computes block 0's
+ * attention with one wave per task on the vector ALUs; 1: for tiles of 8
+ * five-arm tasks, on the matrix cores (the shared position-embedding terms as
+ * MFMA products, the per-token terms as scalars).  Same algebra, different fp32
+ * summation order; equal speed at config 2.  */
 #define DPT_TUNE_DECODE_TILE 1
 #define DPT_TUNE_PREFILL 2
 #define DPT_TUNE_DARKROOM_MEMO 3

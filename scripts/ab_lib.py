@@ -1,7 +1,7 @@
 """A/B of library builds (Makefile `variants`): one bandit rollout timing per library,
 each in its own process (python scripts/ab_lib.py libA.so libB.so ...; rounds alternate).
-An argument libX.so:<bytes> runs libX.so with dpt_hip.set_cache_budget(<bytes>); a suffix +nob0 runs
-it with dpt_hip.set_block0_mfma(False).
+An argument libX.so:<bytes> runs libX.so with dpt_hip.set_cache_budget(<bytes>); a suffix +b0 / +nob0
+runs it with dpt_hip.set_block0_mfma(True / False).
 Env: AB_H, AB_N, AB_A, AB_TILE, AB_ROUNDS."""
 import json
 import os
@@ -16,16 +16,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def child(lib):
     sys.path[:0] = [os.path.join(ROOT, "decision-pretrained-transformer_amd"), ROOT]
     from dpt_hip import _lib
-    nob0 = lib.endswith("+nob0")  # "libX.so+nob0": block 0 on the vector ALUs (DPT_TUNE_BLOCK0_MFMA 0)
-    lib = lib[: -len("+nob0")] if nob0 else lib
+    b0 = None  # "libX.so+b0" / "+nob0": DPT_TUNE_BLOCK0_MFMA 1 / 0
+    for suf, on in (("+nob0", False), ("+b0", True)):
+        if lib.endswith(suf):
+            lib, b0 = lib[: -len(suf)], on
     _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.__file__), lib.split(":")[0])
     import torch
     import bench
     import dpt_hip
     H, N, A = (int(os.environ.get(k, d)) for k, d in (("AB_H", "500"), ("AB_N", "4096"), ("AB_A", "5")))
     dpt_hip.set_decode_tile(int(os.environ.get("AB_TILE", "8")))
-    if nob0:
-        dpt_hip.set_block0_mfma(False)
+    if b0 is not None:
+        dpt_hip.set_block0_mfma(b0)
     if ":" in lib:  # "libX.so:<bytes>": the same library at another DPT_TUNE_CACHE_BUDGET
         dpt_hip.set_cache_budget(int(lib.split(":")[1]))
     if os.environ.get("AB_WL") == "darkroom":  # config 3: 4096 tasks x 40 episodes x 100 steps

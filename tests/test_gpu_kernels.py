@@ -238,7 +238,7 @@ def test_decode_tiles_bit_identical():
                          w.cpu().numpy()])
     finally:
         dpt_hip.set_decode_tile(8)  # the library defaults
-        dpt_hip.set_block0_mfma(True)
+        dpt_hip.set_block0_mfma(False)
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
     assert_logits(outs[1][3], g["T101/preds_train"])
@@ -246,7 +246,7 @@ def test_decode_tiles_bit_identical():
 
 @pytest.mark.parametrize("N,H", [(100, 40), (1000, 130)])
 def test_rollout_block0_mfma_matches_vector_path(N, H):
-    """Block 0 on the matrix cores (l0_tiles / l0_merge, the default at tile 8 and 5 arms) against
+    """Block 0 on the matrix cores (l0_tiles / l0_merge, DPT_TUNE_BLOCK0_MFMA) against
     the one-wave-per-task vector path: same algebra, another fp32 summation order.  Per task, the
     per-step logits agree within the 1e-5 bar up to the first step whose sampled action differs
     (a uniform within rounding of a cdf edge), and such divergences are rare."""
@@ -260,7 +260,7 @@ def test_rollout_block0_mfma_matches_vector_path(N, H):
             o = m.rollout_bandit(means, H, 0.3, True, seed=17, want_logits=True)
             outs.append((o["actions"].cpu().numpy(), o["logits"].cpu().numpy()))
     finally:
-        dpt_hip.set_block0_mfma(True)
+        dpt_hip.set_block0_mfma(False)
     (a0, l0), (a1, l1) = outs
     diff = a0 != a1
     first = np.where(diff.any(1), diff.argmax(1), H)  # first differing step per task
