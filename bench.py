@@ -51,12 +51,12 @@ def algorithmic_bytes(N, H, n_layer, E=32):
     """Minimal HBM bytes of one fused rollout launch (rollout_bandit_kernel's
     algorithm): at step h, blocks 1..L-1 stream the cached LayerNorm output y_p
     of positions < h (E*4 B each; y serves as both key and value on folded
-    weights) and block 0 reads the 8-B (action, reward) record of
-    each position < h (its attention is recomputed from the tokens); the new y
-    rows and record are written, and means[a] (8 B) is read + action (4 B),
-    reward and arm value (8 B each) are written.  wpe and the weights are shared
-    by every task and served from L2 (not counted)."""
-    per_pos = (n_layer - 1) * E * 4 + 8
+    weights) and block 0 reads the 16-B token record of each position
+    < h (action, reward and the ln_1 mean / rstd: its attention is recomputed from
+    the tokens); the new y rows and record are written, and means[a] (8 B) is
+    read + action (4 B), reward and arm value (8 B each) are written.  wpe and the
+    weights are shared by every task and served from L2 (not counted)."""
+    per_pos = (n_layer - 1) * E * 4 + 16
     per_task = per_pos * H * (H - 1) // 2 + (per_pos + 28) * H
     return N * per_task
 
