@@ -209,7 +209,7 @@ int dpt_model_free(dpt_model* m) {
 int dpt_kvcache_numel(const dpt_model* m, int32_t N, int32_t max_pos, int64_t* numel) {
     REQUIRE(m && numel, "null model/numel");
     REQUIRE(N >= 1 && max_pos >= 1, "N=%d max_pos=%d", N, max_pos);
-    *numel = (int64_t)2 * m->desc.n_layer * N * (int64_t)max_pos * kE;
+    *numel = (int64_t)2 * m->desc.n_layer * kv_tasks(N) * (int64_t)max_pos * kE;  // whole tiles (dpt_decode.hip)
     return DPT_OK;
 }
 

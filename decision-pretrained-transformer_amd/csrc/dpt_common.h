@@ -244,6 +244,11 @@ struct L0Off {
     static constexpr int size = bvp + kE;
 };
 
+// Tasks the K/V workspace is laid out for: N rounded up to whole tiles of the
+// largest decode tile (16), so the bandit rollout's tile-interleaved y rows of a
+// partial last tile stay inside their block's slot (dpt_kvcache_numel).
+__host__ __device__ inline int kv_tasks(int N) { return (N + 15) & ~15; }
+
 // ----------------------------------------------------------------------------- env arithmetic
 // envs/bandit_env.py:59: means[a] + np.random.normal(0, var) == means[a] + (0.0 + var*g).
 __device__ inline double gaussian_reward(double mean, double var, double g) {

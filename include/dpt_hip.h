@@ -148,7 +148,8 @@ int dpt_prefill_max_window(const dpt_model* model, int32_t* tokens_out_host);
  * Exact incremental form of the growing-window forward used by the bandit
  * online loop (evals/eval_bandit.py:70-89): the query token is identical at
  * every step, so positions 0..h-1 are unchanged between steps h-1 and h and
- * their keys/values can be cached.  Cache layout [2][n_layer][N][max_pos][E].  */
+ * their keys/values can be cached.  Cache layout [2][n_layer][N'][max_pos][E],
+ * N' = N rounded up to a multiple of 16 (whole decode tiles).                 */
 int dpt_kvcache_numel(const dpt_model* model, int32_t N, int32_t max_pos, int64_t* numel_out_host);
 /* one decode position for all N tasks: token (N,F) packed features of position
  * `pos` (pos 0 is the query token), appends K/V at `pos`, logits (N,A) of it.  */
@@ -236,8 +237,9 @@ typedef struct dpt_bandit_rollout_args {
     const double* uniforms; /* (H, N) or NULL                             */
     const double* noise;    /* (H, N) or NULL (normals, or bernoulli uniforms) */
     float* kvcache;         /* dpt_kvcache_numel(model, N, H) floats: blocks
-                             * 1..L-1 keep their K/V; block 0 is recomputed
-                             * from the tokens, so its K slot holds the (a, r)
+                             * 1..L-1 keep their ln_1 outputs y (tile-
+                             * interleaved rows); block 0 is recomputed from
+                             * the tokens, so its K slot holds the 16-B token
                              * records and its V slot the per-step draws     */
     int32_t* actions_out;   /* (N, H)                                       */
     double* rewards_out;    /* (N, H)                                       */
