@@ -84,6 +84,13 @@ __device__ inline void bar_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// The token record (TokRec) of task tile0 + t at position p: [position][task in
+// tile] at the start of the tile's block-0 K slot (max_pos x TILE x 16 B of its
+// max_pos x TILE x 128 B).
+__device__ inline float* tokrec(float* kv, int max_pos, int tile0, int p, int tile, int t) {
+    return kv + (size_t)tile0 * max_pos * kE + ((size_t)p * tile + t) * 4;
+}
+
 // The rollout's K/V workspace holds whole tiles (kv_tasks, dpt_common.h): blocks
 // l >= 1 keep their y rows tile-interleaved, [tile][position][task in tile][E], so
 // a tile's 8 (16) attention waves streaming the same positions read one
@@ -392,6 +399,8 @@ __device__ __attribute__((always_inline)) inline float4 attend_one(const float* 
 // folded into c_proj (L0Off::Wvp, bvp).  Writes o = sum_p P_p y_p.  The current
 // position's x is xcur (the residual row, before attention).  Scores are kept in
 // the log2 domain (v_exp_f32).
+// tok: the task's token records, TS float4 apart per position (tokrec)
+template <int TS>
 __device__ __attribute__((always_inline)) inline float4 attend_l0(const float4* __restrict__ tok, const float* __restrict__ wpe, int pos,
                                  const float* u, const float* xcur, const float* baseT, const float* wr,
                                  const float* lng, const float* lnb, float* o, int lane) {
@@ -431,7 +440,7 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float4* 
 #pragma unroll
         for (int r = 0; r < R; ++r) {  // past the end: re-read position pos-1, masked below
             const int p = min(base + 8 * r + g, pos - 1);
-            tk[r] = tok[p];
+            tk[r] = tok[(size_t)p * TS];
             wp[r] = *reinterpret_cast<const floatx4*>(wpe + (size_t)p * kE + 4 * c);
         }
         floatx4 d[R];
@@ -524,8 +533,8 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float4* 
 // sums, the arm sums and the wpe sum) goes to part[w][task][48] for l0_merge.
 constexpr int kL0Part = 64;  // floats per (wave, task) partial of l0_tiles (36 + NA <= 64)
 
-template <int NA>
-__device__ __attribute__((always_inline)) inline void l0_tiles(const float* __restrict__ rec_base, size_t task_stride,
+template <int NA, int TILE>
+__device__ __attribute__((always_inline)) inline void l0_tiles(const float* __restrict__ rec_base,
                                                                int ntask, int pos, const float* __restrict__ wpe,
                                                                const float* q, const float* cst, const float* lng,
                                                                float* part, int wave, int lane) {
@@ -538,7 +547,8 @@ __device__ __attribute__((always_inline)) inline void l0_tiles(const float* __re
     for (int s = 0; s < 8; ++s) gb[s] = tv ? lng[8 * j + s] * q[n * kE + 8 * j + s] : 0.f;
     const float* cn = cst + (tv ? n : 0) * kE;
     const float alpha = cn[0], gamma = cn[1];
-    const float4* rec = reinterpret_cast<const float4*>(rec_base + (size_t)(tv ? n : 0) * task_stride);
+    // this lane's task's records, TILE float4 apart per position (tokrec)
+    const float4* rec = reinterpret_cast<const float4*>(rec_base) + (tv ? n : 0);
     float m = -1e30f, l = 0.f, sr = 0.f, sm = 0.f;
     float W[NA];
 #pragma unroll
@@ -554,7 +564,7 @@ __device__ __attribute__((always_inline)) inline void l0_tiles(const float* __re
         float4 R[4];
         float wo0[4], wo1[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) R[r] = rec[min(p0 + 4 * j + r, pos - 1)];
+        for (int r = 0; r < 4; ++r) R[r] = rec[(size_t)min(p0 + 4 * j + r, pos - 1) * TILE];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float* wr = wpe + (size_t)min(p0 + 4 * j + r, pos - 1) * kE + n;
@@ -817,7 +827,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         S.xn[t][j] = ln_halfwave(x, P[pl.layers + PLay::ln1_g + j], P[pl.layers + PLay::ln1_b + j], &mean, &rstd);
         const int task = tile0 + t;
         if (L0R && j == 0 && task < N)  // the LayerNorm statistics of this position's TokRec
-            *reinterpret_cast<float2*>(kv + (size_t)task * max_pos * kE + 4 * pos + 2) = make_float2(mean, rstd);
+            *reinterpret_cast<float2*>(tokrec(kv, max_pos, tile0, pos, TILE, t) + 2) = make_float2(mean, rstd);
     }
     bar_lds();
     DPT_STAMP(0);
@@ -905,7 +915,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         DPT_STAMP(1);
         if constexpr (L0M > 0) {
             if (li == 0) {  // block 0: every wave takes a share of the tile's cached positions
-                l0_tiles<L0M>(kv + (size_t)tile0 * max_pos * kE, (size_t)max_pos * kE, min(TILE, N - tile0),
+                l0_tiles<L0M, TILE>(tokrec(kv, max_pos, tile0, 0, TILE, 0), min(TILE, N - tile0),
                               DPT_EXP_L0POS(pos), M.wpe, &S.q[0][0], &S.vcur[0][0], PL + PLay::ln1_g,
                               &S.part[0][0][0], wave, lane);
                 bar_lds();
@@ -921,8 +931,13 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 const float* kc = kv + li * lstride + (size_t)task * max_pos * kE;
                 // the rollout's y rows are tile-interleaved (yrow): one position of the tile's tasks is
                 // TILE adjacent rows
-                const float* yc = kv + li * lstride + (size_t)tile0 * max_pos * kE + wave * kE;
-                constexpr int YPS = TILE * kE;
+#ifndef DPT_YGROUP
+#define DPT_YGROUP TILE
+#endif
+                constexpr int YG = DPT_YGROUP;  // tasks per interleave group
+                const int grp0 = tile0 / YG * YG;
+                const float* yc = kv + li * lstride + (size_t)grp0 * max_pos * kE + (task - grp0) * kE;
+                constexpr int YPS = YG * kE;
                 const float* vc = kv + vhalf + li * lstride + (size_t)task * max_pos * kE;
                 if (L0R) {
                     const RolloutLDS rl = RolloutLDS::make(M.A, M.n_layer);
@@ -930,7 +945,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                         (L0M > 0 && l0) ? l0_merge<(L0M > 0 ? L0M : 1)>(&S.part[0][0][0], wave, S.q[wave], S.x[wave], D + rl.base,
                                                              P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
                                                              PL + PLay::ln1_b, lane)
-                        : l0 ? attend_l0(reinterpret_cast<const float4*>(kc), M.wpe, DPT_EXP_L0POS(pos), S.q[wave], S.x[wave],
+                        : l0 ? attend_l0<TILE>(reinterpret_cast<const float4*>(tokrec(kv, max_pos, tile0, 0, TILE, wave)), M.wpe, DPT_EXP_L0POS(pos), S.q[wave], S.x[wave],
                                        D + rl.base, P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
                                        PL + PLay::ln1_b, nullptr, lane)
                            // scores y_p . u, output sum_p P_p y_p; y_pos is in S.kcur
@@ -1038,7 +1053,9 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
             if (L0R && !last) {  // block li+1's y at `pos`: its K/V-cache row (128 B per half-wave)
                 S.kcur[t][j] = y;
                 const int task = tile0 + t;
-                float* yd = kv + (li + 1) * lstride + ((size_t)tile0 * max_pos + (size_t)pos * TILE + t) * kE + j;
+                constexpr int YG = DPT_YGROUP;
+                const int grp0 = tile0 / YG * YG;
+                float* yd = kv + (li + 1) * lstride + ((size_t)grp0 * max_pos + (size_t)pos * YG + (task - grp0)) * kE + j;
                 if (task < N) {
                     if (pos < lpin(li + 1)) *yd = y;
                     else __builtin_nontemporal_store(y, yd);
@@ -1152,12 +1169,14 @@ __global__ __launch_bounds__(TILE * 64, 4) void window_decode_kernel(
     }
 }
 
-// TokRec: the rollout's record of one bandit token, 16 B per position, packed at
-// the start of each task's block-0 K slot: (a_p as int bits, float(r_p)) written
-// after the selection that chose them, (mean_p, rstd_p) of ln_1 of block 0 written
-// by the embedding phase of position p.  Position 0 is the query: (A, 0).
+// TokRec: the rollout's record of one bandit token, 16 B per position: (a_p as int
+// bits, float(r_p)) written after the selection that chose them, (mean_p, rstd_p) of
+// ln_1 of block 0 written by the embedding phase of position p.  Position 0 is the
+// query: (A, 0).  Records are tile-interleaved like the y rows, at the start of the
+// tile's block-0 K slot: [position][task in tile] (tokrec), so one position of a
+// tile's tasks is 128 B (tile 8) or 256 B (tile 16) of adjacent records.
 struct BanditRolloutParams {
-    int N, H, A, type, sample, n_layer;
+    int N, H, A, type, sample, n_layer, tile;
     // y rows of positions < pin (+ 8 kYRows for blocks 1..pin_x) use the default cache
     // policy (Infinity-Cache resident), later ones non-temporal (rollout_pin)
     int pin, pin_x;
@@ -1174,12 +1193,13 @@ struct BanditRolloutParams {
     float* logits_out;
 };
 
-// Block 0's V slot of a task (unused by the K/V-free block 0) holds the task's
-// per-step draw pairs (u = selection uniform, g = reward normal or Bernoulli
-// uniform), 16 B x H of the slot's 128 B x H.
-__device__ inline double2* draw_pairs(const BanditRolloutParams& Pr, int task) {
+// Block 0's V slot (unused by the K/V-free block 0) holds the per-step draw pairs
+// (u = selection uniform, g = reward normal or Bernoulli uniform), tile-interleaved
+// like the records: [tile][step][task in tile], 16 B each.
+__device__ inline double2* draw_pair(const BanditRolloutParams& Pr, int task, int h) {
     const size_t vhalf = (size_t)Pr.n_layer * kv_tasks(Pr.N) * Pr.H * kE;
-    return reinterpret_cast<double2*>(Pr.kv + vhalf + (size_t)task * Pr.H * kE);
+    const int tile0 = task / Pr.tile * Pr.tile;
+    return reinterpret_cast<double2*>(Pr.kv + vhalf + (size_t)tile0 * Pr.H * kE) + (size_t)h * Pr.tile + (task - tile0);
 }
 
 // Every draw of the rollout, one thread per (task, step), before the rollout
@@ -1199,7 +1219,7 @@ __global__ void rollout_draws_kernel(BanditRolloutParams Pr) {
         g = philox_uniform(Pr.seed, ctr, gtask, DPT_STREAM_REWARD);
     else
         g = philox_normal(Pr.seed, ctr, gtask, DPT_STREAM_REWARD);
-    draw_pairs(Pr, task)[h] = make_double2(u, g);
+    *draw_pair(Pr, task, h) = make_double2(u, g);
 }
 
 // select_from_logits with the logits in registers for the configured arm counts
@@ -1272,17 +1292,17 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
             D[rl.gx + i] = (float)acc;  // row kE lands in gx0 (= gx + kE * C)
         }
     }
-    // per task, block 0's K slot holds the token record of every position (TokRec)
-    auto tokrec = [&](int task) {
-        return reinterpret_cast<float2*>(Pr.kv + (size_t)task * Pr.H * kE);
+    // (a_p, r_p) of this thread's task's token record of position p (TokRec)
+    auto tokrec_ar = [&](int p) {
+        return reinterpret_cast<float2*>(tokrec(Pr.kv, Pr.H, tile0, p, TILE, tid));
     };
     // position 0: the query token [state=1, 0_A, 0, 0] (BanditEnv.state = [1], ctrl_bandit.py:426)
     if (tid < TILE) {
         S.tok[tid][0] = 1.f;
-        if (tile0 + tid < Pr.N) tokrec(tile0 + tid)[0] = make_float2(__int_as_float(A), 0.f);
+        if (tile0 + tid < Pr.N) *tokrec_ar(0) = make_float2(__int_as_float(A), 0.f);
     }
-    // this thread's task's (u, g) draw pairs (rollout_draws_kernel), one per step
-    const double2* draws = (tid < TILE && tile0 + tid < Pr.N) ? draw_pairs(Pr, tile0 + tid) : nullptr;
+    // this thread's task's (u, g) draw pairs (rollout_draws_kernel), one per step, TILE apart
+    const double2* draws = (tid < TILE && tile0 + tid < Pr.N) ? draw_pair(Pr, tile0 + tid, 0) : nullptr;
     float wpe_next = M.wpe[tid & 31];
     __syncthreads();
     for (int h = 0; h < Pr.H; ++h) {
@@ -1291,7 +1311,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
         // consumed after the forward; read once, so non-temporal (keeps the pinned rows resident)
         double2 dr = make_double2(0.0, 0.0);
         if (draws) {
-            const doublex2 d2 = __builtin_nontemporal_load(reinterpret_cast<const doublex2*>(draws + h));
+            const doublex2 d2 = __builtin_nontemporal_load(reinterpret_cast<const doublex2*>(draws + (size_t)h * TILE));
             dr = make_double2(d2[0], d2[1]);
         }
         decode_position<TILE, true, GL, L0M>(S, P, pl, M, Pr.kv, Pr.N, Pr.H, tile0, h, wpe_j, D, Pr.pin, Pr.pin_x);
@@ -1319,7 +1339,7 @@ __global__ __launch_bounds__(TILE * 64, 4) void rollout_bandit_kernel(ModelView 
             if (Pr.logits_out)  // S.logits is next rewritten by step h+1's head phase
                 for (int k = 0; k < A; ++k) Pr.logits_out[((size_t)h * Pr.N + task) * A + k] = S.logits[t][k];
             // first read from memory by step h+2 (positions < h+2), so it may land during step h+1
-            if (h + 1 < Pr.H) tokrec(task)[2 * (h + 1)] = make_float2(__int_as_float(a), (float)r);
+            if (h + 1 < Pr.H) *tokrec_ar(h + 1) = make_float2(__int_as_float(a), (float)r);
         }
         DPT_STAMP(7);
     }
@@ -1517,6 +1537,7 @@ int launch_rollout_bandit(const ModelView& M, const dpt_bandit_rollout_args& a, 
     P.actions_out = a.actions_out; P.rewards_out = a.rewards_out; P.arm_value_out = a.arm_value_out;
     P.logits_out = a.logits_out;
     P.n_layer = M.n_layer;
+    P.tile = g_decode_tile;
     rollout_pin(a.N, a.H, M.n_layer, &P.pin, &P.pin_x);
     const int64_t nd = (int64_t)a.N * a.H;
     hipLaunchKernelGGL(rollout_draws_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st, P);
