@@ -4,7 +4,8 @@ One "step" = one full online rollout (evals/eval_bandit.py:56-103 with the DPT
 controller sampling, ctrls/ctrl_bandit.py:422-444) of N_local = 4096 tasks x
 H = 500 env steps on each GPU (BASELINE.json configs[1]; weak scaling over
 GPUs: contiguous task blocks, Philox keyed by global task id), followed by
-the RCCL all-gather of the per-task arm-value curves (the regret inputs).
+the regret statistics over all tasks (evals/eval_bandit.py:169-178: mean and
+SEM curves, from an RCCL all_reduce of per-step moments for N > 1).
 Inputs (weights, means) are resident in HBM before the timed region.
 
 Other workloads (not the headline line): --workload linear (config 4 shard:
@@ -146,7 +147,7 @@ def main():
         else:
             dist.init_process_group(backend)
     import dpt_hip
-    from dpt_hip.distributed import gather_rows, shard
+    from dpt_hip.distributed import gather_rows, regret_stats_allreduce, shard
 
     N, L, wl = args.tasks, args.layers, args.workload
     n_total = N * world
@@ -163,11 +164,17 @@ def main():
             means_all = np.stack([arms @ t for t in thetas])
         means = torch.from_numpy(means_all[first:first + count]).cuda()
 
-        def one(step_idx):
+        opt = means.max(dim=1, keepdim=True).values  # the Opt controller's arm value (eval_bandit.py:123-128)
+
+        def one(step_idx, ev=None):
+            if ev is not None:
+                ev[0].record()
             out = model.rollout_bandit(means, H, args.var, True, seed=1000 + step_idx, first_task=first)
-            if dist is not None:
-                gather_rows(out["arm_value"], n_total)
-            return out
+            if ev is not None:  # the rollout kernel's own span (the roofline's launch duration)
+                ev[1].record()
+            # the eval's output: suboptimality / cumulative-regret mean and SEM curves over all tasks
+            # (evals/eval_bandit.py:169-178), from two all_reduces of 2 x H fp64 moments (RCCL for N>1)
+            return regret_stats_allreduce(opt, out["arm_value"], n_total)
 
         env_steps_per_step = n_total * H
         workload = (f"{A}-arm {'Gaussian' if wl == 'bandit' else 'linear (d=2)'} bandit online eval, DPT sampling "
@@ -188,7 +195,7 @@ def main():
         envs = [DarkroomEnv(10, g, H) for g in goals_all[first:first + count]]
         vec = DarkroomEnvVec(envs, first_task=first)
 
-        def one(step_idx):
+        def one(step_idx, ev=None):
             np.random.seed(step_idx)
             ctrl = DarkroomTransformerController(tmodel, batch_size=count, sample=True)
             ret = eval_darkroom.deploy_online_vec(vec, ctrl, Heps, H, H)
@@ -207,17 +214,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record()
-        one(100 + k)
+        one(100 + k, kev[k])
         ev[k][1].record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    # bandit: the rollout kernel launch alone (kev); darkroom: the whole step (one fused launch)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in (kev if wl in ("bandit", "linear") else ev)]))
     if dist is not None:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -225,8 +234,8 @@ def main():
 
     value = env_steps_per_step * args.steps / elapsed
     if wl in ("bandit", "linear"):
-        # the timed span per step is the rollout launch (+ the gather for N>1): for N=1 the
-        # events bracket exactly the one rollout_bandit_kernel launch on the current stream
+        # kern_ms: HIP events around the one rollout launch (draws + rollout_bandit_kernel) on the
+        # current stream
         abytes = algorithmic_bytes(count, H, L)
         achieved = abytes / (kern_ms * 1e-3) / 1e9
         traffic = None

@@ -55,14 +55,18 @@ def regret_stats_allreduce(opt_local, lnr_local, n_total, group=None):
     scipy uses, so a large mean relative to the spread loses nothing to cancellation,
     as the sum-of-squares form would).  Equal to scipy.stats.sem over the gathered
     curves up to fp64 summation order.
-    opt_local / lnr_local: (count, H) arm-value curves of this rank's tasks."""
+    opt_local / lnr_local: (count, H) (or broadcastable (count, 1)) arm-value curves of this
+    rank's tasks.  Without an initialised process group it is the single-process statistic."""
+    distributed = dist.is_available() and dist.is_initialized()  # else: one process holds every task
     diff = opt_local.to(torch.float64) - lnr_local.to(torch.float64)
     cr = torch.cumsum(diff, dim=1)
     n = float(n_total)
     s1 = torch.stack([diff.sum(0), cr.sum(0)])
-    dist.all_reduce(s1, group=group)
+    if distributed:
+        dist.all_reduce(s1, group=group)
     mean = s1 / n
     m2 = torch.stack([((diff - mean[0]) ** 2).sum(0), ((cr - mean[1]) ** 2).sum(0)])
-    dist.all_reduce(m2, group=group)
+    if distributed:
+        dist.all_reduce(m2, group=group)
     sem = torch.sqrt(m2 / (n - 1.0) / n)
     return dict(subopt_mean=mean[0], subopt_sem=sem[0], regret_mean=mean[1], regret_sem=sem[1])
