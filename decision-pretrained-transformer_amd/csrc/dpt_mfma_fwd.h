@@ -291,11 +291,19 @@ __device__ inline void c_attn_n(KV& S, const float* W, const FragSrc& fs, const 
 }
 
 // Causal flash attention of query block qb over keys [key_lo, 16*qb + c]:
-// per token column the running max m (-inf when no key), sum l and the
-// unnormalised o^T (C-layout).
+// per token column a softmax reference m (-inf when no key; never more than
+// kSlack below the column's max), l = sum_s e^(s-m) and the unnormalised o^T =
+// sum_s e^(s-m) v_s (C-layout).
 template <class KV>
 __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
                               float& lsum, float (&o)[8]) {
+    // The running reference m of a token column moves only when a key tile holds a
+    // score more than kSlack above it (always for the first tile with a key): the
+    // probabilities are exp(s - m) <= e^kSlack, so the sums cannot overflow, and the
+    // result sum_s e^(s-m) v / sum_s e^(s-m) is the same softmax for any reference.
+    // Tiles that move nothing skip the cross-lane column max and the rescale of o
+    // and lsum, which shortens the per-tile chain (the test is one wave vote).
+    constexpr float kSlack = 32.f;
     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
     m = -INFINITY;
     lsum = 0.f;
@@ -320,20 +328,23 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
             if ((kb == qb && 4 * g + r > c) || key < key_lo) sv[r] = -INFINITY;
             mt = fmaxf(mt, sv[r]);
         }
-        mt = max_cols(mt);
-        const float mn = fmaxf(m, mt);
-        const float base = mn == -INFINITY ? 0.f : mn;  // no key yet: keep 0, not NaN
-        const float corr = __expf(m - base);
+        if (__builtin_amdgcn_ballot_w64(mt > m + kSlack)) {  // wave-uniform
+            mt = max_cols(mt);
+            const float mn = fmaxf(m, mt);
+            const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+            lsum *= corr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                o0[r] *= corr;
+                o1[r] *= corr;
+            }
+            m = mn;
+        }
+        const float base = m == -INFINITY ? 0.f : m;  // no key yet: keep 0, not NaN
         float pr[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - base);
-        lsum = lsum * corr + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
-        m = mn;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            o0[r] *= corr;
-            o1[r] *= corr;
-        }
+        lsum += (pr[0] + pr[1]) + (pr[2] + pr[3]);
         const floatx4 v0 = ld4(&S.Vt[c][kb * 16 + 4 * g]);
         const floatx4 v1 = ld4(&S.Vt[16 + c][kb * 16 + 4 * g]);
 #pragma unroll
