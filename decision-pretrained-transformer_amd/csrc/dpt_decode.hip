@@ -929,15 +929,10 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
             const int task = tile0 + wave;
             if (task < N) {
                 const float* kc = kv + li * lstride + (size_t)task * max_pos * kE;
-                // the rollout's y rows are tile-interleaved (yrow): one position of the tile's tasks is
+                // the rollout's y rows are tile-interleaved: one position of the tile's tasks is
                 // TILE adjacent rows
-#ifndef DPT_YGROUP
-#define DPT_YGROUP TILE
-#endif
-                constexpr int YG = DPT_YGROUP;  // tasks per interleave group
-                const int grp0 = tile0 / YG * YG;
-                const float* yc = kv + li * lstride + (size_t)grp0 * max_pos * kE + (task - grp0) * kE;
-                constexpr int YPS = YG * kE;
+                const float* yc = kv + li * lstride + (size_t)tile0 * max_pos * kE + wave * kE;
+                constexpr int YPS = TILE * kE;
                 const float* vc = kv + vhalf + li * lstride + (size_t)task * max_pos * kE;
                 if (L0R) {
                     const RolloutLDS rl = RolloutLDS::make(M.A, M.n_layer);
@@ -1053,9 +1048,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
             if (L0R && !last) {  // block li+1's y at `pos`: its K/V-cache row (128 B per half-wave)
                 S.kcur[t][j] = y;
                 const int task = tile0 + t;
-                constexpr int YG = DPT_YGROUP;
-                const int grp0 = tile0 / YG * YG;
-                float* yd = kv + (li + 1) * lstride + ((size_t)grp0 * max_pos + (size_t)pos * YG + (task - grp0)) * kE + j;
+                float* yd = kv + (li + 1) * lstride + ((size_t)tile0 * max_pos + (size_t)pos * TILE + t) * kE + j;
                 if (task < N) {
                     if (pos < lpin(li + 1)) *yd = y;
                     else __builtin_nontemporal_store(y, yd);
