@@ -62,6 +62,9 @@ int set_decode_tile(int);
 int set_darkroom_memo(int);
 int set_cache_budget(int64_t);
 int set_block0_mfma(int);
+int regret_max_steps();
+int64_t regret_workspace_numel(int N, int H);
+int launch_regret_moments(const double*, const double*, int, int, int, const double*, double*, double*, hipStream_t);
 
 }  // namespace dpt
 
@@ -338,6 +341,27 @@ int dpt_rollout_policy(const dpt_policy_rollout_args* a, void* stream) {
         return DPT_EUNSUPPORTED;
     }
     return launch_rollout_policy(*a, S(stream));
+}
+
+int dpt_regret_max_steps(int32_t* out) {
+    REQUIRE(out, "null out");
+    *out = regret_max_steps();
+    return DPT_OK;
+}
+
+int dpt_regret_workspace_numel(int32_t N, int32_t H, int64_t* numel) {
+    REQUIRE(numel && N >= 1 && H >= 1, "N=%d H=%d", N, H);
+    *numel = regret_workspace_numel(N, H);
+    return DPT_OK;
+}
+
+int dpt_regret_moments(const double* arm_value, const double* opt, int32_t N, int32_t H, int32_t mode,
+                       const double* mean, double* workspace, double* out, void* stream) {
+    REQUIRE(arm_value && opt && workspace && out, "null pointer");
+    REQUIRE(N >= 1 && H >= 1 && H <= regret_max_steps(), "N=%d H=%d (H <= %d)", N, H, regret_max_steps());
+    REQUIRE(mode == DPT_REGRET_SUMS || mode == DPT_REGRET_CENTRED, "mode=%d", mode);
+    REQUIRE(mode == DPT_REGRET_SUMS || mean, "centred pass needs the mean");
+    return launch_regret_moments(arm_value, opt, N, H, mode, mean, workspace, out, S(stream));
 }
 
 int dpt_rollout_bandit(const dpt_model* m, const dpt_bandit_rollout_args* a, void* stream) {

@@ -1074,7 +1074,17 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
             for (int r = 0; r < 4; ++r) S.logits[kq * 4 + r][col] = acc[r] + bias;
         }
     }
-    bar_lds();
+    if (L0R && ntile == 1) {
+        // the rollout selects on wave 0, which wrote every logit: a wave-local LDS hand-off
+        // instead of a workgroup barrier (the other waves go on to the step's closing barrier)
+        if (wave == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    } else {
+        bar_lds();
+    }
     DPT_STAMP(6);
 }
 

@@ -350,6 +350,32 @@ def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=Tr
     return out
 
 
+def regret_moments(arm_value, opt, mode=_lib.REGRET_SUMS, mean=None):
+    """One pass of the device regret statistics (evals/eval_bandit.py:169-178, scipy's two-pass
+    form): arm_value (N, H) fp64, opt (N,) fp64 -> (2, H) fp64 sums over tasks of
+    (diff, cumsum(diff)) for REGRET_SUMS, or of their squared deviations from ``mean`` (2, H)
+    for REGRET_CENTRED."""
+    dev = device()
+    av = _dev(arm_value, torch.float64, dev)
+    op = _dev(opt, torch.float64, dev).reshape(-1)
+    N, H = av.shape
+    if op.shape[0] != N:
+        raise ValueError(f"opt has {op.shape[0]} tasks, arm_value {N}")
+    n = ctypes.c_int64()
+    _lib.call("dpt_regret_workspace_numel", N, H, ctypes.byref(n))
+    ws = torch.empty(n.value, dtype=torch.float64, device=dev)
+    out = torch.empty((2, H), dtype=torch.float64, device=dev)
+    mn = None if mean is None else _dev(mean, torch.float64, dev)
+    _lib.call("dpt_regret_moments", _p(av), _p(op), N, H, int(mode), _p(mn), _p(ws), _p(out), _stream())
+    return out
+
+
+def regret_max_steps():
+    n = ctypes.c_int32()
+    _lib.call("dpt_regret_max_steps", ctypes.byref(n))
+    return n.value
+
+
 def set_decode_tile(tile):
     """Tasks per workgroup of the decode kernels (8: two workgroups per CU; 16: one)."""
     _lib.call("dpt_tuning_set", _lib.TUNE_DECODE_TILE, int(tile))

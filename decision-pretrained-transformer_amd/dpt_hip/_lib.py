@@ -163,3 +163,10 @@ class DarkroomRolloutArgs(ctypes.Structure):
 
 SIGNATURES["dpt_prefill_max_window"] = (_i32, [_c_void_p, ctypes.POINTER(_i32)])
 SIGNATURES["dpt_rollout_darkroom"] = (_i32, [_c_void_p, ctypes.POINTER(DarkroomRolloutArgs), _c_void_p])
+
+REGRET_SUMS = 0
+REGRET_CENTRED = 1
+SIGNATURES["dpt_regret_max_steps"] = (_i32, [ctypes.POINTER(_i32)])
+SIGNATURES["dpt_regret_workspace_numel"] = (_i32, [_i32, _i32, ctypes.POINTER(_i64)])
+SIGNATURES["dpt_regret_moments"] = (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,
+                                           _c_void_p, _c_void_p])

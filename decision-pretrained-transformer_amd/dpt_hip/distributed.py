@@ -45,6 +45,11 @@ def sharded_online(rollout_fn, means_all, group=None):
     return gather_rows(out["arm_value"], n_total, group), out
 
 
+def _regret_max_steps():
+    import dpt_hip
+    return dpt_hip.regret_max_steps()
+
+
 def regret_stats_allreduce(opt_local, lnr_local, n_total, group=None):
     """Suboptimality and cumulative-regret mean / SEM curves over ALL tasks of all ranks
     (evals/eval_bandit.py:169-178: diff = opt - lnr, cumsum over steps, mean and
@@ -56,16 +61,28 @@ def regret_stats_allreduce(opt_local, lnr_local, n_total, group=None):
     as the sum-of-squares form would).  Equal to scipy.stats.sem over the gathered
     curves up to fp64 summation order.
     opt_local / lnr_local: (count, H) (or broadcastable (count, 1)) arm-value curves of this
-    rank's tasks.  Without an initialised process group it is the single-process statistic."""
+    rank's tasks.  Without an initialised process group it is the single-process statistic.
+    fp64 curves on the GPU take the device passes (dpt_regret_moments); others the torch ops."""
     distributed = dist.is_available() and dist.is_initialized()  # else: one process holds every task
-    diff = opt_local.to(torch.float64) - lnr_local.to(torch.float64)
-    cr = torch.cumsum(diff, dim=1)
     n = float(n_total)
-    s1 = torch.stack([diff.sum(0), cr.sum(0)])
-    if distributed:
-        dist.all_reduce(s1, group=group)
-    mean = s1 / n
-    m2 = torch.stack([((diff - mean[0]) ** 2).sum(0), ((cr - mean[1]) ** 2).sum(0)])
+    H = lnr_local.shape[1]
+    if lnr_local.is_cuda and lnr_local.dtype == torch.float64 and H <= _regret_max_steps():
+        # device passes (dpt_regret_moments, HIP): one read of the curves each
+        import dpt_hip
+        opt = opt_local.reshape(lnr_local.shape[0], -1)[:, 0]
+        s1 = dpt_hip.regret_moments(lnr_local, opt)
+        if distributed:
+            dist.all_reduce(s1, group=group)
+        mean = s1 / n
+        m2 = dpt_hip.regret_moments(lnr_local, opt, dpt_hip._lib.REGRET_CENTRED, mean)
+    else:
+        diff = opt_local.to(torch.float64) - lnr_local.to(torch.float64)
+        cr = torch.cumsum(diff, dim=1)
+        s1 = torch.stack([diff.sum(0), cr.sum(0)])
+        if distributed:
+            dist.all_reduce(s1, group=group)
+        mean = s1 / n
+        m2 = torch.stack([((diff - mean[0]) ** 2).sum(0), ((cr - mean[1]) ** 2).sum(0)])
     if distributed:
         dist.all_reduce(m2, group=group)
     sem = torch.sqrt(m2 / (n - 1.0) / n)

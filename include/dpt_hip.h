@@ -329,6 +329,23 @@ typedef struct dpt_darkroom_rollout_args {
 int dpt_rollout_darkroom(const dpt_model* model, const dpt_darkroom_rollout_args* args_host,
                          void* stream);
 
+/* Regret statistics of the online bandit eval: replaces evals/eval_bandit.py:169-178
+ * (diff = opt - lnr per step, cumsum over steps, mean and scipy.stats.sem over
+ * tasks) on device, in scipy's two-pass form so that ranks can all-reduce between
+ * the passes.  With diff[t][h] = opt[t] - arm_value[t][h] and cr[t][h] its cumsum
+ * over h, out (2, H) fp64 is
+ *   DPT_REGRET_SUMS:    (sum_t diff[.][h], sum_t cr[.][h])                 (mean unused)
+ *   DPT_REGRET_CENTRED: (sum_t (diff - mean[0][h])^2, sum_t (cr - mean[1][h])^2)
+ * for a caller-supplied mean (2, H).  Fixed reduction order (deterministic).
+ * arm_value (N, H) fp64 (dpt_rollout_bandit's arm_value_out), opt (N) fp64,
+ * H <= dpt_regret_max_steps(), workspace dpt_regret_workspace_numel(N, H) doubles. */
+#define DPT_REGRET_SUMS 0
+#define DPT_REGRET_CENTRED 1
+int dpt_regret_max_steps(int32_t* steps_out_host);
+int dpt_regret_workspace_numel(int32_t N, int32_t H, int64_t* numel_out_host);
+int dpt_regret_moments(const double* arm_value, const double* opt, int32_t N, int32_t H, int32_t mode,
+                       const double* mean, double* workspace, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

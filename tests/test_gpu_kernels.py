@@ -543,3 +543,27 @@ def test_empty_batches():
     _, md, _ = model_from_golden("darkroom")
     o = md.rollout_darkroom(np.zeros((0, 2), np.int64), 3, 10, 1, want_forwards=True)
     assert o["returns"].shape == (0, 3) and o["forwards"].shape == (0, 3)
+
+
+@pytest.mark.parametrize("N,H", [(1000, 500), (4096, 1000), (3, 7)])
+def test_regret_moments_match_scipy(N, H):
+    """dpt_regret_moments (the eval's regret mean / SEM, evals/eval_bandit.py:169-178) against
+    numpy + scipy.stats.sem on the same curves, through distributed.regret_stats_allreduce's
+    single-process device path; deterministic run to run."""
+    import scipy.stats
+    import torch
+    from dpt_hip.distributed import regret_stats_allreduce
+    rs = np.random.RandomState(N + H)
+    means = rs.uniform(0, 1, (N, 5))
+    av = means[np.arange(N)[:, None], rs.randint(0, 5, (N, H))] + 3.0  # offset: mean >> spread
+    opt = means.max(1) + 3.0
+    st = regret_stats_allreduce(torch.from_numpy(opt[:, None]).cuda(), torch.from_numpy(av).cuda(), N)
+    st2 = regret_stats_allreduce(torch.from_numpy(opt[:, None]).cuda(), torch.from_numpy(av).cuda(), N)
+    for k in st:
+        assert torch.equal(st[k], st2[k])
+    diff = opt[:, None] - av
+    cr = np.cumsum(diff, 1)
+    ref = dict(subopt_mean=diff.mean(0), subopt_sem=scipy.stats.sem(diff, 0),
+               regret_mean=cr.mean(0), regret_sem=scipy.stats.sem(cr, 0))
+    for k, v in ref.items():
+        np.testing.assert_allclose(st[k].cpu().numpy(), v, rtol=1e-10, atol=1e-12)
