@@ -197,6 +197,9 @@ __device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn
     const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);
     floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
     floatx4 h[2];
+    // c_fc fragments of chunk c+1 are requested one chunk ahead (their L2 latency hides
+    // behind chunk c's MFMAs instead of stalling the chain; -0.6 % at config 3)
+    floatx4 fa = fs.ld(FragOff::fc, 2), fbq = fs.ld(FragOff::fc, 3);
     {
         const floatx4 fb = ld4(W + PL::fc_b + 4 * g);
         h[0] = fb;
@@ -211,7 +214,12 @@ __device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn
             const floatx4 fb = ld4(W + PL::fc_b + (c + 1) * 16 + 4 * g);
             hn[0] = fb;
             hn[1] = fb;
-            mfma32n<NB>(fs.ld(FragOff::fc, 2 * (c + 1)), fs.ld(FragOff::fc, 2 * (c + 1) + 1), xn, hn);
+            const floatx4 wa = fa, wb = fbq;
+            if (c + 2 < kFF / 16) {
+                fa = fs.ld(FragOff::fc, 2 * (c + 2));
+                fbq = fs.ld(FragOff::fc, 2 * (c + 2) + 1);
+            }
+            mfma32n<NB>(wa, wb, xn, hn);
         }
         floatx4 gl[2];
 #pragma unroll
