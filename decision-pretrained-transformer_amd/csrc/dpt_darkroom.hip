@@ -153,7 +153,30 @@ struct DarkroomParams {
     int32_t* forwards_out;
     int memo;  // 1: reuse this episode's logits for a state already queried (see the kernel)
     const float* frag;
+    float* ws;  // per task: layer-0 inputs x and queries u of the window, C-layout (l0_cache), or null
 };
+
+// The per-task workspace: within an episode the context tokens' layer-0 inputs
+// (embedding + wpe) and queries (u = LN1(x) G + g0) are fixed, so the episode
+// prologue stores them and every step reloads them instead of re-embedding and
+// re-projecting; only the query token (position 0) is recomputed.  Layout per task:
+// [x | u][block][lane][8] fp32, each lane's 8 C-layout values contiguous (2 x 16 B).
+constexpr int kDrWsPerTask = 2 * kFwdBlocks * 64 * 8;
+__device__ inline float* l0_cache(const DarkroomParams& p, int task, int which, int blk) {
+    return p.ws + (size_t)task * kDrWsPerTask + ((size_t)(which * kFwdBlocks + blk) * 64 + lane_id()) * 8;
+}
+__device__ inline void ws_store(float* d, const float (&v)[8]) {
+    *reinterpret_cast<floatx4*>(d) = floatx4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<floatx4*>(d + 4) = floatx4{v[4], v[5], v[6], v[7]};
+}
+__device__ inline void ws_load(const float* d, float (&v)[8]) {
+    const floatx4 a = *reinterpret_cast<const floatx4*>(d), b = *reinterpret_cast<const floatx4*>(d + 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        v[r] = a[r];
+        v[4 + r] = b[r];
+    }
+}
 
 // Token embeddings of block qb (embed_transition + wpe, models/net.py:52-54):
 // the query [state, 0...] at position 0, context transitions after it, zeros
@@ -233,6 +256,14 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
             DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
                            c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 2), kv_from_y<NB>(S.kv, qb, xn)));
+            if (p.ws) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (j >= nb) break;
+                    ws_store(l0_cache(p, task, 0, qb[j]), x[j]);
+                    ws_store(l0_cache(p, task, 1, qb[j]), q[j]);
+                }
+            }
             bar_lds();
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -302,18 +333,35 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 if (t >= p.horizon) break;
             }
             float x[2][8];
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
+            float q[2][8];
             const int sx = S.sx, sy = S.sy;
+            if (p.ws) {
+                // the context tokens' inputs and queries from the episode's workspace; block 0
+                // (wave 0's first block) is re-embedded for its new query token
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (j >= nb) break;
+                    ws_load(l0_cache(p, task, 1, qb[j]), q[j]);
+                    if (qb[j] == 0) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
+                    else ws_load(l0_cache(p, task, 0, qb[j]), x[j]);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
+            }
 
-            // ---- layer 0: queries re-projected, the query token's key/value new
+            // ---- layer 0: queries of the window (token 0's is never used: it has no
+            // earlier key), the query token's key/value new
             {
-                float q[2][8];
                 {
                     float xn[2][8];
-                    DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                                   c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 2)));
+                    if (p.ws) {
+                        if (wave == 0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
+                    } else {
+                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
+                                       c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 2)));
+                    }
                     if (wave == 0) {  // block 0 (slot 0 of wave 0): key/value (= y) of the query token
                         kv_from_y<1>(S.kv, qb, xn);
                         const int lane = lane_id();
@@ -662,6 +710,7 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     p.forwards_out = a.forwards_out;
     p.memo = g_darkroom_memo && a.dim * a.dim <= kMemoStates;
     p.frag = frag;
+    p.ws = a.workspace;
     if (M.n_layer < 2) {
         set_error(DPT_EUNSUPPORTED, "fused darkroom rollout needs n_layer >= 2 (got %d)", M.n_layer);
         return DPT_EUNSUPPORTED;
@@ -679,6 +728,8 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
 }
 
 int darkroom_max_window() { return kFwdT; }
+
+int64_t darkroom_workspace_numel(int N) { return (int64_t)N * kDrWsPerTask; }
 
 }  // namespace dpt
 

@@ -204,15 +204,19 @@ class DeviceModel:
                 if out[k] is not None:
                     out[k].zero_()
             return out
+        n_ws = ctypes.c_int64()
+        _lib.call("dpt_darkroom_workspace_numel", N, ctypes.byref(n_ws))
+        ws = torch.empty(n_ws.value, dtype=torch.float32, device=dev) if _darkroom_ws else None
         args = _lib.DarkroomRolloutArgs(
             N, int(Heps), int(horizon), int(ctx_episodes), int(dim), int(bool(sample)), int(first_task),
             int(seed) & (2 ** 64 - 1), int(counter), float(temp), 0, _p(goals_d).value,
             None if perms_d is None else _p(perms_d).value, None if u_d is None else _p(u_d).value,
             _p(out["returns"]).value, None if out["actions"] is None else _p(out["actions"]).value,
             None if out["logits"] is None else _p(out["logits"]).value,
-            None if out["forwards"] is None else _p(out["forwards"]).value)
+            None if out["forwards"] is None else _p(out["forwards"]).value,
+            None if ws is None else _p(ws).value)
         _lib.call("dpt_rollout_darkroom", self._h, ctypes.byref(args), _stream())
-        out["_keep"] = (goals_d, perms_d, u_d)
+        out["_keep"] = (goals_d, perms_d, u_d, ws)
         return out
 
 
@@ -395,6 +399,14 @@ def set_block0_mfma(on):
 
 
 _darkroom_memo = True
+_darkroom_ws = True
+
+
+def set_darkroom_workspace(on):
+    """DarkRoom rollout: keep the context tokens' layer-0 inputs and queries in a per-task device
+    workspace for the episode (default) or recompute them every step (the workspace-free path)."""
+    global _darkroom_ws
+    _darkroom_ws = bool(on)
 
 
 def set_darkroom_memo(on):

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdpt_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 DPT_OK = 0
 DPT_EINVAL = -1
@@ -158,7 +158,7 @@ class DarkroomRolloutArgs(ctypes.Structure):
                 ("sample", _i32), ("first_task", _i64), ("seed", _u64), ("counter", _u64), ("temp", _f32),
                 ("reserved0", _i32), ("goals", _c_void_p), ("perms", _c_void_p), ("uniforms", _c_void_p),
                 ("returns_out", _c_void_p), ("actions_out", _c_void_p), ("logits_out", _c_void_p),
-                ("forwards_out", _c_void_p)]
+                ("forwards_out", _c_void_p), ("workspace", _c_void_p)]
 
 
 SIGNATURES["dpt_prefill_max_window"] = (_i32, [_c_void_p, ctypes.POINTER(_i32)])
@@ -170,3 +170,4 @@ SIGNATURES["dpt_regret_max_steps"] = (_i32, [ctypes.POINTER(_i32)])
 SIGNATURES["dpt_regret_workspace_numel"] = (_i32, [_i32, _i32, ctypes.POINTER(_i64)])
 SIGNATURES["dpt_regret_moments"] = (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,
                                            _c_void_p, _c_void_p])
+SIGNATURES["dpt_darkroom_workspace_numel"] = (_i32, [_i32, ctypes.POINTER(_i64)])

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 3
+#define DPT_ABI_VERSION 4
 
 /* error codes (mapped to the reference's Python exceptions by dpt_hip/_lib.py) */
 #define DPT_OK 0
@@ -324,7 +324,12 @@ typedef struct dpt_darkroom_rollout_args {
     int32_t* actions_out;       /* (N, Heps*horizon) or NULL */
     float* logits_out;          /* (Heps*horizon, N, 5) or NULL */
     int32_t* forwards_out;      /* (N, Heps) window forwards run per task and episode, or NULL */
+    float* workspace;           /* dpt_darkroom_workspace_numel(N) floats, or NULL: the context
+                                 * tokens' layer-0 inputs and queries, fixed within an episode,
+                                 * are kept there instead of recomputed every step */
 } dpt_darkroom_rollout_args;
+
+int dpt_darkroom_workspace_numel(int32_t N, int64_t* numel_out_host);
 
 int dpt_rollout_darkroom(const dpt_model* model, const dpt_darkroom_rollout_args* args_host,
                          void* stream);

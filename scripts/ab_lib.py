@@ -20,6 +20,8 @@ def child(lib):
     for suf, on in (("+nob0", False), ("+b0", True)):
         if lib.endswith(suf):
             lib, b0 = lib[: -len(suf)], on
+    nows = lib.endswith("+nows")  # DarkRoom without the per-episode layer-0 workspace
+    lib = lib[: -len("+nows")] if nows else lib
     _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.__file__), lib.split(":")[0])
     import torch
     import bench
@@ -28,6 +30,8 @@ def child(lib):
     dpt_hip.set_decode_tile(int(os.environ.get("AB_TILE", "8")))
     if b0 is not None:
         dpt_hip.set_block0_mfma(b0)
+    if nows:
+        dpt_hip.set_darkroom_workspace(False)
     if ":" in lib:  # "libX.so:<bytes>": the same library at another DPT_TUNE_CACHE_BUDGET
         dpt_hip.set_cache_budget(int(lib.split(":")[1]))
     if os.environ.get("AB_WL") == "darkroom":  # config 3: 4096 tasks x 40 episodes x 100 steps

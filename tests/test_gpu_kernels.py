@@ -567,3 +567,23 @@ def test_regret_moments_match_scipy(N, H):
                regret_mean=cr.mean(0), regret_sem=scipy.stats.sem(cr, 0))
     for k, v in ref.items():
         np.testing.assert_allclose(st[k].cpu().numpy(), v, rtol=1e-10, atol=1e-12)
+
+
+def test_rollout_darkroom_workspace_bit_identical():
+    """The per-episode layer-0 workspace (context tokens' inputs and queries kept instead of
+    recomputed each step) changes nothing: actions, logits and returns are bit-identical."""
+    import dpt_hip
+    _, m, _ = model_from_golden("darkroom")
+    rs = np.random.RandomState(23)
+    N = 300
+    goals = rs.randint(0, 10, (N, 2))
+    outs = []
+    try:
+        for on in (False, True):
+            dpt_hip.set_darkroom_workspace(on)
+            o = m.rollout_darkroom(goals, 4, 100, 1, seed=4, want_actions=True, want_logits=True)
+            outs.append({k: o[k].cpu().numpy() for k in ("actions", "logits", "returns")})
+    finally:
+        dpt_hip.set_darkroom_workspace(True)
+    for k in ("actions", "logits", "returns"):
+        assert np.array_equal(outs[0][k], outs[1][k]), k
