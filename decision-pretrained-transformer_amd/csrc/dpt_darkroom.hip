@@ -132,6 +132,7 @@ struct alignas(16) DrSmem {
     float memo_lg[kMemoStates][kDrA];
     double memo_q[kMemoStates][kDrA];  // and their selection cdf (cdf_fixed), so a hit selects by 5 compares
     int memo_ok[kMemoStates];
+    double u_ep[kFwdT];                // this episode's selection uniforms, one per step
     int sx, sy, ret, nfwd, tnext;
 };
 
@@ -246,6 +247,15 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             S.nfwd = 0;
         }
         for (int i = tid; i < kMemoStates; i += blockDim.x) S.memo_ok[i] = 0;
+        // the episode's selection uniforms up front, one thread per step (off the serial
+        // select chain of thread 0; ordered before their use by the barriers below)
+        if (p.sample) {
+            for (int t = tid; t < p.horizon; t += blockDim.x) {
+                const int step = ep * p.horizon + t;
+                S.u_ep[t] = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
+                                       : philox_uniform(p.seed, p.counter + step, p.first_task + task, DPT_STREAM_SELECT);
+            }
+        }
         __syncthreads();
 
         // layer-0 episode cache: causal partial over keys 1..t of every token
@@ -288,10 +298,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         // equals select_fixed(lg, u) bit for bit
         auto finish_step = [&](const float (&lg)[kDrA], const double* q, int t, int sx, int sy) {
             const int step = ep * p.horizon + t;
-            double u = 0.0;
-            if (p.sample)
-                u = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
-                               : philox_uniform(p.seed, p.counter + step, p.first_task + task, DPT_STREAM_SELECT);
+            const double u = p.sample ? S.u_ep[t] : 0.0;
             const int a = p.sample ? select_from_cdf<kDrA>(q, u) : select_fixed<kDrA>(lg, 0, p.temp, u);
             const int ea = p.perms ? p.perms[(size_t)task * kDrA + a] : a;
             int nx = sx + (ea == 0) - (ea == 1);

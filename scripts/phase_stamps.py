@@ -22,7 +22,7 @@ import dpt_hip  # noqa: E402
 names = ["embed+ln1", "c_attn", "attention", "c_proj+ln2", "c_fc->mlp", "reduce+ln", "head", "select+env"]
 sd, _ = bench.synthetic_state_dict(4, 1, 5, 500)
 m = dpt_hip.DeviceModel(sd, 4, 1, 5, 2004)
-N = 4096
+N = int(os.environ.get("ST_N", "4096"))
 means = torch.from_numpy(np.random.RandomState(1).uniform(0, 1, (N, 5))).cuda()
 res = {}
 for tile in [int(t) for t in os.environ.get("ST_TILES", "16,8").split(",")]:
