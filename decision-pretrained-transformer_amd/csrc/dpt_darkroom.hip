@@ -133,7 +133,7 @@ struct alignas(16) DrSmem {
     double memo_q[kMemoStates][kDrA];  // and their selection cdf (cdf_fixed), so a hit selects by 5 compares
     int memo_ok[kMemoStates];
     double u_ep[kFwdT];                // this episode's selection uniforms, one per step
-    int sx, sy, ret, nfwd, tnext;
+    int sx, sy, nfwd, tnext;
 };
 
 __device__ inline int2 pack_tr(int x, int y, int a, int nx, int ny, int r) {
@@ -233,6 +233,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     for (int i = tid; i < kDrA; i += blockDim.x) P[pt.head_b + i] = M.head_b[i];
     for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
 
+    // the task's goal and action permutation, once (wave-uniform: scalar registers), not
+    // reloaded from memory on thread 0's serial select chain every step
+    const int goal_x = p.goals[2 * task], goal_y = p.goals[2 * task + 1];
+    int perm[kDrA];
+#pragma unroll
+    for (int k = 0; k < kDrA; ++k) perm[k] = p.perms ? p.perms[(size_t)task * kDrA + k] : k;
     for (int ep = 0; ep < p.Heps; ++ep) {
         const int nctx = min(ep, p.R) * p.horizon;
         const int T = 1 + nctx;
@@ -243,9 +249,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         if (tid == 0) {
             S.sx = 0;
             S.sy = 0;
-            S.ret = 0;
             S.nfwd = 0;
         }
+        // thread 0's copy of the state and the episode's return (it runs every selection)
+        int cur_x = 0, cur_y = 0, cur_ret = 0;
         for (int i = tid; i < kMemoStates; i += blockDim.x) S.memo_ok[i] = 0;
         // the episode's selection uniforms up front, one thread per step (off the serial
         // select chain of thread 0; ordered before their use by the barriers below)
@@ -300,17 +307,16 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             const int step = ep * p.horizon + t;
             const double u = p.sample ? S.u_ep[t] : 0.0;
             const int a = p.sample ? select_from_cdf<kDrA>(q, u) : select_fixed<kDrA>(lg, 0, p.temp, u);
-            const int ea = p.perms ? p.perms[(size_t)task * kDrA + a] : a;
+            const int ea = p.perms ? perm[a] : a;
             int nx = sx + (ea == 0) - (ea == 1);
             int ny = sy + (ea == 2) - (ea == 3);
             nx = min(max(nx, 0), p.dim - 1);
             ny = min(max(ny, 0), p.dim - 1);
-            const int gx = p.goals[2 * task], gy = p.goals[2 * task + 1];
-            const int r = (nx == gx && ny == gy) ? 1 : 0;
+            const int r = (nx == goal_x && ny == goal_y) ? 1 : 0;
             S.cur[t] = pack_tr(sx, sy, a, nx, ny, r);
-            S.sx = nx;
-            S.sy = ny;
-            S.ret += r;
+            cur_x = nx;  // thread 0's registers; published to S.sx / S.sy before other threads read them
+            cur_y = ny;
+            cur_ret += r;
             if (p.actions_out) p.actions_out[(size_t)task * steps_total + step] = a;
             if (p.logits_out) {
 #pragma unroll
@@ -325,14 +331,16 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 if (tid == 0) {
                     int tt = t;
                     while (tt < p.horizon) {
-                        const int sidx = S.sx * p.dim + S.sy;
+                        const int sidx = cur_x * p.dim + cur_y;
                         if (!S.memo_ok[sidx]) break;
                         float lg[kDrA];
 #pragma unroll
                         for (int k = 0; k < kDrA; ++k) lg[k] = S.memo_lg[sidx][k];
-                        finish_step(lg, S.memo_q[sidx], tt, S.sx, S.sy);
+                        finish_step(lg, S.memo_q[sidx], tt, cur_x, cur_y);
                         ++tt;
                     }
+                    S.sx = cur_x;
+                    S.sy = cur_y;
                     S.tnext = tt;
                 }
                 bar_lds();
@@ -648,6 +656,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                         S.nfwd += 1;
                         finish_step(lg, q, t, sx, sy);
+                        S.sx = cur_x;
+                        S.sy = cur_y;
                     }
                 }
             }
@@ -657,7 +667,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 
         // episode bookkeeping: returns, then shift-append the context (eval_darkroom.py:75-82)
         if (tid == 0) {
-            p.returns_out[(size_t)task * p.Heps + ep] = S.ret;
+            p.returns_out[(size_t)task * p.Heps + ep] = cur_ret;
             if (p.forwards_out) p.forwards_out[(size_t)task * p.Heps + ep] = S.nfwd;
         }
         const int R = p.R, H = p.horizon;
