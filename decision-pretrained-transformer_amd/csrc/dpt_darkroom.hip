@@ -155,6 +155,7 @@ struct DarkroomParams {
     int memo;  // 1: reuse this episode's logits for a state already queried (see the kernel)
     const float* frag;
     float* ws;  // per task: layer-0 inputs x and queries u of the window, C-layout (l0_cache), or null
+    const float* tab;  // per grid state: the query token's layer-0 input and LN1 output (state_tables), or null
 };
 
 // The per-task workspace: within an episode the context tokens' layer-0 inputs
@@ -162,9 +163,12 @@ struct DarkroomParams {
 // prologue stores them and every step reloads them instead of re-embedding and
 // re-projecting; only the query token (position 0) is recomputed.  Layout per task:
 // [x | u][block][lane][8] fp32, each lane's 8 C-layout values contiguous (2 x 16 B).
+// The workspace starts with the per-state table (kDrTab floats), then the task caches.
 constexpr int kDrWsPerTask = 2 * kFwdBlocks * 64 * 8;
+constexpr int kDrTabPerState = 2 * 4 * 8;
+constexpr int kDrTab = kMemoStates * kDrTabPerState;
 __device__ inline float* l0_cache(const DarkroomParams& p, int task, int which, int blk) {
-    return p.ws + (size_t)task * kDrWsPerTask + ((size_t)(which * kFwdBlocks + blk) * 64 + lane_id()) * 8;
+    return p.ws + kDrTab + (size_t)task * kDrWsPerTask + ((size_t)(which * kFwdBlocks + blk) * 64 + lane_id()) * 8;
 }
 __device__ inline void ws_store(float* d, const float (&v)[8]) {
     *reinterpret_cast<floatx4*>(d) = floatx4{v[0], v[1], v[2], v[3]};
@@ -205,6 +209,54 @@ __device__ inline void embed_block(const DrSmem& S, const float* P, const PTop& 
         const floatx4 pe = tok == 0 ? ld4(P + pt.wpe0 + d0) : ld4(wpe + (size_t)tok * kE + d0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[blk * 4 + r] = acc[r] + pe[r];
+    }
+}
+
+// The query token (position 0) is [state, 0...]: its layer-0 input x = emb(state) +
+// wpe[0] and its LN1 output y (its key and value in the folded attention) depend on
+// the grid state alone, so one table per launch replaces the per-step re-embedding,
+// LayerNorm and LDS hand-off of wave 0 (and the barrier after it).  Block = one
+// state; each lane computes exactly what embed_block / ln_cols compute for token 0
+// in the rollout (same lane layout, same operation order: bit-identical), and
+// lanes of column 0 store [x | y][g][8] for g = lane >> 4.
+__global__ void __launch_bounds__(64) state_tables_kernel(ModelView M, int dim, float* __restrict__ tab) {
+    __shared__ float sp[kE * (kDrF + 4)];
+    float* emb_b = sp;
+    float* wpe0 = sp + kE;
+    float* g1 = sp + 2 * kE;
+    float* b1 = sp + 3 * kE;
+    float* emb_w = sp + 4 * kE;
+    for (int i = threadIdx.x; i < kE; i += 64) {
+        emb_b[i] = M.emb_b[i];
+        wpe0[i] = M.wpe[i];
+        g1[i] = M.layers[LayerOff::ln1_g + i];
+        b1[i] = M.layers[LayerOff::ln1_b + i];
+    }
+    for (int i = threadIdx.x; i < kDrF * kE; i += 64) emb_w[i] = M.emb_w[i];
+    __syncthreads();
+    const int s = blockIdx.x, lane = lane_id(), g = lane >> 4;
+    const float fv[6] = {(float)(s / dim), (float)(s % dim), 0.0f, 0.0f, 0.0f, 0.0f};
+    const int rows[6] = {0, 1, 2, 7, 8, 9};
+    float x[8], y[8];
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+        const int d0 = 16 * blk + 4 * g;
+        floatx4 acc = ld4(emb_b + d0);
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+            const floatx4 w = ld4(emb_w + rows[f] * kE + d0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = fmaf(fv[f], w[r], acc[r]);
+        }
+        const floatx4 pe = ld4(wpe0 + d0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[blk * 4 + r] = acc[r] + pe[r];
+    }
+    ln_cols(x, y, g1, b1);
+    if ((lane & 15) == 0) {
+        float* d = tab + (size_t)s * kDrTabPerState + g * 8;
+        ws_store(d, x);
+        ws_store(d + 32, y);
     }
 }
 
@@ -353,12 +405,18 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             if (p.ws) {
                 // the context tokens' inputs and queries from the episode's workspace; block 0
                 // (wave 0's first block) is re-embedded for its new query token
+// (with the state table, token 0's input comes from it and the other columns of block 0
+                // from the workspace)
+                const bool col0 = (lane_id() & 15) == 0;
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     if (j >= nb) break;
                     ws_load(l0_cache(p, task, 1, qb[j]), q[j]);
-                    if (qb[j] == 0) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
-                    else ws_load(l0_cache(p, task, 0, qb[j]), x[j]);
+                    if (qb[j] == 0 && !p.tab) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
+                    else
+                        ws_load(qb[j] == 0 && col0 ? p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 8 * (lane_id() >> 4)
+                                                   : l0_cache(p, task, 0, qb[j]),
+                                x[j]);
                 }
             } else {
 #pragma unroll
@@ -369,7 +427,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             // ---- layer 0: queries of the window (token 0's is never used: it has no
             // earlier key), the query token's key/value new
             {
-                {
+                if (!p.tab) {
                     float xn[2][8];
                     if (p.ws) {
                         if (wave == 0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
@@ -389,14 +447,17 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             }
                         }
                     }
+                    bar_lds();
                 }
-                bar_lds();
                 DR_STAMP(0);
                 if (nb > 0) {
                     // merge key 0 into the cached partial of every token column
                     const int lane = lane_id(), g = lane >> 4;
-                    const floatx4 ka = ld4(&S.k0[4 * g]), kc = ld4(&S.k0[16 + 4 * g]);
-                    const floatx4 va = ld4(&S.v0[4 * g]), vb = ld4(&S.v0[16 + 4 * g]);
+                    const float* y0 = p.tab ? p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 32 + 8 * g : nullptr;
+                    const floatx4 ka = p.tab ? ld4(y0) : ld4(&S.k0[4 * g]);
+                    const floatx4 kc = p.tab ? ld4(y0 + 4) : ld4(&S.k0[16 + 4 * g]);
+                    const floatx4 va = p.tab ? ka : ld4(&S.v0[4 * g]);
+                    const floatx4 vb = p.tab ? kc : ld4(&S.v0[16 + 4 * g]);
                     float o[2][8];
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
@@ -728,6 +789,7 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     p.memo = g_darkroom_memo && a.dim * a.dim <= kMemoStates;
     p.frag = frag;
     p.ws = a.workspace;
+    p.tab = a.workspace && a.dim * a.dim <= kMemoStates ? a.workspace : nullptr;
     if (M.n_layer < 2) {
         set_error(DPT_EUNSUPPORTED, "fused darkroom rollout needs n_layer >= 2 (got %d)", M.n_layer);
         return DPT_EUNSUPPORTED;
@@ -740,13 +802,17 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     if (dyn > 64 * 1024)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rollout_darkroom_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    if (p.tab) {
+        hipLaunchKernelGGL(state_tables_kernel, dim3(a.dim * a.dim), dim3(64), 0, st, M, a.dim, a.workspace);
+        if (int rc = check_hip(hipGetLastError(), "state_tables_kernel launch")) return rc;
+    }
     hipLaunchKernelGGL(rollout_darkroom_kernel, dim3(a.N), dim3(kFwdWaves * 64), dyn, st, M, p);
     return check_hip(hipGetLastError(), "rollout_darkroom_kernel launch");
 }
 
 int darkroom_max_window() { return kFwdT; }
 
-int64_t darkroom_workspace_numel(int N) { return (int64_t)N * kDrWsPerTask; }
+int64_t darkroom_workspace_numel(int N) { return kDrTab + (int64_t)N * kDrWsPerTask; }
 
 }  // namespace dpt
 
