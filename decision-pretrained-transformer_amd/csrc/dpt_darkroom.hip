@@ -273,6 +273,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     const PTop pt = PTop::make(L);
     const FragSrc frag0{__builtin_amdgcn_make_buffer_rsrc((void*)p.frag, (short)0, L * FragOff::size * 4, 0x00020000),
                         0};
+    const FragSrc3 split0{__builtin_amdgcn_make_buffer_rsrc((void*)(p.frag + (size_t)L * FragOff::size), (short)0,
+                                                            L * Frag3::bytes, 0x00020000),
+                          0};
     load_layer_params(P, M, tid, blockDim.x);
     for (int i = tid; i < kE; i += blockDim.x) {
         P[pt.lnf_g + i] = M.lnf_g[i];
@@ -484,7 +487,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
                     float xn[2][8];
                     DPT_BLOCKS(nb, (attn_proj<NB>(P, frag0, o, x), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
-                                   mlp_n<NB>(P, frag0, xn, x)));
+                                   mlp3_n<NB>(P, frag0, split0, xn, x)));
                 }
                 DR_STAMP(1);
             }
@@ -543,7 +546,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 DR_STAMP(2 * layer + 1);
                 {
                     float xn[2][8];
-                    DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b), mlp_n<NB>(W, fs, xn, x)));
+                    DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b),
+                                   mlp3_n<NB>(W, fs, split0.layer(layer), xn, x)));
                 }
             }
 
@@ -751,12 +755,46 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     }
 }
 
-int launch_pack_fragments(const ModelView& M, float* frag, hipStream_t st) {
-    hipLaunchKernelGGL(pack_fragments_kernel, dim3(64), dim3(256), 0, st, M, frag);
-    return check_hip(hipGetLastError(), "pack_fragments_kernel launch");
+// The bf16 3-way split tiles (Frag3) of every layer, written after the fp32 fragments.
+__global__ void pack_split_kernel(ModelView M, unsigned short* __restrict__ out) {
+    const int per_layer = Frag3::tiles * 64 * 8;
+    const int total = M.n_layer * per_layer;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int layer = i / per_layer;
+        const int o = i % per_layer;
+        const int tile = o / 512, lane = (o >> 3) & 63, j = o & 7;
+        const int g = lane >> 4, c = lane & 15;
+        const float* W = M.layers + (size_t)layer * LayerOff::size;
+        const float* F = M.l0 + (size_t)layer * L0Off::size;
+        const int kin = 16 * (j >> 2) + 4 * g + (j & 3);
+        float w;
+        if (tile < Frag3::proj) w = F[L0Off::G + kin * kE + tile * 16 + c];
+        else if (tile < Frag3::fc) w = F[L0Off::Wvp + kin * kE + (tile - Frag3::proj) * 16 + c];
+        else if (tile < Frag3::mp) w = W[LayerOff::fc_w + kin * kFF + (tile - Frag3::fc) * 16 + c];
+        else {
+            const int ob = (tile - Frag3::mp) >> 2, pair = (tile - Frag3::mp) & 3;
+            w = W[LayerOff::mp_w + (32 * pair + kin) * kE + ob * 16 + c];
+        }
+        const __bf16 h = (__bf16)w;
+        const float r = w - (float)h;
+        const __bf16 m = (__bf16)r;
+        const __bf16 l = (__bf16)(r - (float)m);
+        unsigned short* d = out + (size_t)layer * (Frag3::bytes / 2) + ((size_t)tile * 3 * 64 + lane) * 8 + j;
+        d[0] = __builtin_bit_cast(unsigned short, h);
+        d[64 * 8] = __builtin_bit_cast(unsigned short, m);
+        d[2 * 64 * 8] = __builtin_bit_cast(unsigned short, l);
+    }
 }
 
-int64_t fragments_numel(int n_layer) { return (int64_t)n_layer * FragOff::size; }
+int launch_pack_fragments(const ModelView& M, float* frag, hipStream_t st) {
+    hipLaunchKernelGGL(pack_fragments_kernel, dim3(64), dim3(256), 0, st, M, frag);
+    if (int rc = check_hip(hipGetLastError(), "pack_fragments_kernel launch")) return rc;
+    hipLaunchKernelGGL(pack_split_kernel, dim3(64), dim3(256), 0, st, M,
+                       reinterpret_cast<unsigned short*>(frag + (size_t)M.n_layer * FragOff::size));
+    return check_hip(hipGetLastError(), "pack_split_kernel launch");
+}
+
+int64_t fragments_numel(int n_layer) { return (int64_t)n_layer * (FragOff::size + Frag3::bytes / 4); }
 
 static bool g_darkroom_memo = true;  // DPT_TUNE_DARKROOM_MEMO
 

@@ -76,6 +76,69 @@ struct FragSrc {
     __device__ FragSrc layer(int l) const { return FragSrc{r, l * FragOff::size * 4}; }
 };
 
+// ---- fp32 products on the bf16 matrix cores (emulated fp32, "x6").  A value is
+// split exactly into three bf16 parts, v = h + m + l + O(2^-24 v) (each residual is
+// exact in fp32), and a K=32 product W^T x^T is the sum of the six part products
+// whose size is at least 2^-16 of h*h (m*l, l*m, l*l are below fp32's own rounding).
+// One v_mfma_f32_16x16x32_bf16 (16 cycles) does the K=32 work of eight
+// v_mfma_f32_16x16x4_f32 (32 cycles each): six of them take 96 cycles instead of 256.
+// The bf16 products are exact and accumulate in fp32, so the result agrees with the
+// fp32 MFMA chain to fp32 rounding (not bit for bit).  Operand layout: lane (g, c)
+// supplies its 8 C-layout values (features 16*(j>>2) + 4g + (j&3), j = 0..7) as the
+// 8 k-elements of its lane group; the weights are packed with the same k order
+// (Frag3), so the logical k permutation cancels.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+struct Split3 {
+    bf16x8 h, m, l;
+};
+__device__ inline Split3 split3(const float (&v)[8]) {
+    Split3 s;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const __bf16 h = (__bf16)v[k];
+        const float r = v[k] - (float)h;
+        const __bf16 m = (__bf16)r;
+        s.h[k] = h;
+        s.m[k] = m;
+        s.l[k] = (__bf16)(r - (float)m);
+    }
+    return s;
+}
+__device__ inline floatx4 mfma_bf16(const bf16x8& a, const bf16x8& b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// acc + A B over k = 32, smallest part products first
+__device__ inline floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 acc) {
+    acc = mfma_bf16(a.m, b.m, acc);
+    acc = mfma_bf16(a.h, b.l, acc);
+    acc = mfma_bf16(a.l, b.h, acc);
+    acc = mfma_bf16(a.h, b.m, acc);
+    acc = mfma_bf16(a.m, b.h, acc);
+    return mfma_bf16(a.h, b.h, acc);
+}
+
+// The split weight tiles of one block (after the fp32 fragments of all layers):
+// [tile][part h|m|l][64 lanes][8 bf16], tile element (lane (g, c), j) = W[in][out]
+// with in = 16*(j>>2) + 4g + (j&3) (mp: hidden 32*pair + that) and out = 16*ob + c.
+struct Frag3 {
+    static constexpr int attn = 0;   // 2 tiles: G
+    static constexpr int proj = 2;   // 2 tiles: Wvp
+    static constexpr int fc = 4;     // 8 tiles: c_fc, output chunk ob
+    static constexpr int mp = 12;    // [2 ob][4 pairs]: mlp.c_proj over hidden chunks 2p, 2p+1
+    static constexpr int tiles = 20;
+    static constexpr int bytes = tiles * 3 * 64 * 16;  // 61,440 per layer
+};
+struct FragSrc3 {
+    __amdgpu_buffer_rsrc_t r;
+    int base;  // byte offset of this layer's tiles
+    __device__ bf16x8 ld1(int tile, int part) const {
+        return __builtin_bit_cast(
+            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, base + (tile * 3 + part) * 1024, 0));
+    }
+    __device__ Split3 ld(int tile) const { return Split3{ld1(tile, 0), ld1(tile, 1), ld1(tile, 2)}; }
+    __device__ FragSrc3 layer(int l) const { return FragSrc3{r, l * Frag3::bytes}; }
+};
+
 // Cross-lane-group reductions with the gfx950 VALU permutes instead of
 // ds_bpermute: v_permlane16_swap / v_permlane32_swap applied to (v, v) return
 // the lane's own value and its xor-16 / xor-32 partner (in an order that
@@ -233,6 +296,60 @@ __device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn
                 __builtin_amdgcn_sched_group_barrier(0x002, 4 / NB, 0);  // gelu(c) VALU
             }
         }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                y0[j] = mfma4(b0[s], gl[j][s], y0[j]);
+                y1[j] = mfma4(b1[s], gl[j][s], y1[j]);
+            }
+        h[0] = hn[0];
+        h[1] = hn[1];
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            x[j][r] += y0[j][r];
+            x[j][4 + r] += y1[j][r];
+        }
+}
+
+// mlp_n with c_fc on the bf16 matrix cores (mfma_x6); mlp.c_proj stays on the fp32
+// MFMA (its input is produced per 16-unit chunk).
+template <int NB>
+__device__ inline void mlp3_n(const float* W, const FragSrc& fs, const FragSrc3& f3, const float (&xn)[2][8],
+                              float (&x)[2][8]) {
+    const int g = lane_id() >> 4;
+    const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);
+    floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
+    Split3 xs[2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) xs[j] = split3(xn[j]);
+    floatx4 h[2];
+    Split3 wn = f3.ld(Frag3::fc);
+    {
+        const floatx4 fb = ld4(W + PL::fc_b + 4 * g);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) h[j] = mfma_x6(wn, xs[j], fb);
+    }
+    if (kFF / 16 > 1) wn = f3.ld(Frag3::fc + 1);
+#pragma unroll
+    for (int c = 0; c < kFF / 16; ++c) {
+        const floatx4 b0 = fs.ld(FragOff::mp, c), b1 = fs.ld(FragOff::mp, 8 + c);
+        floatx4 hn[2] = {h[0], h[1]};
+        if (c + 1 < kFF / 16) {
+            const floatx4 fb = ld4(W + PL::fc_b + (c + 1) * 16 + 4 * g);
+            const Split3 wc = wn;
+            if (c + 2 < kFF / 16) wn = f3.ld(Frag3::fc + c + 2);
+#pragma unroll
+            for (int j = 0; j < NB; ++j) hn[j] = mfma_x6(wc, xs[j], fb);
+        }
+        floatx4 gl[2];
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gl[j][r] = gelu_fast(h[j][r]);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
