@@ -127,7 +127,7 @@ struct alignas(16) DrSmem {
     float ql[kE], xl[kE];             // last layer: q and residual of token T-1
     float part_o[kFwdBlocks][kE];      // last layer: per-key-tile attention partials
     float part_m[kFwdBlocks], part_l[kFwdBlocks];
-    float part_y[kFF / 16][kE];       // last layer: per-hidden-chunk MLP partials
+    float part_y[kFF / 32][kE];       // last layer: MLP partials per pair of hidden chunks
     // per-episode logits memo, one row per grid state (dim * dim <= kMemoStates)
     float memo_lg[kMemoStates][kDrA];
     double memo_q[kMemoStates][kDrA];  // and their selection cdf (cdf_fixed), so a hit selects by 5 compares
@@ -326,8 +326,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                           c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 2), kv_from_y<NB>(S.kv, qb, xn)));
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b), u_proj3_n<NB>(P, split0, xn, q),
+                           kv_from_y<NB>(S.kv, qb, xn)));
             if (p.ws) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -436,7 +436,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         if (wave == 0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
                     } else {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                                       c_attn_n<NB>(S.kv, P, frag0, qb, xn, q, 0, 2)));
+                                       u_proj3_n<NB>(P, split0, xn, q)));
                     }
                     if (wave == 0) {  // block 0 (slot 0 of wave 0): key/value (= y) of the query token
                         kv_from_y<1>(S.kv, qb, xn);
@@ -486,8 +486,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                     }
                     float xn[2][8];
-                    DPT_BLOCKS(nb, (attn_proj<NB>(P, frag0, o, x), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
-                                   mlp3_n<NB>(P, frag0, split0, xn, x)));
+                    DPT_BLOCKS(nb, (attn_proj3<NB>(P, split0, o, x), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                                   mlp3_n<NB>(P, split0, xn, x)));
                 }
                 DR_STAMP(1);
             }
@@ -501,7 +501,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     float xn[2][8];
                     if (!last) {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       c_attn_n<NB>(S.kv, W, fs, qb, xn, q, 0, 2), kv_from_y<NB>(S.kv, qb, xn)));
+                                       u_proj3_n<NB>(W, split0.layer(layer), xn, q), kv_from_y<NB>(S.kv, qb, xn)));
                     } else {
                         // the last layer needs q only for token T-1 (block qlast)
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(S.kv, qb, xn)));
@@ -512,7 +512,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                                 float xn1[2][8], q1[2][8];
 #pragma unroll
                                 for (int k = 0; k < 8; ++k) xn1[0][k] = xn[j][k];
-                                c_attn_n<1>(S.kv, W, fs, one, xn1, q1, 0, 2);
+                                u_proj3_n<1>(W, split0.layer(layer), xn1, q1);
                                 const int lane = lane_id();
                                 if ((lane & 15) == clast) {
 #pragma unroll
@@ -540,14 +540,14 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
                         for (int k = 0; k < 8; ++k) o[j][k] *= inv;
                     }
-                    DPT_BLOCKS(nb, attn_proj<NB>(W, fs, o, x));
+                    DPT_BLOCKS(nb, attn_proj3<NB>(W, split0.layer(layer), o, x));
                 }
                 bar_lds();  // every read of this layer's K/V is done
                 DR_STAMP(2 * layer + 1);
                 {
                     float xn[2][8];
                     DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b),
-                                   mlp3_n<NB>(W, fs, split0.layer(layer), xn, x)));
+                                   mlp3_n<NB>(W, split0.layer(layer), xn, x)));
                 }
             }
 
@@ -555,19 +555,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             // column of these MFMAs carries the same token (B operands broadcast).
             {
                 const float* W = P + (L - 1) * PL::size;
-                const FragSrc fs = frag0.layer(L - 1);
-                // this wave's tail weight fragments, in flight across the first barrier
-                floatx4 pw[4], fw[2][2], mw[2][2];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) pw[k] = fs.ld(FragOff::proj, k);
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int cj = wave + 4 * h;
-                    fw[h][0] = fs.ld(FragOff::fc, 2 * cj);
-                    fw[h][1] = fs.ld(FragOff::fc, 2 * cj + 1);
-                    mw[h][0] = fs.ld(FragOff::mp, cj);
-                    mw[h][1] = fs.ld(FragOff::mp, 8 + cj);
-                }
+                const FragSrc3 f3 = split0.layer(L - 1);
+                // this wave's tail weight tiles (c_proj, c_fc of hidden chunks 2 wave and
+                // 2 wave + 1), in flight across the first barrier
+                static_assert(kFF / 32 == kFwdWaves, "one pair of hidden chunks per wave");
+                const Split3 pj0 = f3.ld(Frag3::proj), pj1 = f3.ld(Frag3::proj + 1);
+                const Split3 fj0 = f3.ld(Frag3::fc + 2 * wave), fj1 = f3.ld(Frag3::fc + 2 * wave + 1);
                 // (1) key tiles wave and wave+4 of the attention, as flash partials (m, l, o)
                 {
                     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
@@ -645,30 +638,35 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         xl[r] = xa[r];
                         xl[4 + r] = xb[r];
                     }
+                    {
+                        const Split3 os = split3(o);
+                        const floatx4 a0 = mfma_x6(pj0, os, ld4(W + PL::proj_b + 4 * g));
+                        const floatx4 a1 = mfma_x6(pj1, os, ld4(W + PL::proj_b + 16 + 4 * g));
 #pragma unroll
-                    for (int ob2 = 0; ob2 < 2; ++ob2) {
-                        const floatx4 acc = mfma32(pw[2 * ob2], pw[2 * ob2 + 1], o, ld4(W + PL::proj_b + ob2 * 16 + 4 * g));
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) xl[ob2 * 4 + r] += acc[r];
+                        for (int r = 0; r < 4; ++r) {
+                            xl[r] += a0[r];
+                            xl[4 + r] += a1[r];
+                        }
                     }
                     float xn[8];
                     ln_cols(xl, xn, W + PL::ln2_g, W + PL::ln2_b);
+                    {
+                        const Split3 xs = split3(xn);
+                        const floatx4 h0 = mfma_x6(fj0, xs, ld4(W + PL::fc_b + 2 * wave * 16 + 4 * g));
+                        const floatx4 h1 = mfma_x6(fj1, xs, ld4(W + PL::fc_b + (2 * wave + 1) * 16 + 4 * g));
+                        float gv[8];
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int cj = wave + 4 * h;
-                        floatx4 hh = mfma32(fw[h][0], fw[h][1], xn, ld4(W + PL::fc_b + cj * 16 + 4 * g));
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) hh[r] = gelu_fast(hh[r]);
-                        const floatx4 m0 = mw[h][0], m1 = mw[h][1];
-                        floatx4 y0 = {0.f, 0.f, 0.f, 0.f}, y1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) {
-                            y0 = mfma4(m0[s4], hh[s4], y0);
-                            y1 = mfma4(m1[s4], hh[s4], y1);
+                        for (int r = 0; r < 4; ++r) {
+                            gv[r] = gelu_fast(h0[r]);
+                            gv[4 + r] = gelu_fast(h1[r]);
                         }
+                        const Split3 gs = split3(gv);
+                        const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+                        const floatx4 y0 = mfma_x6(f3.ld(Frag3::mp + wave), gs, zero);
+                        const floatx4 y1 = mfma_x6(f3.ld(Frag3::mp + 4 + wave), gs, zero);
                         if ((lane_id() & 15) == 0) {
-                            *reinterpret_cast<floatx4*>(&S.part_y[cj][4 * g]) = y0;
-                            *reinterpret_cast<floatx4*>(&S.part_y[cj][16 + 4 * g]) = y1;
+                            *reinterpret_cast<floatx4*>(&S.part_y[wave][4 * g]) = y0;
+                            *reinterpret_cast<floatx4*>(&S.part_y[wave][16 + 4 * g]) = y1;
                         }
                     }
                 }
@@ -679,7 +677,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     const int lane = lane_id(), g = lane >> 4;
                     floatx4 ya = ld4(W + PL::mp_b + 4 * g), yb = ld4(W + PL::mp_b + 16 + 4 * g);
 #pragma unroll
-                    for (int w = 0; w < kFF / 16; ++w) {
+                    for (int w = 0; w < kFF / 32; ++w) {
                         const floatx4 pa = ld4(&S.part_y[w][4 * g]), pb = ld4(&S.part_y[w][16 + 4 * g]);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {

@@ -315,50 +315,38 @@ __device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn
         }
 }
 
-// mlp_n with c_fc on the bf16 matrix cores (mfma_x6); mlp.c_proj stays on the fp32
-// MFMA (its input is produced per 16-unit chunk).
+// mlp_n on the bf16 matrix cores (mfma_x6): c_fc per 16-unit chunk, mlp.c_proj per
+// pair of chunks (its K = 32 input is the two chunks' gelu outputs, C-layout).
 template <int NB>
-__device__ inline void mlp3_n(const float* W, const FragSrc& fs, const FragSrc3& f3, const float (&xn)[2][8],
-                              float (&x)[2][8]) {
+__device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&x)[2][8]) {
     const int g = lane_id() >> 4;
     const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);
     floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
     Split3 xs[2];
 #pragma unroll
     for (int j = 0; j < NB; ++j) xs[j] = split3(xn[j]);
-    floatx4 h[2];
-    Split3 wn = f3.ld(Frag3::fc);
-    {
-        const floatx4 fb = ld4(W + PL::fc_b + 4 * g);
+#pragma unroll 1
+    for (int p = 0; p < kFF / 32; ++p) {
+        float gv[2][8];
 #pragma unroll
-        for (int j = 0; j < NB; ++j) h[j] = mfma_x6(wn, xs[j], fb);
-    }
-    if (kFF / 16 > 1) wn = f3.ld(Frag3::fc + 1);
-#pragma unroll
-    for (int c = 0; c < kFF / 16; ++c) {
-        const floatx4 b0 = fs.ld(FragOff::mp, c), b1 = fs.ld(FragOff::mp, 8 + c);
-        floatx4 hn[2] = {h[0], h[1]};
-        if (c + 1 < kFF / 16) {
-            const floatx4 fb = ld4(W + PL::fc_b + (c + 1) * 16 + 4 * g);
-            const Split3 wc = wn;
-            if (c + 2 < kFF / 16) wn = f3.ld(Frag3::fc + c + 2);
-#pragma unroll
-            for (int j = 0; j < NB; ++j) hn[j] = mfma_x6(wc, xs[j], fb);
-        }
-        floatx4 gl[2];
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) gl[j][r] = gelu_fast(h[j][r]);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int half = 0; half < 2; ++half) {
+            const int c = 2 * p + half;
+            const Split3 wc = f3.ld(Frag3::fc + c);
+            const floatx4 fb = ld4(W + PL::fc_b + c * 16 + 4 * g);
 #pragma unroll
             for (int j = 0; j < NB; ++j) {
-                y0[j] = mfma4(b0[s], gl[j][s], y0[j]);
-                y1[j] = mfma4(b1[s], gl[j][s], y1[j]);
+                const floatx4 h = mfma_x6(wc, xs[j], fb);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gv[j][4 * half + r] = gelu_fast(h[r]);
             }
-        h[0] = hn[0];
-        h[1] = hn[1];
+        }
+        const Split3 w0 = f3.ld(Frag3::mp + p), w1 = f3.ld(Frag3::mp + 4 + p);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const Split3 gs = split3(gv[j]);
+            y0[j] = mfma_x6(w0, gs, y0[j]);
+            y1[j] = mfma_x6(w1, gs, y1[j]);
+        }
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j)
@@ -367,6 +355,46 @@ __device__ inline void mlp3_n(const float* W, const FragSrc& fs, const FragSrc3&
             x[j][r] += y0[j][r];
             x[j][4 + r] += y1[j][r];
         }
+}
+
+// u = xn G + g0 of the NB blocks (the folded c_attn: only its q part) on mfma_x6
+template <int NB>
+__device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8]) {
+    const int g = lane_id() >> 4;
+    Split3 xs[2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) xs[j] = split3(xn[j]);
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob) {
+        const Split3 w = f3.ld(Frag3::attn + ob);
+        const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const floatx4 acc = mfma_x6(w, xs[j], bias);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) q[j][ob * 4 + r] = acc[r];
+        }
+    }
+}
+
+// attn_proj on mfma_x6: x^T += Wvp^T o^T + bvp
+template <int NB>
+__device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8]) {
+    const int g = lane_id() >> 4;
+    Split3 os[2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) os[j] = split3(o[j]);
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob) {
+        const Split3 w = f3.ld(Frag3::proj + ob);
+        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const floatx4 acc = mfma_x6(w, os[j], bias);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[j][ob * 4 + r] += acc[r];
+        }
+    }
 }
 
 // Folded attention input of the NB blocks qb[]: keys and values are the
