@@ -325,22 +325,27 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
     Split3 xs[2];
 #pragma unroll
     for (int j = 0; j < NB; ++j) xs[j] = split3(xn[j]);
-#pragma unroll 1
+    // c_fc tiles one pair ahead (in flight across the pair's split + c_proj products), the
+    // pair's c_proj tiles at its start (in flight across its c_fc + gelu)
+    Split3 wf0 = f3.ld(Frag3::fc), wf1 = f3.ld(Frag3::fc + 1);
+#pragma unroll
     for (int p = 0; p < kFF / 32; ++p) {
+        const Split3 w0 = f3.ld(Frag3::mp + p), w1 = f3.ld(Frag3::mp + 4 + p);
         float gv[2][8];
+        const floatx4 fb0 = ld4(W + PL::fc_b + 2 * p * 16 + 4 * g), fb1 = ld4(W + PL::fc_b + (2 * p + 1) * 16 + 4 * g);
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const int c = 2 * p + half;
-            const Split3 wc = f3.ld(Frag3::fc + c);
-            const floatx4 fb = ld4(W + PL::fc_b + c * 16 + 4 * g);
+        for (int j = 0; j < NB; ++j) {
+            const floatx4 h0 = mfma_x6(wf0, xs[j], fb0), h1 = mfma_x6(wf1, xs[j], fb1);
 #pragma unroll
-            for (int j = 0; j < NB; ++j) {
-                const floatx4 h = mfma_x6(wc, xs[j], fb);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) gv[j][4 * half + r] = gelu_fast(h[r]);
+            for (int r = 0; r < 4; ++r) {
+                gv[j][r] = gelu_fast(h0[r]);
+                gv[j][4 + r] = gelu_fast(h1[r]);
             }
         }
-        const Split3 w0 = f3.ld(Frag3::mp + p), w1 = f3.ld(Frag3::mp + 4 + p);
+        if (p + 1 < kFF / 32) {
+            wf0 = f3.ld(Frag3::fc + 2 * p + 2);
+            wf1 = f3.ld(Frag3::fc + 2 * p + 3);
+        }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             const Split3 gs = split3(gv[j]);
