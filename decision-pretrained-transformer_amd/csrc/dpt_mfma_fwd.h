@@ -91,18 +91,40 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 struct Split3 {
     bf16x8 h, m, l;
 };
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+__device__ inline floatx2 widen_bf16x2(bf16x2 b) {
+    const unsigned u = __builtin_bit_cast(unsigned, b);
+    return floatx2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+// pairwise: one v_cvt_pk_bf16_f32 (round to nearest even) per part and pair, the
+// residuals by packed subtraction
 __device__ inline Split3 split3(const float (&v)[8]) {
-    Split3 s;
+#ifdef DPT_EXP_SPLIT1  // timing only: hi part alone (wrong results)
+    Split3 t;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const __bf16 h = (__bf16)v[k];
-        const float r = v[k] - (float)h;
-        const __bf16 m = (__bf16)r;
-        s.h[k] = h;
-        s.m[k] = m;
-        s.l[k] = (__bf16)(r - (float)m);
+        t.h[k] = (__bf16)v[k];
+        t.m[k] = t.h[k];
+        t.l[k] = t.h[k];
     }
-    return s;
+    return t;
+#endif
+    unsigned hh[4], mm[4], ll[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const floatx2 x = {v[2 * p], v[2 * p + 1]};
+        const bf16x2 h = __builtin_convertvector(x, bf16x2);
+        const floatx2 r = x - widen_bf16x2(h);
+        const bf16x2 m = __builtin_convertvector(r, bf16x2);
+        const floatx2 q = r - widen_bf16x2(m);
+        hh[p] = __builtin_bit_cast(unsigned, h);
+        mm[p] = __builtin_bit_cast(unsigned, m);
+        ll[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(q, bf16x2));
+    }
+    return Split3{__builtin_bit_cast(bf16x8, uint4{hh[0], hh[1], hh[2], hh[3]}),
+                  __builtin_bit_cast(bf16x8, uint4{mm[0], mm[1], mm[2], mm[3]}),
+                  __builtin_bit_cast(bf16x8, uint4{ll[0], ll[1], ll[2], ll[3]})};
 }
 __device__ inline floatx4 mfma_bf16(const bf16x8& a, const bf16x8& b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -201,6 +223,9 @@ __device__ inline float gelu_fast(float x) {
     // = x / (1 + 2^(x * (c1 + c2 x^2))), z = sqrt(2/pi)(x + 0.044715 x^3), log2(e) folded in
     const float c1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
     const float c2 = c1 * 0.044715f;
+#ifdef DPT_EXP_NOGELU  // timing only (wrong results)
+    return x * c2;
+#endif
     const float e = __builtin_amdgcn_exp2f(x * fmaf(x * x, c2, c1));
     return x * __builtin_amdgcn_rcpf(1.0f + e);
 }

@@ -1,7 +1,8 @@
 """A/B of library builds (Makefile `variants`): one bandit rollout timing per library,
 each in its own process (python scripts/ab_lib.py libA.so libB.so ...; rounds alternate).
 An argument libX.so:<bytes> runs libX.so with dpt_hip.set_cache_budget(<bytes>); a suffix +b0 / +nob0
-runs it with dpt_hip.set_block0_mfma(True / False).
+runs it with dpt_hip.set_block0_mfma(True / False); +nows / +nomemo run DarkRoom without the
+layer-0 workspace / the logits memo (suffixes in that order: lib.so+nows+nomemo).
 Env: AB_H, AB_N, AB_A, AB_TILE, AB_ROUNDS."""
 import json
 import os
@@ -20,6 +21,8 @@ def child(lib):
     for suf, on in (("+nob0", False), ("+b0", True)):
         if lib.endswith(suf):
             lib, b0 = lib[: -len(suf)], on
+    nomemo = lib.endswith("+nomemo")  # DarkRoom with every step a window forward
+    lib = lib[: -len("+nomemo")] if nomemo else lib
     nows = lib.endswith("+nows")  # DarkRoom without the per-episode layer-0 workspace
     lib = lib[: -len("+nows")] if nows else lib
     _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.__file__), lib.split(":")[0])
@@ -30,6 +33,8 @@ def child(lib):
     dpt_hip.set_decode_tile(int(os.environ.get("AB_TILE", "8")))
     if b0 is not None:
         dpt_hip.set_block0_mfma(b0)
+    if nomemo:
+        dpt_hip.set_darkroom_memo(False)
     if nows:
         dpt_hip.set_darkroom_workspace(False)
     if ":" in lib:  # "libX.so:<bytes>": the same library at another DPT_TUNE_CACHE_BUDGET
