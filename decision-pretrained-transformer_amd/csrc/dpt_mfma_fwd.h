@@ -195,27 +195,25 @@ __device__ inline void bar_lds() {
 // 8 of them; the other 24 live in lanes l^16, l^32, l^48.
 __device__ inline void ln_cols(const float (&v)[8], float (&out)[8], const float* __restrict__ gam,
                                const float* __restrict__ bet) {
+    // pairwise (packed) sums, rstd by v_rsq: fp32-accurate, not the reference's summation order
+    typedef float fx2 __attribute__((ext_vector_type(2)));
     const int g = lane_id() >> 4;
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s += v[k];
-    s = sum_cols(s);
-    const float mean = s * (1.0f / kE);
-    float d[8], s2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        d[k] = v[k] - mean;
-        s2 += d[k] * d[k];
-    }
-    s2 = sum_cols(s2);
-    const float rstd = 1.0f / sqrtf(s2 * (1.0f / kE) + 1e-5f);
+    const fx2 v0 = {v[0], v[1]}, v1 = {v[2], v[3]}, v2 = {v[4], v[5]}, v3 = {v[6], v[7]};
+    const fx2 sa = (v0 + v1) + (v2 + v3);
+    const float mean = sum_cols(sa.x + sa.y) * (1.0f / kE);
+    const fx2 mm = {mean, mean};
+    const fx2 d0 = v0 - mm, d1 = v1 - mm, d2 = v2 - mm, d3 = v3 - mm;
+    const fx2 qa = (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    const float rstd = __builtin_amdgcn_rsqf(sum_cols(qa.x + qa.y) * (1.0f / kE) + 1e-5f);
+    const fx2 rr = {rstd, rstd};
     const floatx4 g0 = ld4(gam + 4 * g), g1 = ld4(gam + 16 + 4 * g);
     const floatx4 b0 = ld4(bet + 4 * g), b1 = ld4(bet + 16 + 4 * g);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        out[r] = fmaf(d[r] * rstd, g0[r], b0[r]);
-        out[4 + r] = fmaf(d[4 + r] * rstd, g1[r], b1[r]);
-    }
+    const fx2 o0 = __builtin_elementwise_fma(d0 * rr, fx2{g0[0], g0[1]}, fx2{b0[0], b0[1]});
+    const fx2 o1 = __builtin_elementwise_fma(d1 * rr, fx2{g0[2], g0[3]}, fx2{b0[2], b0[3]});
+    const fx2 o2 = __builtin_elementwise_fma(d2 * rr, fx2{g1[0], g1[1]}, fx2{b1[0], b1[1]});
+    const fx2 o3 = __builtin_elementwise_fma(d3 * rr, fx2{g1[2], g1[3]}, fx2{b1[2], b1[3]});
+    out[0] = o0.x; out[1] = o0.y; out[2] = o1.x; out[3] = o1.y;
+    out[4] = o2.x; out[5] = o2.y; out[6] = o3.x; out[7] = o3.y;
 }
 
 __device__ inline float gelu_fast(float x) {
