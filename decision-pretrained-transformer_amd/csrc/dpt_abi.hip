@@ -74,7 +74,7 @@ using namespace dpt;
 struct dpt_model {
     dpt_model_desc desc;
     float* blob;
-    float* frag;  // the blocks' weights in MFMA fragment order, attention folded (dpt_mfma_fwd.h FragOff)
+    float* frag;  // the blocks' weights split into bf16 parts in MFMA operand order, attention folded (dpt_mfma_fwd.h Frag3)
     float* l0;    // every block's attention folded (dpt_common.h L0Off)
     ModelView view;
 };
@@ -180,7 +180,7 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
         return DPT_ENOMEM;
     }
     rc = launch_derive_l0(view, l0, nullptr);
-    view.l0 = l0;  // the fragments pack the folded attention (dpt_mfma_fwd.h FragOff)
+    view.l0 = l0;  // the fragments pack the folded attention (dpt_mfma_fwd.h Frag3)
     if (!rc) rc = launch_pack_fragments(view, frag, nullptr);
     if (!rc) rc = check_hip(hipDeviceSynchronize(), "weight derivation");
     if (rc) {

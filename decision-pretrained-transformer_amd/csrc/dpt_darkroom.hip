@@ -4,7 +4,7 @@
 //
 // The query (current state) changes every step, so each step is a full causal
 // forward over the window [query, context transitions...] (models/net.py:41-60);
-// the prediction is the LAST position.  That is fp32-MFMA work: one workgroup
+// the prediction is the LAST position.  That is matrix-core work: one workgroup
 // owns one task for all Heps x horizon steps, and each wave owns 16 tokens of
 // the window (T <= 128).
 //
@@ -15,9 +15,10 @@
 // reads feature 16*(s>>2) + 4g + (s&3)), so c_attn, attention, c_proj, c_fc,
 // gelu and mlp.c_proj chain in registers; only K (token-major) and V
 // (feature-major) go through LDS, because every later token reads them.
-// Weights are the A operand, pre-packed per layer in fragment order (FragOff)
-// and read through one buffer descriptor, so one 16-B load per lane feeds four
-// MFMAs.
+// Weights are the A operand, split into bf16 parts and pre-packed per layer in
+// operand order (Frag3, pack_split_kernel) and read through one buffer
+// descriptor; every dense product runs as fp32-accurate split products on the
+// bf16 matrix cores (mfma_x6), the attention on the fp32 MFMA.
 //
 // Exact restructurings (same arithmetic up to fp32 summation order):
 //  * layer 0: within an episode the context tokens' layer-0 keys/values are
@@ -54,48 +55,6 @@ namespace dpt {
 constexpr int kDrA = 5;                     // DarkRoom actions
 constexpr int kDrF = 10;                    // token features 2*sd + A + 1
 constexpr int kMemoStates = 128;            // logits memo rows (grids up to 11 x 11)
-
-// A-operand fragment of W^T for a k=32 input (W is [in][out], Conv1D layout):
-// lane l, k-step s reads W[16*(s>>2) + 4*(l>>4) + (s&3)][ob*16 + (l&15)];
-// mlp.c_proj ([128][32]): chunk j, step s reads hidden 16j + 4*(l>>4) + s.
-// The attention is folded (FragOff): the attn region packs G ([E][E], tiles 0-1;
-// tiles 2-5 are zero) and the proj region Wvp, both from ModelView::l0.
-__global__ void pack_fragments_kernel(ModelView M, float* __restrict__ frag) {
-    const int total = M.n_layer * FragOff::size;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const int layer = i / FragOff::size;
-        int o = i % FragOff::size;
-        const float* W = M.layers + (size_t)layer * LayerOff::size;
-        const float* F = M.l0 + (size_t)layer * L0Off::size;
-        const float* src;
-        int n_out, in, out;
-        if (o < FragOff::mp) {
-            int base;
-            if (o < FragOff::proj) {
-                if (o >= FragOff::attn + 2 * 512) {  // tiles 2-5: unused in the folded form
-                    frag[i] = 0.f;
-                    continue;
-                }
-                base = FragOff::attn; src = F + L0Off::G; n_out = kE;
-            }
-            else if (o < FragOff::fc) { base = FragOff::proj; src = F + L0Off::Wvp; n_out = kE; }
-            else { base = FragOff::fc; src = W + LayerOff::fc_w; n_out = kFF; }
-            o -= base;
-            const int s4 = o & 3, lane = (o >> 2) & 63, q = (o >> 8) & 1, ob = o >> 9;
-            const int s = 4 * q + s4;
-            in = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
-            out = ob * 16 + (lane & 15);
-        } else {
-            o -= FragOff::mp;
-            src = W + LayerOff::mp_w;
-            const int s = o & 3, lane = (o >> 2) & 63, j = (o >> 8) & 7, ob = o >> 11;
-            in = 16 * j + 4 * (lane >> 4) + s;
-            out = ob * 16 + (lane & 15);
-            n_out = kE;
-        }
-        frag[i] = src[(size_t)in * n_out + out];
-    }
-}
 
 struct PTop {
     int lnf_g, lnf_b, head_w, head_b, emb_b, wpe0, emb_w, total;
@@ -271,11 +230,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     const float scale = 0.17677669529663687f;  // 1/sqrt(head_dim = 32)
     const int L = M.n_layer;
     const PTop pt = PTop::make(L);
-    const FragSrc frag0{__builtin_amdgcn_make_buffer_rsrc((void*)p.frag, (short)0, L * FragOff::size * 4, 0x00020000),
-                        0};
-    const FragSrc3 split0{__builtin_amdgcn_make_buffer_rsrc((void*)(p.frag + (size_t)L * FragOff::size), (short)0,
-                                                            L * Frag3::bytes, 0x00020000),
-                          0};
+    const FragSrc3 split0{__builtin_amdgcn_make_buffer_rsrc((void*)p.frag, (short)0, L * Frag3::bytes, 0x00020000), 0};
     load_layer_params(P, M, tid, blockDim.x);
     for (int i = tid; i < kE; i += blockDim.x) {
         P[pt.lnf_g + i] = M.lnf_g[i];
@@ -495,7 +450,6 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             for (int layer = 1; layer < L; ++layer) {
                 const bool last = layer == L - 1;
                 const float* W = P + layer * PL::size;
-                const FragSrc fs = frag0.layer(layer);
                 float q[2][8];
                 {
                     float xn[2][8];
@@ -508,7 +462,6 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
                         for (int j = 0; j < 2; ++j) {
                             if (j < nb && qb[j] == qlast) {
-                                const int one[2] = {qb[j], qb[j]};
                                 float xn1[2][8], q1[2][8];
 #pragma unroll
                                 for (int k = 0; k < 8; ++k) xn1[0][k] = xn[j][k];
@@ -753,7 +706,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     }
 }
 
-// The bf16 3-way split tiles (Frag3) of every layer, written after the fp32 fragments.
+// The model's fragment buffer: the bf16 3-way split weight tiles (Frag3) of every layer.
 __global__ void pack_split_kernel(ModelView M, unsigned short* __restrict__ out) {
     const int per_layer = Frag3::tiles * 64 * 8;
     const int total = M.n_layer * per_layer;
@@ -785,14 +738,11 @@ __global__ void pack_split_kernel(ModelView M, unsigned short* __restrict__ out)
 }
 
 int launch_pack_fragments(const ModelView& M, float* frag, hipStream_t st) {
-    hipLaunchKernelGGL(pack_fragments_kernel, dim3(64), dim3(256), 0, st, M, frag);
-    if (int rc = check_hip(hipGetLastError(), "pack_fragments_kernel launch")) return rc;
-    hipLaunchKernelGGL(pack_split_kernel, dim3(64), dim3(256), 0, st, M,
-                       reinterpret_cast<unsigned short*>(frag + (size_t)M.n_layer * FragOff::size));
+    hipLaunchKernelGGL(pack_split_kernel, dim3(64), dim3(256), 0, st, M, reinterpret_cast<unsigned short*>(frag));
     return check_hip(hipGetLastError(), "pack_split_kernel launch");
 }
 
-int64_t fragments_numel(int n_layer) { return (int64_t)n_layer * (FragOff::size + Frag3::bytes / 4); }
+int64_t fragments_numel(int n_layer) { return (int64_t)n_layer * Frag3::bytes / 4; }
 
 static bool g_darkroom_memo = true;  // DPT_TUNE_DARKROOM_MEMO
 

@@ -4,7 +4,7 @@
 // wave holds x^T of its blocks in registers as v_mfma_f32_16x16x4_f32 C-layout
 // fragments (lane (g = l>>4, c = l&15): features 16*blk + 4g + r of token c),
 // which is exactly the B operand of the next product W^T x^T.  Weights are the
-// A operand, pre-packed per layer in fragment order (FragOff); only K
+// A operand, split and pre-packed per layer in operand order (Frag3); only K
 // (token-major) and V (feature-major) go through LDS.
 #pragma once
 
@@ -17,18 +17,6 @@ constexpr int kFwdBlocks = 8;                // 16-token blocks per window (two 
 constexpr int kFwdT = 16 * kFwdBlocks;        // max window
 constexpr int kKStride = kE + 4;            // K[token][feature]
 constexpr int kVStride = kFwdT + 4;          // Vt[feature][token] (128-token buffer)
-
-// Fragment-packed weights of one block (floats), see pack_fragments_kernel.
-// The attention is folded (L0Off): the attn region's tiles 0-1 hold G (the u =
-// y G + g0 projection; tiles 2-5 are unused: keys and values are y itself) and
-// the proj region holds Wvp = Wv Wproj.
-struct FragOff {
-    static constexpr int attn = 0;            // [6 ob][2 q][64 lanes][4]
-    static constexpr int proj = attn + 3072;  // [2 ob][2 q][64][4]
-    static constexpr int fc = proj + 1024;    // [8 ob][2 q][64][4]
-    static constexpr int mp = fc + 4096;      // [2 ob][8 chunk][64][4]
-    static constexpr int size = mp + 4096;    // 12,288
-};
 
 // Small parameters copied to LDS once per launch (offsets in floats): per block
 // [ln1_g ln1_b attn_b proj_b ln2_g ln2_b fc_b mp_b], then the model-level ones.
@@ -58,23 +46,6 @@ __device__ inline int lane_id() {
     asm volatile("" : "+v"(t));
     return t & 63;
 }
-
-// Fragment-packed weights through one buffer descriptor: the per-lane part of
-// every address is lane*16; layer, region and block offsets are scalar.
-struct FragSrc {
-    __amdgpu_buffer_rsrc_t r;
-    int base;  // byte offset of this layer's block
-    __device__ floatx4 ld(int region_floats, int k) const {
-#ifdef DPT_FRAG_L1  // timing-only diagnostic build: every fragment load hits the first 4 KB (wrong results)
-        return __builtin_bit_cast(
-            floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, (base + 4 * region_floats + k * 1024) & 3072, 0));
-#else
-        return __builtin_bit_cast(
-            floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, base + 4 * region_floats + k * 1024, 0));
-#endif
-    }
-    __device__ FragSrc layer(int l) const { return FragSrc{r, l * FragOff::size * 4}; }
-};
 
 // ---- fp32 products on the bf16 matrix cores (emulated fp32, "x6").  A value is
 // split exactly into three bf16 parts, v = h + m + l + O(2^-24 v) (each residual is
@@ -139,7 +110,7 @@ __device__ inline floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 acc)
     return mfma_bf16(a.h, b.h, acc);
 }
 
-// The split weight tiles of one block (after the fp32 fragments of all layers):
+// The split weight tiles of one block (the model's fragment buffer, per layer):
 // [tile][part h|m|l][64 lanes][8 bf16], tile element (lane (g, c), j) = W[in][out]
 // with in = 16*(j>>2) + 4g + (j&3) (mp: hidden 32*pair + that) and out = 16*ob + c.
 struct Frag3 {
@@ -228,117 +199,13 @@ __device__ inline float gelu_fast(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
-// acc + W^T xin^T for a k=32 input held as 8 C-layout values, given fragments
-__device__ inline floatx4 mfma32(const floatx4& w0, const floatx4& w1, const float (&xin)[8], floatx4 acc) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma4(w0[s], xin[s], acc);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma4(w1[s], xin[4 + s], acc);
-    return acc;
-}
-
-// The same for the NB (1 or 2) blocks of a wave: one fragment load feeds NB
-// independent accumulation chains, interleaved.
-template <int NB>
-__device__ inline void mfma32n(const floatx4& w0, const floatx4& w1, const float (&xin)[2][8], floatx4 (&acc)[2]) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = mfma4(w0[s], xin[j][s], acc[j]);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = mfma4(w1[s], xin[j][4 + s], acc[j]);
-}
-
 template <int NB>
 __device__ inline void ln_n(const float (&x)[2][8], float (&xn)[2][8], const float* gam, const float* bet) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) ln_cols(x[j], xn[j], gam, bet);
 }
 
-// x^T += c_proj(o^T) (bias included)
-template <int NB>
-__device__ inline void attn_proj(const float* W, const FragSrc& fs, const float (&o)[2][8], float (&x)[2][8]) {
-    const int g = lane_id() >> 4;
-#pragma unroll
-    for (int ob = 0; ob < 2; ++ob) {
-        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g);
-        floatx4 acc[2] = {bias, bias};
-        mfma32n<NB>(fs.ld(FragOff::proj, 2 * ob), fs.ld(FragOff::proj, 2 * ob + 1), o, acc);
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) x[j][ob * 4 + r] += acc[j][r];
-    }
-}
-
-// x^T += MLP(xn^T) over the 8 hidden chunks, software-pipelined: the c_fc
-// MFMAs of chunk c+1 are issued interleaved with the gelu of chunk c (an MFMA
-// leaves most of its 32 issue cycles to independent vector instructions),
-// then chunk c's mlp.c_proj MFMAs.
-template <int NB>
-__device__ inline void mlp_n(const float* W, const FragSrc& fs, const float (&xn)[2][8], float (&x)[2][8]) {
-    const int g = lane_id() >> 4;
-    const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);
-    floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
-    floatx4 h[2];
-    // c_fc fragments of chunk c+1 are requested one chunk ahead (their L2 latency hides
-    // behind chunk c's MFMAs instead of stalling the chain; -0.6 % at config 3)
-    floatx4 fa = fs.ld(FragOff::fc, 2), fbq = fs.ld(FragOff::fc, 3);
-    {
-        const floatx4 fb = ld4(W + PL::fc_b + 4 * g);
-        h[0] = fb;
-        h[1] = fb;
-        mfma32n<NB>(fs.ld(FragOff::fc, 0), fs.ld(FragOff::fc, 1), xn, h);
-    }
-#pragma unroll
-    for (int c = 0; c < kFF / 16; ++c) {
-        const floatx4 b0 = fs.ld(FragOff::mp, c), b1 = fs.ld(FragOff::mp, 8 + c);
-        floatx4 hn[2] = {h[0], h[1]};
-        if (c + 1 < kFF / 16) {
-            const floatx4 fb = ld4(W + PL::fc_b + (c + 1) * 16 + 4 * g);
-            hn[0] = fb;
-            hn[1] = fb;
-            const floatx4 wa = fa, wb = fbq;
-            if (c + 2 < kFF / 16) {
-                fa = fs.ld(FragOff::fc, 2 * (c + 2));
-                fbq = fs.ld(FragOff::fc, 2 * (c + 2) + 1);
-            }
-            mfma32n<NB>(wa, wb, xn, hn);
-        }
-        floatx4 gl[2];
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) gl[j][r] = gelu_fast(h[j][r]);
-        if (c + 1 < kFF / 16) {
-#pragma unroll
-            for (int k = 0; k < 8 * NB; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      // one c_fc(c+1) MFMA
-                __builtin_amdgcn_sched_group_barrier(0x002, 4 / NB, 0);  // gelu(c) VALU
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int j = 0; j < NB; ++j) {
-                y0[j] = mfma4(b0[s], gl[j][s], y0[j]);
-                y1[j] = mfma4(b1[s], gl[j][s], y1[j]);
-            }
-        h[0] = hn[0];
-        h[1] = hn[1];
-    }
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            x[j][r] += y0[j][r];
-            x[j][4 + r] += y1[j][r];
-        }
-}
-
-// mlp_n on the bf16 matrix cores (mfma_x6): c_fc per 16-unit chunk, mlp.c_proj per
+// x^T += MLP(xn^T) on the bf16 matrix cores (mfma_x6): c_fc per 16-unit chunk, mlp.c_proj per
 // pair of chunks (its K = 32 input is the two chunks' gelu outputs, C-layout).
 template <int NB>
 __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&x)[2][8]) {
@@ -440,33 +307,6 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
                 floatx4{xn[j][4 * blk], xn[j][4 * blk + 1], xn[j][4 * blk + 2], xn[j][4 * blk + 3]};
 #pragma unroll
             for (int r = 0; r < 4; ++r) S.Vt[16 * blk + 4 * g + r][tok] = xn[j][4 * blk + r];
-        }
-    }
-}
-
-// c_attn output blocks [ob0, ob1) of (Q0 Q1 K0 K1 V0 V1) for the NB blocks qb[]:
-// Q stays in registers, K -> LDS token-major, V -> LDS feature-major.  With the
-// folded fragments only [0, 2) is used: "Q" is then u = y G + g0.
-template <int NB, class KV>
-__device__ inline void c_attn_n(KV& S, const float* W, const FragSrc& fs, const int (&qb)[2],
-                                const float (&xn)[2][8], float (&q)[2][8], int ob0, int ob1) {
-    for (int ob = ob0; ob < ob1; ++ob) {
-        const int lane = lane_id(), g = lane >> 4;
-        const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);
-        floatx4 acc[2] = {bias, bias};
-        mfma32n<NB>(fs.ld(FragOff::attn, 2 * ob), fs.ld(FragOff::attn, 2 * ob + 1), xn, acc);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const int tok = qb[j] * 16 + (lane & 15);
-            if (ob < 2) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) q[j][ob * 4 + r] = acc[j][r];
-            } else if (ob < 4) {
-                *reinterpret_cast<floatx4*>(&S.K[tok][16 * (ob - 2) + 4 * g]) = acc[j];
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) S.Vt[16 * (ob - 4) + 4 * g + r][tok] = acc[j][r];
-            }
         }
     }
 }

@@ -61,8 +61,7 @@ prefill_kernel(ModelView M, PrefillArgs a) {
     const int T = a.C + 1;
     const float scale = 0.17677669529663687f;  // 1/sqrt(head_dim = 32)
     const PfTop pt = PfTop::make(L, F, A);
-    const FragSrc frag0{__builtin_amdgcn_make_buffer_rsrc((void*)a.frag, (short)0, L * FragOff::size * 4, 0x00020000),
-                        0};
+    const FragSrc3 split0{__builtin_amdgcn_make_buffer_rsrc((void*)a.frag, (short)0, L * Frag3::bytes, 0x00020000), 0};
     load_layer_params(P, M, tid, blockDim.x);
     for (int i = tid; i < kE; i += blockDim.x) {
         P[pt.lnf_g + i] = M.lnf_g[i];
@@ -109,11 +108,11 @@ prefill_kernel(ModelView M, PrefillArgs a) {
 
     for (int layer = 0; layer < L; ++layer) {
         const float* W = P + layer * PL::size;
-        const FragSrc fs = frag0.layer(layer);
+        const FragSrc3 fs = split0.layer(layer);
         float q[2][8];
         {
             float xn[2][8];
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), c_attn_n<NB>(S, W, fs, qb, xn, q, 0, 2),
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), u_proj3_n<NB>(W, fs, xn, q),
                             kv_from_y<NB>(S, qb, xn)));
         }
         bar_lds();
@@ -128,12 +127,12 @@ prefill_kernel(ModelView M, PrefillArgs a) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) o[j][k] *= inv;
             }
-            DPT_BLOCKS(nb, attn_proj<NB>(W, fs, o, x));
+            DPT_BLOCKS(nb, attn_proj3<NB>(W, fs, o, x));
         }
         bar_lds();  // every read of this layer's K/V is done
         {
             float xn[2][8];
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b), mlp_n<NB>(W, fs, xn, x)));
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b), mlp3_n<NB>(W, fs, xn, x)));
         }
     }
 
