@@ -400,7 +400,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
                             for (int k = 0; k < 8; ++k) {
                                 const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
-                                S.k0[d] = S.kv.K[0][d];
+                                S.k0[d] = S.kv.Vt[d][0];  // folded attention: key = value = y
                                 S.v0[d] = S.kv.Vt[d][0];
                             }
                         }
@@ -522,6 +522,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     for (int h = 0; h < 2; ++h) {
                         const int kt = wave + 4 * h;
                         if (kt > qlast) break;
+#ifndef DPT_ATTN_F32
+                        // split key tile x the split query, broadcast to every column
+                        const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
+                        const Split3 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane], S.kv.KS[kt][2][lane]};
+                        const floatx4 sc = mfma_x6(ks, split3(qv), floatx4{0.f, 0.f, 0.f, 0.f});
+#else
                         const floatx4 k0 = ld4(&S.kv.K[kt * 16 + c][4 * g]);
                         const floatx4 k1 = ld4(&S.kv.K[kt * 16 + c][16 + 4 * g]);
                         floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
@@ -531,6 +537,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             sb = mfma4(k1[s4], qc[s4], sb);
                         }
                         const floatx4 sc = sa + sb;
+#endif
                         float sv[4], mt = -INFINITY;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {

@@ -24,13 +24,24 @@ struct PL {
     static constexpr int ln1_g = 0, ln1_b = 32, attn_b = 64, proj_b = 160, ln2_g = 192, ln2_b = 224,
                          fc_b = 256, mp_b = 384, size = 416;
 };
-// This workgroup's keys and values of the current layer, for windows of up to TMAX tokens.
-template <int TMAX>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// This workgroup's keys and values of the current layer, for windows of up to TMAX
+// tokens.  Keys are either fp32 token-major (K) or, with SPLITK, the split bf16 A
+// operand tiles of the score product (KS[block][part h|m|l][lane], written once by
+// the lane that computed the key: 3 KB per 16 keys instead of 2.25 KB, no split per
+// read).  Values stay fp32 feature-major (Vt).
+template <int TMAX, bool SPLITK = false>
 struct KVBuf {
-    float K[TMAX][kKStride];
+    static constexpr bool kSplitK = SPLITK;
+    float K[SPLITK ? 1 : TMAX][kKStride];
+    bf16x8 KS[SPLITK ? TMAX / 16 : 1][3][64];
     float Vt[kE][TMAX + 4];
 };
-using KVLds = KVBuf<kFwdT>;
+#ifndef DPT_ATTN_F32
+using KVLds = KVBuf<kFwdT, true>;
+#else
+using KVLds = KVBuf<kFwdT, false>;
+#endif
 
 __device__ inline floatx4 mfma4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -58,7 +69,6 @@ __device__ inline int lane_id() {
 // supplies its 8 C-layout values (features 16*(j>>2) + 4g + (j&3), j = 0..7) as the
 // 8 k-elements of its lane group; the weights are packed with the same k order
 // (Frag3), so the logical k permutation cancels.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 struct Split3 {
     bf16x8 h, m, l;
 };
@@ -301,10 +311,17 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const int tok = qb[j] * 16 + (lane & 15);
+        if constexpr (KV::kSplitK) {  // the lane's 8 values are its A-operand k-elements
+            const Split3 ks = split3(xn[j]);
+            S.KS[qb[j]][0][lane] = ks.h;
+            S.KS[qb[j]][1][lane] = ks.m;
+            S.KS[qb[j]][2][lane] = ks.l;
+        }
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
-            *reinterpret_cast<floatx4*>(&S.K[tok][16 * blk + 4 * g]) =
-                floatx4{xn[j][4 * blk], xn[j][4 * blk + 1], xn[j][4 * blk + 2], xn[j][4 * blk + 3]};
+            if constexpr (!KV::kSplitK)
+                *reinterpret_cast<floatx4*>(&S.K[tok][16 * blk + 4 * g]) =
+                    floatx4{xn[j][4 * blk], xn[j][4 * blk + 1], xn[j][4 * blk + 2], xn[j][4 * blk + 3]};
 #pragma unroll
             for (int r = 0; r < 4; ++r) S.Vt[16 * blk + 4 * g + r][tok] = xn[j][4 * blk + r];
         }
@@ -326,10 +343,27 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     // and lsum, which shortens the per-tile chain (the test is one wave vote).
     constexpr float kSlack = 32.f;
     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
+#ifndef DPT_ATTN_F32
+    const Split3 qs = split3(q);
+#endif
     m = -INFINITY;
     lsum = 0.f;
     floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
     for (int kb = 0; kb <= qb; ++kb) {
+#ifndef DPT_ATTN_F32
+        // S^T = K Q^T on mfma_x6: the key tile is the A operand (lane (g, c): key
+        // 16 kb + c, the lane group's 8 features), Q^T the B operand (q's C-layout)
+        Split3 ks;
+        if constexpr (KV::kSplitK) {
+            ks = Split3{S.KS[kb][0][lane], S.KS[kb][1][lane], S.KS[kb][2][lane]};
+        } else {
+            const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
+            const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
+            const float kv[8] = {k0[0], k0[1], k0[2], k0[3], k1[0], k1[1], k1[2], k1[3]};
+            ks = split3(kv);
+        }
+        const floatx4 sc = mfma_x6(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
+#else
         const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
         const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
         // two independent 4-deep chains (features 0-15 / 16-31) instead of one 8-deep
@@ -340,6 +374,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
             sb = mfma4(k1[s], q[4 + s], sb);
         }
         const floatx4 sc = sa + sb;
+#endif
         float sv[4];
         float mt = -INFINITY;
 #pragma unroll
