@@ -73,14 +73,18 @@ struct PTop {
     }
 };
 
-// 16-B multiple: the dynamic parameter block P follows it and is read with 16-B loads
+// 16-B multiple: the dynamic parameter block P follows it and is read with 16-B loads.
+// kWs (a per-task workspace is given): the layer-0 partials live in the workspace and
+// the freed LDS holds the values as split tiles (both attention products on mfma_x6);
+// without one they stay here and the values are fp32.
+template <bool kWs>
 struct alignas(16) DrSmem {
-    KVLds kv;
+    KVBuf<kFwdT, kSplitKeys, kSplitKeys && kWs> kv;
     int2 ctx[kFwdT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
     int2 cur[kFwdT];   // this episode's transitions
     // layer-0 episode cache: the causal softmax partial of every token over keys
     // 1..t, unnormalised o^T in C-layout per (block, lane), m and l per token
-    float l0o[kFwdBlocks][64][8];
+    float l0o[kWs ? 1 : kFwdBlocks][64][8];
     float l0m[kFwdT], l0l[kFwdT];
     float k0[kE], v0[kE];             // layer 0: key / value of the query token
     float ql[kE], xl[kE];             // last layer: q and residual of token T-1
@@ -121,9 +125,10 @@ struct DarkroomParams {
 // (embedding + wpe) and queries (u = LN1(x) G + g0) are fixed, so the episode
 // prologue stores them and every step reloads them instead of re-embedding and
 // re-projecting; only the query token (position 0) is recomputed.  Layout per task:
-// [x | u][block][lane][8] fp32, each lane's 8 C-layout values contiguous (2 x 16 B).
+// [x | u | o][block][lane][8] fp32, each lane's 8 C-layout values contiguous (2 x 16 B);
+// o is the layer-0 episode partial (the prologue's attention over keys 1..t).
 // The workspace starts with the per-state table (kDrTab floats), then the task caches.
-constexpr int kDrWsPerTask = 2 * kFwdBlocks * 64 * 8;
+constexpr int kDrWsPerTask = 3 * kFwdBlocks * 64 * 8;  // [x | u | layer-0 partial o]
 constexpr int kDrTabPerState = 2 * 4 * 8;
 constexpr int kDrTab = kMemoStates * kDrTabPerState;
 __device__ inline float* l0_cache(const DarkroomParams& p, int task, int which, int blk) {
@@ -145,7 +150,8 @@ __device__ inline void ws_load(const float* d, float (&v)[8]) {
 // Token embeddings of block qb (embed_transition + wpe, models/net.py:52-54):
 // the query [state, 0...] at position 0, context transitions after it, zeros
 // past the window.
-__device__ inline void embed_block(const DrSmem& S, const float* P, const PTop& pt, const float* wpe, int qb, int T,
+template <class Smem>
+__device__ inline void embed_block(const Smem& S, const float* P, const PTop& pt, const float* wpe, int qb, int T,
                                    float (&x)[8]) {
     const int lane = lane_id(), g = lane >> 4, tok = qb * 16 + (lane & 15);
 #pragma unroll
@@ -219,9 +225,11 @@ __global__ void __launch_bounds__(64) state_tables_kernel(ModelView M, int dim, 
     }
 }
 
+template <bool kWs>
 __global__ void __launch_bounds__(kFwdWaves * 64, 2)
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
-    __shared__ DrSmem S;
+    __shared__ DrSmem<kWs> S;
+    constexpr bool kSplitV = decltype(S.kv)::kSplitV;
     extern __shared__ float P[];
     const int task = blockIdx.x;
     const int tid = threadIdx.x;
@@ -241,6 +249,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     for (int i = tid; i < kE * kDrA; i += blockDim.x)  // transposed to [a][E] for 16-B reads
         P[pt.head_w + (i % kDrA) * kE + i / kDrA] = M.head_w[i];
     for (int i = tid; i < kDrA; i += blockDim.x) P[pt.head_b + i] = M.head_b[i];
+    if constexpr (kSplitV) {  // finite values in tiles no episode has written yet (attend)
+        uint4* vs = reinterpret_cast<uint4*>(&S.kv.VS[0][0][0][0]);
+        for (int i = tid; i < (int)(sizeof(S.kv.VS) / 16); i += blockDim.x) vs[i] = uint4{0u, 0u, 0u, 0u};
+    }
     for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
 
     // the task's goal and action permutation, once (wave-uniform: scalar registers), not
@@ -298,8 +310,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 float m, l, o[8];
                 attend(S.kv, q[j], qb[j], 1, scale, m, l, o);
                 const int lane = lane_id();
-                *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][0]) = {o[0], o[1], o[2], o[3]};
-                *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][4]) = {o[4], o[5], o[6], o[7]};
+                if constexpr (kWs) {
+                    ws_store(l0_cache(p, task, 2, qb[j]), o);
+                } else {
+                    *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][0]) = {o[0], o[1], o[2], o[3]};
+                    *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][4]) = {o[4], o[5], o[6], o[7]};
+                }
                 if (lane < 16) {
                     S.l0m[qb[j] * 16 + lane] = m;
                     S.l0l[qb[j] * 16 + lane] = l;
@@ -396,12 +412,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     if (wave == 0) {  // block 0 (slot 0 of wave 0): key/value (= y) of the query token
                         kv_from_y<1>(S.kv, qb, xn);
                         const int lane = lane_id();
-                        if ((lane & 15) == 0) {
+                        if ((lane & 15) == 0) {  // token 0's y (folded attention: key = value = y)
 #pragma unroll
                             for (int k = 0; k < 8; ++k) {
                                 const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
-                                S.k0[d] = S.kv.Vt[d][0];  // folded attention: key = value = y
-                                S.v0[d] = S.kv.Vt[d][0];
+                                S.k0[d] = xn[0][k];
+                                S.v0[d] = xn[0][k];
                             }
                         }
                     }
@@ -433,7 +449,15 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         const float mn = fmaxf(mt, s0);
                         const float ea = __expf(mt - mn), eb = __expf(s0 - mn);
                         const float inv = 1.0f / (lt * ea + eb);
-                        const floatx4 oa = ld4(&S.l0o[qb[j]][lane][0]), ob = ld4(&S.l0o[qb[j]][lane][4]);
+                        floatx4 oa, ob;
+                        if constexpr (kWs) {
+                            const float* po = l0_cache(p, task, 2, qb[j]);
+                            oa = ld4(po);
+                            ob = ld4(po + 4);
+                        } else {
+                            oa = ld4(&S.l0o[qb[j]][lane][0]);
+                            ob = ld4(&S.l0o[qb[j]][lane][4]);
+                        }
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             o[j][r] = (oa[r] * ea + va[r] * eb) * inv;
@@ -514,8 +538,58 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 static_assert(kFF / 32 == kFwdWaves, "one pair of hidden chunks per wave");
                 const Split3 pj0 = f3.ld(Frag3::proj), pj1 = f3.ld(Frag3::proj + 1);
                 const Split3 fj0 = f3.ld(Frag3::fc + 2 * wave), fj1 = f3.ld(Frag3::fc + 2 * wave + 1);
-                // (1) key tiles wave and wave+4 of the attention, as flash partials (m, l, o)
-                {
+                // (1) the attention as flash partials (m, l, o): with split values key
+                // tiles 2 wave and 2 wave + 1 (one pair, both products on mfma_x6), else
+                // key tiles wave and wave + 4
+                const int nparts = kSplitV ? (qlast >> 1) + 1 : qlast + 1;
+                if constexpr (kSplitV) {
+                    const int lane = lane_id(), g = lane >> 4, c = lane & 15;
+                    const int kb = 2 * wave;
+                    if (kb <= qlast) {
+                        const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
+                        const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
+                        const Split3 qs = split3(qv);  // the query, broadcast to every column
+                        float sv[8], mt = -INFINITY;
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int kt = kb + h;
+                            if (kt > qlast) {
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
+                                continue;
+                            }
+                            const Split3 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane], S.kv.KS[kt][2][lane]};
+                            const floatx4 sc = mfma_x6(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const float sr = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * scale : -INFINITY;
+                                sv[4 * h + r] = sr;
+                                mt = fmaxf(mt, sr);
+                            }
+                        }
+                        mt = max_cols(mt);
+                        float pr[8];
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) pr[r] = __expf(sv[r] - mt);
+                        float lt = ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
+                        lt = sum_cols(lt);
+                        const Split3 ps = split3(pr);
+                        const int pp = wave;
+                        const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+                        const floatx4 o0 = mfma_x6(Split3{S.kv.VS[pp][0][0][lane], S.kv.VS[pp][0][1][lane],
+                                                          S.kv.VS[pp][0][2][lane]}, ps, zero);
+                        const floatx4 o1 = mfma_x6(Split3{S.kv.VS[pp][1][0][lane], S.kv.VS[pp][1][1][lane],
+                                                          S.kv.VS[pp][1][2][lane]}, ps, zero);
+                        if (c == 0) {
+                            *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
+                            *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;
+                        }
+                        if (lane == 0) {
+                            S.part_m[wave] = mt;
+                            S.part_l[wave] = lt;
+                        }
+                    }
+                } else {
                     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
                     const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
 #pragma unroll
@@ -531,6 +605,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         const floatx4 k0 = ld4(&S.kv.K[kt * 16 + c][4 * g]);
                         const floatx4 k1 = ld4(&S.kv.K[kt * 16 + c][16 + 4 * g]);
                         floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+                        (void)lane;
 #pragma unroll
                         for (int s4 = 0; s4 < 4; ++s4) {
                             sa = mfma4(k0[s4], qa[s4], sa);
@@ -575,10 +650,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 {
                     const int g = lane_id() >> 4;
                     float mx = -INFINITY;
-                    for (int w = 0; w <= qlast; ++w) mx = fmaxf(mx, S.part_m[w]);
+                    for (int w = 0; w < nparts; ++w) mx = fmaxf(mx, S.part_m[w]);
                     float lsum = 0.f;
                     floatx4 oa = {0.f, 0.f, 0.f, 0.f}, ob = {0.f, 0.f, 0.f, 0.f};
-                    for (int w = 0; w <= qlast; ++w) {
+                    for (int w = 0; w < nparts; ++w) {
                         const float e = __expf(S.part_m[w] - mx);
                         lsum += S.part_l[w] * e;
                         const floatx4 pa = ld4(&S.part_o[w][4 * g]), pb = ld4(&S.part_o[w][16 + 4 * g]);
@@ -667,7 +742,11 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
                     if (lane == 0) {
                         double q[kDrA] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#ifdef DPT_EXP_NOCDF  // timing only (wrong results): no softmax cdf
+                        if (p.sample) q[0] = lg[0];
+#else
                         if (p.sample) cdf_fixed<kDrA>(lg, p.temp, q);
+#endif
                         if (p.memo) {
                             const int sidx = sx * p.dim + sy;
 #pragma unroll
@@ -788,18 +867,20 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
         return DPT_EUNSUPPORTED;
     }
     const size_t dyn = sizeof(float) * (size_t)PTop::make(M.n_layer).total;
-    if (dyn + sizeof(DrSmem) > 160 * 1024) {
+    const bool ws = a.workspace != nullptr;
+    const void* kern = ws ? reinterpret_cast<const void*>(rollout_darkroom_kernel<true>)
+                          : reinterpret_cast<const void*>(rollout_darkroom_kernel<false>);
+    if (dyn + (ws ? sizeof(DrSmem<true>) : sizeof(DrSmem<false>)) > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "n_layer=%d: parameter block does not fit in LDS", M.n_layer);
         return DPT_EUNSUPPORTED;
     }
-    if (dyn > 64 * 1024)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rollout_darkroom_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    if (dyn > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
     if (p.tab) {
         hipLaunchKernelGGL(state_tables_kernel, dim3(a.dim * a.dim), dim3(64), 0, st, M, a.dim, a.workspace);
         if (int rc = check_hip(hipGetLastError(), "state_tables_kernel launch")) return rc;
     }
-    hipLaunchKernelGGL(rollout_darkroom_kernel, dim3(a.N), dim3(kFwdWaves * 64), dyn, st, M, p);
+    if (ws) hipLaunchKernelGGL(rollout_darkroom_kernel<true>, dim3(a.N), dim3(kFwdWaves * 64), dyn, st, M, p);
+    else hipLaunchKernelGGL(rollout_darkroom_kernel<false>, dim3(a.N), dim3(kFwdWaves * 64), dyn, st, M, p);
     return check_hip(hipGetLastError(), "rollout_darkroom_kernel launch");
 }
 

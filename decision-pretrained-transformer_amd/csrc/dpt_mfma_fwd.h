@@ -30,17 +30,23 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // operand tiles of the score product (KS[block][part h|m|l][lane], written once by
 // the lane that computed the key: 3 KB per 16 keys instead of 2.25 KB, no split per
 // read).  Values stay fp32 feature-major (Vt).
-template <int TMAX, bool SPLITK = false>
+// With SPLITV (requires SPLITK) the values are kept as the split A operand of
+// O^T += V^T P^T over a pair of key tiles: VS[pair][feature half][part][lane (g, c)],
+// element j = V[key 16 (2 pair + (j >> 2)) + 4g + (j & 3)][feature 16 half + c] (the
+// lane group's k order of P^T's C-layout over the two tiles), 6 KB per 32 keys.
+template <int TMAX, bool SPLITK = false, bool SPLITV = false>
 struct KVBuf {
-    static constexpr bool kSplitK = SPLITK;
+    static_assert(SPLITK || !SPLITV, "split values need split keys");
+    static constexpr bool kSplitK = SPLITK, kSplitV = SPLITV;
     float K[SPLITK ? 1 : TMAX][kKStride];
-    bf16x8 KS[SPLITK ? TMAX / 16 : 1][3][64];
-    float Vt[kE][TMAX + 4];
+    bf16x8 KS[SPLITK ? TMAX / 16 : 1][SPLITK ? 3 : 1][SPLITK ? 64 : 1];  // (16 B when unused)
+    bf16x8 VS[SPLITV ? TMAX / 32 : 1][SPLITV ? 2 : 1][SPLITV ? 3 : 1][SPLITV ? 64 : 1];
+    float Vt[SPLITV ? 1 : kE][TMAX + 4];
 };
 #ifndef DPT_ATTN_F32
-using KVLds = KVBuf<kFwdT, true>;
+constexpr bool kSplitKeys = true;  // scores (and, with SPLITV, PV) on mfma_x6
 #else
-using KVLds = KVBuf<kFwdT, false>;
+constexpr bool kSplitKeys = false;
 #endif
 
 __device__ inline floatx4 mfma4(float a, float b, floatx4 c) {
@@ -316,14 +322,28 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
             S.KS[qb[j]][0][lane] = ks.h;
             S.KS[qb[j]][1][lane] = ks.m;
             S.KS[qb[j]][2][lane] = ks.l;
+            if constexpr (KV::kSplitV) {
+                // the same split values, scattered into V^T's pair-tile order: value k of
+                // lane (g, c) is feature 16 (k >> 2) + 4g + (k & 3) of token 16 b + c
+                const int b = qb[j], c = lane & 15;
+                __bf16* vs = reinterpret_cast<__bf16*>(&S.VS[b >> 1][0][0][0]);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int off = ((k >> 2) * 3 * 64 + (c >> 2) * 16 + 4 * g + (k & 3)) * 8 + (b & 1) * 4 + (c & 3);
+                    vs[off] = ks.h[k];
+                    vs[off + 64 * 8] = ks.m[k];
+                    vs[off + 2 * 64 * 8] = ks.l[k];
+                }
+            }
         }
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
             if constexpr (!KV::kSplitK)
                 *reinterpret_cast<floatx4*>(&S.K[tok][16 * blk + 4 * g]) =
                     floatx4{xn[j][4 * blk], xn[j][4 * blk + 1], xn[j][4 * blk + 2], xn[j][4 * blk + 3]};
+            if constexpr (!KV::kSplitV)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) S.Vt[16 * blk + 4 * g + r][tok] = xn[j][4 * blk + r];
+                for (int r = 0; r < 4; ++r) S.Vt[16 * blk + 4 * g + r][tok] = xn[j][4 * blk + r];
         }
     }
 }
@@ -345,6 +365,68 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
 #ifndef DPT_ATTN_F32
     const Split3 qs = split3(q);
+    if constexpr (KV::kSplitV) {
+        // both products on mfma_x6, key tiles in pairs: per tile S^T = K Q^T, per pair
+        // and feature half O^T += V^T P^T with K = the pair's 32 keys (P^T's C-layout of
+        // the two tiles is the B operand as it stands).  An unpaired last tile reads the
+        // pair's second tile from LDS with probability 0 (the rollout zeroes VS at launch,
+        // so it holds finite values).  The softmax reference moves as in the per-tile
+        // form below (kSlack, one vote per pair).
+        m = -INFINITY;
+        lsum = 0.f;
+        floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+        for (int kb = 0; kb <= qb; kb += 2) {
+            float sv[8];
+            float mt = -INFINITY;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int kt = kb + h;
+                if (kt > qb) {  // wave-uniform
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
+                    continue;
+                }
+                const Split3 ks{S.KS[kt][0][lane], S.KS[kt][1][lane], S.KS[kt][2][lane]};
+                const floatx4 sc = mfma_x6(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = kt * 16 + 4 * g + r;
+                    float sr = sc[r] * scale;
+                    if ((kt == qb && 4 * g + r > c) || key < key_lo) sr = -INFINITY;
+                    sv[4 * h + r] = sr;
+                    mt = fmaxf(mt, sr);
+                }
+            }
+            if (__builtin_amdgcn_ballot_w64(mt > m + kSlack)) {  // wave-uniform
+                mt = max_cols(mt);
+                const float mn = fmaxf(m, mt);
+                const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+                lsum *= corr;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    o0[r] *= corr;
+                    o1[r] *= corr;
+                }
+                m = mn;
+            }
+            const float base = m == -INFINITY ? 0.f : m;  // no key yet: keep 0, not NaN
+            float pr[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) pr[r] = __expf(sv[r] - base);
+            lsum += ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
+            const Split3 ps = split3(pr);
+            const int pp = kb >> 1;
+            o0 = mfma_x6(Split3{S.VS[pp][0][0][lane], S.VS[pp][0][1][lane], S.VS[pp][0][2][lane]}, ps, o0);
+            o1 = mfma_x6(Split3{S.VS[pp][1][0][lane], S.VS[pp][1][1][lane], S.VS[pp][1][2][lane]}, ps, o1);
+        }
+        lsum = sum_cols(lsum);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            o[r] = o0[r];
+            o[4 + r] = o1[r];
+        }
+        return;
+    }
 #endif
     m = -INFINITY;
     lsum = 0.f;
@@ -401,12 +483,17 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
 #pragma unroll
         for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - base);
         lsum += (pr[0] + pr[1]) + (pr[2] + pr[3]);
+#ifdef DPT_EXP_NOPV  // timing only (wrong results): no PV product
+        o0[0] += pr[0] + pr[1];
+        o1[0] += pr[2] + pr[3];
+#else
         const floatx4 v0 = ld4(&S.Vt[c][kb * 16 + 4 * g]);
         const floatx4 v1 = ld4(&S.Vt[16 + c][kb * 16 + 4 * g]);
 #pragma unroll
         for (int s = 0; s < 4; ++s) o0 = mfma4(v0[s], pr[s], o0);
 #pragma unroll
         for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
+#endif
     }
     lsum = sum_cols(lsum);
 #pragma unroll

@@ -325,8 +325,9 @@ typedef struct dpt_darkroom_rollout_args {
     float* logits_out;          /* (Heps*horizon, N, 5) or NULL */
     int32_t* forwards_out;      /* (N, Heps) window forwards run per task and episode, or NULL */
     float* workspace;           /* dpt_darkroom_workspace_numel(N) floats, or NULL: the context
-                                 * tokens' layer-0 inputs and queries, fixed within an episode,
-                                 * are kept there instead of recomputed every step */
+                                 * tokens' layer-0 inputs, queries and attention partials, fixed
+                                 * within an episode, are kept there instead of recomputed every
+                                 * step (or kept in LDS: the partials) */
 } dpt_darkroom_rollout_args;
 
 int dpt_darkroom_workspace_numel(int32_t N, int64_t* numel_out_host);

@@ -569,13 +569,17 @@ def test_regret_moments_match_scipy(N, H):
         np.testing.assert_allclose(st[k].cpu().numpy(), v, rtol=1e-10, atol=1e-12)
 
 
-def test_rollout_darkroom_workspace_bit_identical():
-    """The per-episode layer-0 workspace (context tokens' inputs and queries kept instead of
-    recomputed each step) changes nothing: actions, logits and returns are bit-identical."""
+def test_rollout_darkroom_workspace_matches_lds_path():
+    """With the per-episode workspace (context tokens' layer-0 inputs, queries and attention
+    partials kept instead of recomputed each step) the rollout keeps the values as split tiles
+    and runs both attention products on the split bf16 matrix cores; without it the values stay
+    fp32 and P V runs on 16x16x4_f32.  Same forward up to fp32 rounding: per task the logits agree
+    within the 1e-5 bar up to the first step whose sampled action differs (a uniform within
+    rounding of a cdf edge), and such divergences are rare."""
     import dpt_hip
     _, m, _ = model_from_golden("darkroom")
     rs = np.random.RandomState(23)
-    N = 300
+    N, steps = 300, 400
     goals = rs.randint(0, 10, (N, 2))
     outs = []
     try:
@@ -585,5 +589,11 @@ def test_rollout_darkroom_workspace_bit_identical():
             outs.append({k: o[k].cpu().numpy() for k in ("actions", "logits", "returns")})
     finally:
         dpt_hip.set_darkroom_workspace(True)
-    for k in ("actions", "logits", "returns"):
-        assert np.array_equal(outs[0][k], outs[1][k]), k
+    diff = outs[0]["actions"] != outs[1]["actions"]
+    first = np.where(diff.any(1), diff.argmax(1), steps)  # first differing step per task
+    assert (first < steps).mean() <= 0.01
+    same = first == steps
+    assert np.array_equal(outs[0]["returns"][same], outs[1]["returns"][same])
+    for t in range(N):
+        f = min(first[t] + 1, steps)  # logits of steps <= first[t] were computed on identical windows
+        assert_logits(outs[1]["logits"][:f, t], outs[0]["logits"][:f, t])
