@@ -2,6 +2,9 @@
 // Validates shapes on the host (a kernel is never launched on an argument the
 // grid arithmetic does not cover), maps failures to DPT_E* codes and keeps a
 // thread-local message for dpt_last_error().
+#include <algorithm>
+#include <cmath>
+#include <vector>
 #include <stdarg.h>
 #include <stdio.h>
 
@@ -89,6 +92,49 @@ struct dpt_model {
 
 static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Power-of-two scales of the MLP's fp16 two-part products (ModelView::mlp_ew / mlp_ex,
+// dpt_mfma_fwd.h Split2), from static bounds over every layer: |W| of c_fc and
+// mlp.c_proj, and the activations split -- ln_2 outputs (|(x - mean) rstd| <= sqrt(E - 1),
+// then g, b) and gelu outputs (|gelu(h)| <= max(|h|, 0.17), |h| <= sum_i |Wfc[i][j]| B_x +
+// |b_j|).  Scaled values stay below 2^14 (fp16 max 65504) and as large as that allows,
+// so the residual parts of small values stay normal fp16 numbers.
+static int mlp_scales(ModelView& v, int n_layer) {
+    std::vector<float> h((size_t)n_layer * LayerOff::size);
+    int rc = check_hip(hipMemcpy(h.data(), v.layers, h.size() * sizeof(float), hipMemcpyDeviceToHost),
+                       "layer weights to host");
+    if (rc) return rc;
+    double wmax = 0.0, amax = 1.0;
+    for (int l = 0; l < n_layer; ++l) {
+        const float* W = h.data() + (size_t)l * LayerOff::size;
+        double gmax = 0.0, bmax = 0.0;
+        for (int i = 0; i < kE; ++i) {
+            gmax = std::max(gmax, (double)std::fabs(W[LayerOff::ln2_g + i]));
+            bmax = std::max(bmax, (double)std::fabs(W[LayerOff::ln2_b + i]));
+        }
+        const double bx = std::sqrt((double)(kE - 1)) * gmax + bmax;
+        double bh = 0.17;
+        for (int j = 0; j < kFF; ++j) {
+            double s = std::fabs(W[LayerOff::fc_b + j]);
+            for (int i = 0; i < kE; ++i) s += std::fabs(W[LayerOff::fc_w + i * kFF + j]) * bx;
+            bh = std::max(bh, s);
+        }
+        for (int i = 0; i < kE * kFF; ++i)
+            wmax = std::max({wmax, (double)std::fabs(W[LayerOff::fc_w + i]), (double)std::fabs(W[LayerOff::mp_w + i])});
+        amax = std::max({amax, bx, bh});
+    }
+    if (!std::isfinite(wmax) || !std::isfinite(amax)) {
+        set_error(DPT_EINVAL, "non-finite MLP weights");
+        return DPT_EINVAL;
+    }
+    auto expo = [](double bound, int lo, int hi) {  // largest e with bound * 2^e <= 2^14
+        int e = bound > 0.0 ? (int)std::floor(std::log2(16384.0 / bound)) : hi;
+        return std::min(std::max(e, lo), hi);
+    };
+    v.mlp_ew = expo(wmax, -24, 12);
+    v.mlp_ex = expo(amax, -24, 8);
+    return DPT_OK;
+}
+
 static int validate_desc(const dpt_model_desc* d) {
     REQUIRE(d != nullptr, "null model desc");
     if (d->n_embd != kE) {
@@ -169,6 +215,11 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
         return rc;
     }
     ModelView view = make_view(blob, *d);
+    rc = mlp_scales(view, d->n_layer);
+    if (rc) {
+        (void)hipFree(blob);
+        return rc;
+    }
     float* frag = nullptr;
     float* l0 = nullptr;
     const size_t frag_bytes = (size_t)fragments_numel(d->n_layer) * sizeof(float);

@@ -59,6 +59,10 @@ struct ModelView {
     // g0 = Wk bq, Wvp = Wv Wproj, bvp = bv Wproj + bproj
     const float* l0;
     int n_layer, sd, A, F, n_positions;
+    // MLP products on fp16 two-part splits (dpt_mfma_fwd.h Split2): c_fc / mlp.c_proj
+    // weights are packed x 2^mlp_ew and the activations split x 2^mlp_ex, powers of two
+    // chosen at model creation from static bounds (mlp_scales), so nothing overflows fp16
+    int mlp_ew, mlp_ex;
 };
 
 // ----------------------------------------------------------------------------- Philox4x32-10

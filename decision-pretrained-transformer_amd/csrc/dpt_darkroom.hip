@@ -466,7 +466,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
                     float xn[2][8];
                     DPT_BLOCKS(nb, (attn_proj3<NB>(P, split0, o, x), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
-                                   mlp3_n<NB>(P, split0, xn, x)));
+                                   mlp3_n<NB>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
                 }
                 DR_STAMP(1);
             }
@@ -524,7 +524,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 {
                     float xn[2][8];
                     DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b),
-                                   mlp3_n<NB>(W, split0.layer(layer), xn, x)));
+                                   mlp3_n<NB>(W, split0.layer(layer), xn, x, M.mlp_ew, M.mlp_ex)));
                 }
             }
 
@@ -537,7 +537,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 // 2 wave + 1), in flight across the first barrier
                 static_assert(kFF / 32 == kFwdWaves, "one pair of hidden chunks per wave");
                 const Split3 pj0 = f3.ld(Frag3::proj), pj1 = f3.ld(Frag3::proj + 1);
-                const Split3 fj0 = f3.ld(Frag3::fc + 2 * wave), fj1 = f3.ld(Frag3::fc + 2 * wave + 1);
+                const Split2 fj0 = f3.ld2(Frag3::fc + 2 * wave), fj1 = f3.ld2(Frag3::fc + 2 * wave + 1);
                 // (1) the attention as flash partials (m, l, o): with split values key
                 // tiles 2 wave and 2 wave + 1 (one pair, both products on mfma_x6), else
                 // key tiles wave and wave + 4
@@ -686,19 +686,23 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     float xn[8];
                     ln_cols(xl, xn, W + PL::ln2_g, W + PL::ln2_b);
                     {
-                        const Split3 xs = split3(xn);
-                        const floatx4 h0 = mfma_x6(fj0, xs, ld4(W + PL::fc_b + 2 * wave * 16 + 4 * g));
-                        const floatx4 h1 = mfma_x6(fj1, xs, ld4(W + PL::fc_b + (2 * wave + 1) * 16 + 4 * g));
+                        // the MLP's fp16 two-part products at scale 2^(mlp_ew + mlp_ex) (mlp3_n)
+                        const float xs_scale = exp2i(M.mlp_ex), up = exp2i(M.mlp_ew + M.mlp_ex),
+                                    down = exp2i(-(M.mlp_ew + M.mlp_ex));
+                        const Split2 xs = split2(xn, xs_scale);
+                        const floatx4 h0 = mfma_x3(fj0, xs, ld4(W + PL::fc_b + 2 * wave * 16 + 4 * g) * up) * down;
+                        const floatx4 h1 =
+                            mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * wave + 1) * 16 + 4 * g) * up) * down;
                         float gv[8];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             gv[r] = gelu_fast(h0[r]);
                             gv[4 + r] = gelu_fast(h1[r]);
                         }
-                        const Split3 gs = split3(gv);
+                        const Split2 gs = split2(gv, xs_scale);
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-                        const floatx4 y0 = mfma_x6(f3.ld(Frag3::mp + wave), gs, zero);
-                        const floatx4 y1 = mfma_x6(f3.ld(Frag3::mp + 4 + wave), gs, zero);
+                        const floatx4 y0 = mfma_x3(f3.ld2(Frag3::mp + wave), gs, zero) * down;
+                        const floatx4 y1 = mfma_x3(f3.ld2(Frag3::mp + 4 + wave), gs, zero) * down;
                         if ((lane_id() & 15) == 0) {
                             *reinterpret_cast<floatx4*>(&S.part_y[wave][4 * g]) = y0;
                             *reinterpret_cast<floatx4*>(&S.part_y[wave][16 + 4 * g]) = y1;
@@ -812,11 +816,20 @@ __global__ void pack_split_kernel(ModelView M, unsigned short* __restrict__ out)
             const int ob = (tile - Frag3::mp) >> 2, pair = (tile - Frag3::mp) & 3;
             w = W[LayerOff::mp_w + (32 * pair + kin) * kE + ob * 16 + c];
         }
+        unsigned short* d = out + (size_t)layer * (Frag3::bytes / 2) + ((size_t)tile * 3 * 64 + lane) * 8 + j;
+        if (tile >= Frag3::fc) {  // MLP: fp16 two-part split of W x 2^mlp_ew (Split2)
+            const float ws = w * __int_as_float((M.mlp_ew + 127) << 23);
+            const _Float16 h = (_Float16)ws;
+            const _Float16 m = (_Float16)(ws - (float)h);
+            d[0] = __builtin_bit_cast(unsigned short, h);
+            d[64 * 8] = __builtin_bit_cast(unsigned short, m);
+            d[2 * 64 * 8] = 0;
+            continue;
+        }
         const __bf16 h = (__bf16)w;
         const float r = w - (float)h;
         const __bf16 m = (__bf16)r;
         const __bf16 l = (__bf16)(r - (float)m);
-        unsigned short* d = out + (size_t)layer * (Frag3::bytes / 2) + ((size_t)tile * 3 * 64 + lane) * 8 + j;
         d[0] = __builtin_bit_cast(unsigned short, h);
         d[64 * 8] = __builtin_bit_cast(unsigned short, m);
         d[2 * 64 * 8] = __builtin_bit_cast(unsigned short, l);

@@ -1368,6 +1368,8 @@ ModelView make_view(const float* blob, const dpt_model_desc& d) {
     v.A = d.action_dim;
     v.F = F;
     v.n_positions = d.n_positions;
+    v.mlp_ew = 0;  // set by dpt_model_create (mlp_scales)
+    v.mlp_ex = 0;
     return v;
 }
 

@@ -116,6 +116,47 @@ __device__ inline Split3 split3(const float (&v)[8]) {
 __device__ inline floatx4 mfma_bf16(const bf16x8& a, const bf16x8& b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// timing only (wrong results): three part products, the count of a two-part fp16 split
+__device__ inline floatx4 mfma_x3(const Split3& a, const Split3& b, floatx4 acc) {
+    acc = mfma_bf16(a.h, b.m, acc);
+    acc = mfma_bf16(a.m, b.h, acc);
+    return mfma_bf16(a.h, b.h, acc);
+}
+// ---- the MLP's products on fp16 two-part splits ("x3"): v = h + m + O(2^-22 v) with
+// h, m fp16 (11-bit significands; the residual is exact in fp32), and a K = 32 product
+// is h_a h_b + h_a m_b + m_a h_b (exact fp16 products, fp32 accumulation) on three
+// v_mfma_f32_16x16x32_f16, half the matrix cycles of mfma_x6.  The dropped terms are
+// below 2^-21 of |a||b| per product; weights (x 2^mlp_ew) and activations (x 2^mlp_ex)
+// are scaled by powers of two so their residuals stay normal fp16 numbers.
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+struct Split2 {
+    halfx8 h, m;
+};
+__device__ inline Split2 split2(const float (&v)[8], float scale) {
+    unsigned hh[4], mm[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const floatx2 x = floatx2{v[2 * p], v[2 * p + 1]} * floatx2{scale, scale};
+        const halfx2 h = __builtin_convertvector(x, halfx2);
+        const floatx2 r = x - __builtin_convertvector(h, floatx2);
+        hh[p] = __builtin_bit_cast(unsigned, h);
+        mm[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, halfx2));
+    }
+    return Split2{__builtin_bit_cast(halfx8, uint4{hh[0], hh[1], hh[2], hh[3]}),
+                  __builtin_bit_cast(halfx8, uint4{mm[0], mm[1], mm[2], mm[3]})};
+}
+__device__ inline floatx4 mfma_f16(const halfx8& a, const halfx8& b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ inline floatx4 mfma_x3(const Split2& a, const Split2& b, floatx4 acc) {
+    acc = mfma_f16(a.h, b.m, acc);
+    acc = mfma_f16(a.m, b.h, acc);
+    return mfma_f16(a.h, b.h, acc);
+}
+// 2^e as a float (|e| < 127)
+__device__ inline float exp2i(int e) { return __int_as_float((e + 127) << 23); }
+
 // acc + A B over k = 32, smallest part products first
 __device__ inline floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 acc) {
     acc = mfma_bf16(a.m, b.m, acc);
@@ -129,6 +170,7 @@ __device__ inline floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 acc)
 // The split weight tiles of one block (the model's fragment buffer, per layer):
 // [tile][part h|m|l][64 lanes][8 bf16], tile element (lane (g, c), j) = W[in][out]
 // with in = 16*(j>>2) + 4g + (j&3) (mp: hidden 32*pair + that) and out = 16*ob + c.
+// The MLP tiles (fc, mp) hold the fp16 two-part split of W x 2^mlp_ew in parts h, m.
 struct Frag3 {
     static constexpr int attn = 0;   // 2 tiles: G
     static constexpr int proj = 2;   // 2 tiles: Wvp
@@ -145,6 +187,9 @@ struct FragSrc3 {
             bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, base + (tile * 3 + part) * 1024, 0));
     }
     __device__ Split3 ld(int tile) const { return Split3{ld1(tile, 0), ld1(tile, 1), ld1(tile, 2)}; }
+    __device__ Split2 ld2(int tile) const {
+        return Split2{__builtin_bit_cast(halfx8, ld1(tile, 0)), __builtin_bit_cast(halfx8, ld1(tile, 1))};
+    }
     __device__ FragSrc3 layer(int l) const { return FragSrc3{r, l * Frag3::bytes}; }
 };
 
@@ -221,27 +266,32 @@ __device__ inline void ln_n(const float (&x)[2][8], float (&xn)[2][8], const flo
     for (int j = 0; j < NB; ++j) ln_cols(x[j], xn[j], gam, bet);
 }
 
-// x^T += MLP(xn^T) on the bf16 matrix cores (mfma_x6): c_fc per 16-unit chunk, mlp.c_proj per
-// pair of chunks (its K = 32 input is the two chunks' gelu outputs, C-layout).
+// x^T += MLP(xn^T) on fp16 two-part products (mfma_x3): c_fc per 16-unit chunk, mlp.c_proj
+// per pair of chunks (its K = 32 input is the two chunks' gelu outputs, C-layout).  Products
+// accumulate at scale 2^(mlp_ew + mlp_ex) (the biases enter scaled, exactly) and are scaled
+// back by the exact power of two.
 template <int NB>
-__device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&x)[2][8]) {
+__device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&x)[2][8],
+                              int ew, int ex) {
     const int g = lane_id() >> 4;
-    const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);
+    const float xs_scale = exp2i(ex), up = exp2i(ew + ex), down = exp2i(-(ew + ex));
+    const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g) * up, yb1 = ld4(W + PL::mp_b + 16 + 4 * g) * up;
     floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
-    Split3 xs[2];
+    Split2 xs[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split3(xn[j]);
+    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], xs_scale);
     // c_fc tiles one pair ahead (in flight across the pair's split + c_proj products), the
     // pair's c_proj tiles at its start (in flight across its c_fc + gelu)
-    Split3 wf0 = f3.ld(Frag3::fc), wf1 = f3.ld(Frag3::fc + 1);
+    Split2 wf0 = f3.ld2(Frag3::fc), wf1 = f3.ld2(Frag3::fc + 1);
 #pragma unroll
     for (int p = 0; p < kFF / 32; ++p) {
-        const Split3 w0 = f3.ld(Frag3::mp + p), w1 = f3.ld(Frag3::mp + 4 + p);
+        const Split2 w0 = f3.ld2(Frag3::mp + p), w1 = f3.ld2(Frag3::mp + 4 + p);
         float gv[2][8];
-        const floatx4 fb0 = ld4(W + PL::fc_b + 2 * p * 16 + 4 * g), fb1 = ld4(W + PL::fc_b + (2 * p + 1) * 16 + 4 * g);
+        const floatx4 fb0 = ld4(W + PL::fc_b + 2 * p * 16 + 4 * g) * up;
+        const floatx4 fb1 = ld4(W + PL::fc_b + (2 * p + 1) * 16 + 4 * g) * up;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-            const floatx4 h0 = mfma_x6(wf0, xs[j], fb0), h1 = mfma_x6(wf1, xs[j], fb1);
+            const floatx4 h0 = mfma_x3(wf0, xs[j], fb0) * down, h1 = mfma_x3(wf1, xs[j], fb1) * down;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 gv[j][r] = gelu_fast(h0[r]);
@@ -249,23 +299,25 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
             }
         }
         if (p + 1 < kFF / 32) {
-            wf0 = f3.ld(Frag3::fc + 2 * p + 2);
-            wf1 = f3.ld(Frag3::fc + 2 * p + 3);
+            wf0 = f3.ld2(Frag3::fc + 2 * p + 2);
+            wf1 = f3.ld2(Frag3::fc + 2 * p + 3);
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-            const Split3 gs = split3(gv[j]);
-            y0[j] = mfma_x6(w0, gs, y0[j]);
-            y1[j] = mfma_x6(w1, gs, y1[j]);
+            const Split2 gs = split2(gv[j], xs_scale);
+            y0[j] = mfma_x3(w0, gs, y0[j]);
+            y1[j] = mfma_x3(w1, gs, y1[j]);
         }
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j)
+    for (int j = 0; j < NB; ++j) {
+        const floatx4 d0 = y0[j] * down, d1 = y1[j] * down;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            x[j][r] += y0[j][r];
-            x[j][4 + r] += y1[j][r];
+            x[j][r] += d0[r];
+            x[j][4 + r] += d1[r];
         }
+    }
 }
 
 // u = xn G + g0 of the NB blocks (the folded c_attn: only its q part) on mfma_x6

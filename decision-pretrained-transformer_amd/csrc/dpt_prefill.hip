@@ -132,7 +132,7 @@ prefill_kernel(ModelView M, PrefillArgs a) {
         bar_lds();  // every read of this layer's K/V is done
         {
             float xn[2][8];
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b), mlp3_n<NB>(W, fs, xn, x)));
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b), mlp3_n<NB>(W, fs, xn, x, M.mlp_ew, M.mlp_ex)));
         }
     }
 

@@ -56,3 +56,38 @@ def test_six_term_dot_within_fp32_rounding():
     # a plain fp32 dot product has error up to ~K * 2^-24 of sum |a||b|; the split form
     # adds the dropped m*l, l*m, l*l terms (< 3 * 2^-24) and six fp32 roundings
     assert worst < 4 * 2.0 ** -24, worst  # measured: 0.8 * 2^-24
+
+
+def split2_f16(v, e):
+    """The MLP's fp16 two-part split (dpt_mfma_fwd.h split2): v x 2^e -> h + m, both fp16
+    (round to nearest even), the residual exact in fp32."""
+    x = (np.asarray(v, np.float32) * np.float32(2.0 ** e)).astype(np.float32)
+    h = x.astype(np.float16).astype(np.float32)
+    m = (x - h).astype(np.float32).astype(np.float16).astype(np.float32)
+    return h, m
+
+
+def x3_dot(a, b, ea, eb):
+    """h_a m_b + m_a h_b + h_a h_b (exact fp16 products, fp32 accumulation in the kernel's
+    order) at scale 2^(ea + eb), scaled back exactly."""
+    ah, am = (p.astype(np.float64) for p in split2_f16(a, ea))
+    bh, bm = (p.astype(np.float64) for p in split2_f16(b, eb))
+    acc = np.float32(0)
+    for pa, pb in ((ah, bm), (am, bh), (ah, bh)):
+        acc = np.float32(acc + np.float32((pa * pb).sum()))
+    return float(acc) * 2.0 ** -(ea + eb)
+
+
+def test_fp16_two_part_dot_within_fp32_rounding():
+    """The MLP's three-product form at the scales dpt_model_create picks for GPT-2-init
+    weights (2^12 on |W| < 4, 2^8 on the activations): within a few 2^-24 of sum |a||b|,
+    i.e. as accurate as a plain fp32 dot product of that length."""
+    rs = np.random.RandomState(2)
+    worst = 0.0
+    for _ in range(2000):
+        a = (rs.standard_normal(32) * np.exp(rs.uniform(-4, 2))).astype(np.float32)  # ln_2 / gelu outputs
+        b = (rs.standard_normal(32) * 0.05).astype(np.float32)                       # weights
+        exact = float(np.dot(a.astype(np.float64), b.astype(np.float64)))
+        scale = float(np.dot(np.abs(a.astype(np.float64)), np.abs(b.astype(np.float64))))
+        worst = max(worst, abs(x3_dot(a, b, 8, 12) - exact) / scale)
+    assert worst < 8 * 2.0 ** -24, worst  # measured: 1.6 * 2^-24
