@@ -92,20 +92,42 @@ struct dpt_model {
 
 static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Power-of-two scales of the MLP's fp16 two-part products (ModelView::mlp_ew / mlp_ex,
+// Power-of-two scales of the fp16 two-part products (ModelView::mlp_ew / mlp_ex,
 // dpt_mfma_fwd.h Split2), from static bounds over every layer: |W| of c_fc and
 // mlp.c_proj, and the activations split -- ln_2 outputs (|(x - mean) rstd| <= sqrt(E - 1),
 // then g, b) and gelu outputs (|gelu(h)| <= max(|h|, 0.17), |h| <= sum_i |Wfc[i][j]| B_x +
 // |b_j|).  Scaled values stay below 2^14 (fp16 max 65504) and as large as that allows,
 // so the residual parts of small values stay normal fp16 numbers.
-static int mlp_scales(ModelView& v, int n_layer) {
-    std::vector<float> h((size_t)n_layer * LayerOff::size);
+// The attention's scales (attn_ew / attn_ey / attn_eq) likewise: |G| and |Wvp|; the
+// ln_1 outputs y (keys; the attention outputs are convex combinations of them); the
+// queries u = y G + g0 (|u_j| <= sum_i |G[i][j]| B_y + |g0_j|).  Needs ModelView::l0.
+static int fwd_scales(ModelView& v, int n_layer) {
+    std::vector<float> h((size_t)n_layer * LayerOff::size), f((size_t)n_layer * L0Off::size);
     int rc = check_hip(hipMemcpy(h.data(), v.layers, h.size() * sizeof(float), hipMemcpyDeviceToHost),
                        "layer weights to host");
+    if (!rc) rc = check_hip(hipMemcpy(f.data(), v.l0, f.size() * sizeof(float), hipMemcpyDeviceToHost),
+                            "folded attention to host");
     if (rc) return rc;
-    double wmax = 0.0, amax = 1.0;
+    double wmax = 0.0, amax = 1.0, gw = 0.0, ymax = 1.0, qmax = 1.0;
     for (int l = 0; l < n_layer; ++l) {
         const float* W = h.data() + (size_t)l * LayerOff::size;
+        const float* F = f.data() + (size_t)l * L0Off::size;
+        double g1 = 0.0, b1 = 0.0;
+        for (int i = 0; i < kE; ++i) {
+            g1 = std::max(g1, (double)std::fabs(W[LayerOff::ln1_g + i]));
+            b1 = std::max(b1, (double)std::fabs(W[LayerOff::ln1_b + i]));
+        }
+        const double by = std::sqrt((double)(kE - 1)) * g1 + b1;
+        ymax = std::max(ymax, by);
+        for (int j = 0; j < kE; ++j) {
+            double s = std::fabs(F[L0Off::g0 + j]);
+            for (int i = 0; i < kE; ++i) {
+                s += std::fabs(F[L0Off::G + i * kE + j]) * by;
+                gw = std::max({gw, (double)std::fabs(F[L0Off::G + i * kE + j]),
+                               (double)std::fabs(F[L0Off::Wvp + i * kE + j])});
+            }
+            qmax = std::max(qmax, s);
+        }
         double gmax = 0.0, bmax = 0.0;
         for (int i = 0; i < kE; ++i) {
             gmax = std::max(gmax, (double)std::fabs(W[LayerOff::ln2_g + i]));
@@ -122,8 +144,8 @@ static int mlp_scales(ModelView& v, int n_layer) {
             wmax = std::max({wmax, (double)std::fabs(W[LayerOff::fc_w + i]), (double)std::fabs(W[LayerOff::mp_w + i])});
         amax = std::max({amax, bx, bh});
     }
-    if (!std::isfinite(wmax) || !std::isfinite(amax)) {
-        set_error(DPT_EINVAL, "non-finite MLP weights");
+    if (!std::isfinite(wmax) || !std::isfinite(amax) || !std::isfinite(gw) || !std::isfinite(qmax)) {
+        set_error(DPT_EINVAL, "non-finite block weights");
         return DPT_EINVAL;
     }
     auto expo = [](double bound, int lo, int hi) {  // largest e with bound * 2^e <= 2^14
@@ -132,6 +154,9 @@ static int mlp_scales(ModelView& v, int n_layer) {
     };
     v.mlp_ew = expo(wmax, -24, 12);
     v.mlp_ex = expo(amax, -24, 8);
+    v.attn_ew = expo(gw, -24, 12);
+    v.attn_ey = expo(ymax, -24, 8);
+    v.attn_eq = expo(qmax, -24, 8);
     return DPT_OK;
 }
 
@@ -215,11 +240,6 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
         return rc;
     }
     ModelView view = make_view(blob, *d);
-    rc = mlp_scales(view, d->n_layer);
-    if (rc) {
-        (void)hipFree(blob);
-        return rc;
-    }
     float* frag = nullptr;
     float* l0 = nullptr;
     const size_t frag_bytes = (size_t)fragments_numel(d->n_layer) * sizeof(float);
@@ -232,6 +252,8 @@ int dpt_model_create(const dpt_model_desc* d, const float* packed, dpt_model** o
     }
     rc = launch_derive_l0(view, l0, nullptr);
     view.l0 = l0;  // the fragments pack the folded attention (dpt_mfma_fwd.h Frag3)
+    if (!rc) rc = check_hip(hipDeviceSynchronize(), "attention folding");
+    if (!rc) rc = fwd_scales(view, d->n_layer);  // the packing uses the scales
     if (!rc) rc = launch_pack_fragments(view, frag, nullptr);
     if (!rc) rc = check_hip(hipDeviceSynchronize(), "weight derivation");
     if (rc) {

@@ -63,6 +63,9 @@ struct ModelView {
     // weights are packed x 2^mlp_ew and the activations split x 2^mlp_ex, powers of two
     // chosen at model creation from static bounds (mlp_scales), so nothing overflows fp16
     int mlp_ew, mlp_ex;
+    // the same for the attention's dense products and scores: G and Wvp packed x 2^attn_ew,
+    // ln_1 outputs y (keys) and attention outputs x 2^attn_ey, queries u x 2^attn_eq
+    int attn_ew, attn_ey, attn_eq;
 };
 
 // ----------------------------------------------------------------------------- Philox4x32-10

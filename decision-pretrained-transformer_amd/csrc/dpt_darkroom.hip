@@ -293,8 +293,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b), u_proj3_n<NB>(P, split0, xn, q),
-                           kv_from_y<NB>(S.kv, qb, xn)));
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b), u_proj3_n<NB>(P, split0, xn, q, M),
+                           kv_from_y<NB>(S.kv, qb, xn, M)));
             if (p.ws) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -308,7 +308,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             for (int j = 0; j < 2; ++j) {
                 if (j >= nb) break;
                 float m, l, o[8];
-                attend(S.kv, q[j], qb[j], 1, scale, m, l, o);
+                attend(S.kv, q[j], qb[j], 1, scale, m, l, o, M);
                 const int lane = lane_id();
                 if constexpr (kWs) {
                     ws_store(l0_cache(p, task, 2, qb[j]), o);
@@ -407,10 +407,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         if (wave == 0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
                     } else {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                                       u_proj3_n<NB>(P, split0, xn, q)));
+                                       u_proj3_n<NB>(P, split0, xn, q, M)));
                     }
                     if (wave == 0) {  // block 0 (slot 0 of wave 0): key/value (= y) of the query token
-                        kv_from_y<1>(S.kv, qb, xn);
+                        kv_from_y<1>(S.kv, qb, xn, M);
                         const int lane = lane_id();
                         if ((lane & 15) == 0) {  // token 0's y (folded attention: key = value = y)
 #pragma unroll
@@ -465,7 +465,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                     }
                     float xn[2][8];
-                    DPT_BLOCKS(nb, (attn_proj3<NB>(P, split0, o, x), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                    DPT_BLOCKS(nb, (attn_proj3<NB>(P, split0, o, x, M), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
                                    mlp3_n<NB>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
                 }
                 DR_STAMP(1);
@@ -479,17 +479,17 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     float xn[2][8];
                     if (!last) {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       u_proj3_n<NB>(W, split0.layer(layer), xn, q), kv_from_y<NB>(S.kv, qb, xn)));
+                                       u_proj3_n<NB>(W, split0.layer(layer), xn, q, M), kv_from_y<NB>(S.kv, qb, xn, M)));
                     } else {
                         // the last layer needs q only for token T-1 (block qlast)
-                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(S.kv, qb, xn)));
+                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(S.kv, qb, xn, M)));
 #pragma unroll
                         for (int j = 0; j < 2; ++j) {
                             if (j < nb && qb[j] == qlast) {
                                 float xn1[2][8], q1[2][8];
 #pragma unroll
                                 for (int k = 0; k < 8; ++k) xn1[0][k] = xn[j][k];
-                                u_proj3_n<1>(W, split0.layer(layer), xn1, q1);
+                                u_proj3_n<1>(W, split0.layer(layer), xn1, q1, M);
                                 const int lane = lane_id();
                                 if ((lane & 15) == clast) {
 #pragma unroll
@@ -512,12 +512,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     for (int j = 0; j < 2; ++j) {
                         if (j >= nb) break;
                         float m, l;
-                        attend(S.kv, q[j], qb[j], 0, scale, m, l, o[j]);
+                        attend(S.kv, q[j], qb[j], 0, scale, m, l, o[j], M);
                         const float inv = 1.0f / l;
 #pragma unroll
                         for (int k = 0; k < 8; ++k) o[j][k] *= inv;
                     }
-                    DPT_BLOCKS(nb, attn_proj3<NB>(W, split0.layer(layer), o, x));
+                    DPT_BLOCKS(nb, attn_proj3<NB>(W, split0.layer(layer), o, x, M));
                 }
                 bar_lds();  // every read of this layer's K/V is done
                 DR_STAMP(2 * layer + 1);
@@ -536,7 +536,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 // this wave's tail weight tiles (c_proj, c_fc of hidden chunks 2 wave and
                 // 2 wave + 1), in flight across the first barrier
                 static_assert(kFF / 32 == kFwdWaves, "one pair of hidden chunks per wave");
-                const Split3 pj0 = f3.ld(Frag3::proj), pj1 = f3.ld(Frag3::proj + 1);
+                const Split2 pj0 = f3.ld2(Frag3::proj), pj1 = f3.ld2(Frag3::proj + 1);
                 const Split2 fj0 = f3.ld2(Frag3::fc + 2 * wave), fj1 = f3.ld2(Frag3::fc + 2 * wave + 1);
                 // (1) the attention as flash partials (m, l, o): with split values key
                 // tiles 2 wave and 2 wave + 1 (one pair, both products on mfma_x6), else
@@ -548,7 +548,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     if (kb <= qlast) {
                         const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
-                        const Split3 qs = split3(qv);  // the query, broadcast to every column
+                        const Split2 qs = split2(qv, exp2i(M.attn_eq));  // the query, broadcast to every column
+                        const float kscale = scale * exp2i(-(M.attn_ey + M.attn_eq));
                         float sv[8], mt = -INFINITY;
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
@@ -558,11 +559,11 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                                 for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
                                 continue;
                             }
-                            const Split3 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane], S.kv.KS[kt][2][lane]};
-                            const floatx4 sc = mfma_x6(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
+                            const Split2 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane]};
+                            const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
-                                const float sr = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * scale : -INFINITY;
+                                const float sr = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * kscale : -INFINITY;
                                 sv[4 * h + r] = sr;
                                 mt = fmaxf(mt, sr);
                             }
@@ -599,8 +600,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #ifndef DPT_ATTN_F32
                         // split key tile x the split query, broadcast to every column
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
-                        const Split3 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane], S.kv.KS[kt][2][lane]};
-                        const floatx4 sc = mfma_x6(ks, split3(qv), floatx4{0.f, 0.f, 0.f, 0.f});
+                        const Split2 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane]};
+                        const floatx4 sc = mfma_x3(ks, split2(qv, exp2i(M.attn_eq)), floatx4{0.f, 0.f, 0.f, 0.f}) *
+                                           exp2i(-(M.attn_ey + M.attn_eq));
 #else
                         const floatx4 k0 = ld4(&S.kv.K[kt * 16 + c][4 * g]);
                         const floatx4 k1 = ld4(&S.kv.K[kt * 16 + c][16 + 4 * g]);
@@ -674,9 +676,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         xl[4 + r] = xb[r];
                     }
                     {
-                        const Split3 os = split3(o);
-                        const floatx4 a0 = mfma_x6(pj0, os, ld4(W + PL::proj_b + 4 * g));
-                        const floatx4 a1 = mfma_x6(pj1, os, ld4(W + PL::proj_b + 16 + 4 * g));
+                        const float up = exp2i(M.attn_ew + M.attn_ey), down = exp2i(-(M.attn_ew + M.attn_ey));
+                        const Split2 os = split2(o, exp2i(M.attn_ey));
+                        const floatx4 a0 = mfma_x3(pj0, os, ld4(W + PL::proj_b + 4 * g) * up) * down;
+                        const floatx4 a1 = mfma_x3(pj1, os, ld4(W + PL::proj_b + 16 + 4 * g) * up) * down;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             xl[r] += a0[r];
@@ -817,8 +820,9 @@ __global__ void pack_split_kernel(ModelView M, unsigned short* __restrict__ out)
             w = W[LayerOff::mp_w + (32 * pair + kin) * kE + ob * 16 + c];
         }
         unsigned short* d = out + (size_t)layer * (Frag3::bytes / 2) + ((size_t)tile * 3 * 64 + lane) * 8 + j;
-        if (tile >= Frag3::fc) {  // MLP: fp16 two-part split of W x 2^mlp_ew (Split2)
-            const float ws = w * __int_as_float((M.mlp_ew + 127) << 23);
+        {  // fp16 two-part split of W x 2^mlp_ew (MLP) or 2^attn_ew (G, Wvp): Split2
+            const int e = tile >= Frag3::fc ? M.mlp_ew : M.attn_ew;
+            const float ws = w * __int_as_float((e + 127) << 23);
             const _Float16 h = (_Float16)ws;
             const _Float16 m = (_Float16)(ws - (float)h);
             d[0] = __builtin_bit_cast(unsigned short, h);

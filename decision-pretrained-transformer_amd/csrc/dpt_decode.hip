@@ -1370,6 +1370,7 @@ ModelView make_view(const float* blob, const dpt_model_desc& d) {
     v.n_positions = d.n_positions;
     v.mlp_ew = 0;  // set by dpt_model_create (mlp_scales)
     v.mlp_ex = 0;
+    v.attn_ew = v.attn_ey = v.attn_eq = 0;
     return v;
 }
 

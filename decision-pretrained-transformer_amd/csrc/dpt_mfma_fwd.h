@@ -25,11 +25,12 @@ struct PL {
                          fc_b = 256, mp_b = 384, size = 416;
 };
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 // This workgroup's keys and values of the current layer, for windows of up to TMAX
-// tokens.  Keys are either fp32 token-major (K) or, with SPLITK, the split bf16 A
-// operand tiles of the score product (KS[block][part h|m|l][lane], written once by
-// the lane that computed the key: 3 KB per 16 keys instead of 2.25 KB, no split per
-// read).  Values stay fp32 feature-major (Vt).
+// tokens.  Keys are either fp32 token-major (K) or, with SPLITK, the fp16 two-part A
+// operand tiles of the score product (KS[block][part h|m][lane], y x 2^attn_ey, written
+// once by the lane that computed the key: 2 KB per 16 keys, no split per read).  Values
+// stay fp32 feature-major (Vt).
 // With SPLITV (requires SPLITK) the values are kept as the split A operand of
 // O^T += V^T P^T over a pair of key tiles: VS[pair][feature half][part][lane (g, c)],
 // element j = V[key 16 (2 pair + (j >> 2)) + 4g + (j & 3)][feature 16 half + c] (the
@@ -39,12 +40,12 @@ struct KVBuf {
     static_assert(SPLITK || !SPLITV, "split values need split keys");
     static constexpr bool kSplitK = SPLITK, kSplitV = SPLITV;
     float K[SPLITK ? 1 : TMAX][kKStride];
-    bf16x8 KS[SPLITK ? TMAX / 16 : 1][SPLITK ? 3 : 1][SPLITK ? 64 : 1];  // (16 B when unused)
+    halfx8 KS[SPLITK ? TMAX / 16 : 1][SPLITK ? 2 : 1][SPLITK ? 64 : 1];  // (16 B when unused)
     bf16x8 VS[SPLITV ? TMAX / 32 : 1][SPLITV ? 2 : 1][SPLITV ? 3 : 1][SPLITV ? 64 : 1];
     float Vt[SPLITV ? 1 : kE][TMAX + 4];
 };
 #ifndef DPT_ATTN_F32
-constexpr bool kSplitKeys = true;  // scores (and, with SPLITV, PV) on mfma_x6
+constexpr bool kSplitKeys = true;  // scores on mfma_x3 (and, with SPLITV, PV on mfma_x6)
 #else
 constexpr bool kSplitKeys = false;
 #endif
@@ -116,19 +117,13 @@ __device__ inline Split3 split3(const float (&v)[8]) {
 __device__ inline floatx4 mfma_bf16(const bf16x8& a, const bf16x8& b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-// timing only (wrong results): three part products, the count of a two-part fp16 split
-__device__ inline floatx4 mfma_x3(const Split3& a, const Split3& b, floatx4 acc) {
-    acc = mfma_bf16(a.h, b.m, acc);
-    acc = mfma_bf16(a.m, b.h, acc);
-    return mfma_bf16(a.h, b.h, acc);
-}
-// ---- the MLP's products on fp16 two-part splits ("x3"): v = h + m + O(2^-22 v) with
+// ---- dense products on fp16 two-part splits ("x3"): v = h + m + O(2^-22 v) with
 // h, m fp16 (11-bit significands; the residual is exact in fp32), and a K = 32 product
 // is h_a h_b + h_a m_b + m_a h_b (exact fp16 products, fp32 accumulation) on three
 // v_mfma_f32_16x16x32_f16, half the matrix cycles of mfma_x6.  The dropped terms are
-// below 2^-21 of |a||b| per product; weights (x 2^mlp_ew) and activations (x 2^mlp_ex)
-// are scaled by powers of two so their residuals stay normal fp16 numbers.
-typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+// below 2^-21 of |a||b| per product; weights and activations are scaled by powers of
+// two (ModelView mlp_* / attn_*) so their residuals stay normal fp16 numbers.  Every
+// product of the forward runs this way except the attention's P V (P reaches e^32).
 typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
 struct Split2 {
     halfx8 h, m;
@@ -320,40 +315,46 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
     }
 }
 
-// u = xn G + g0 of the NB blocks (the folded c_attn: only its q part) on mfma_x6
+// u = xn G + g0 of the NB blocks (the folded c_attn: only its q part) on fp16 two-part
+// products (mfma_x3) at scale 2^(attn_ew + attn_ey), scaled back exactly
 template <int NB>
-__device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8]) {
+__device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8],
+                                 const ModelView& M) {
     const int g = lane_id() >> 4;
-    Split3 xs[2];
+    const float up = exp2i(M.attn_ew + M.attn_ey), down = exp2i(-(M.attn_ew + M.attn_ey));
+    Split2 xs[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split3(xn[j]);
+    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
-        const Split3 w = f3.ld(Frag3::attn + ob);
-        const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);
+        const Split2 w = f3.ld2(Frag3::attn + ob);
+        const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g) * up;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-            const floatx4 acc = mfma_x6(w, xs[j], bias);
+            const floatx4 acc = mfma_x3(w, xs[j], bias) * down;
 #pragma unroll
             for (int r = 0; r < 4; ++r) q[j][ob * 4 + r] = acc[r];
         }
     }
 }
 
-// attn_proj on mfma_x6: x^T += Wvp^T o^T + bvp
+// attn_proj on mfma_x3: x^T += Wvp^T o^T + bvp (o, a convex combination of the values y,
+// shares their bound and scale)
 template <int NB>
-__device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8]) {
+__device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8],
+                                  const ModelView& M) {
     const int g = lane_id() >> 4;
-    Split3 os[2];
+    const float up = exp2i(M.attn_ew + M.attn_ey), down = exp2i(-(M.attn_ew + M.attn_ey));
+    Split2 os[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) os[j] = split3(o[j]);
+    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], exp2i(M.attn_ey));
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
-        const Split3 w = f3.ld(Frag3::proj + ob);
-        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g);
+        const Split2 w = f3.ld2(Frag3::proj + ob);
+        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g) * up;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-            const floatx4 acc = mfma_x6(w, os[j], bias);
+            const floatx4 acc = mfma_x3(w, os[j], bias) * down;
 #pragma unroll
             for (int r = 0; r < 4; ++r) x[j][ob * 4 + r] += acc[r];
         }
@@ -364,19 +365,19 @@ __device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const floa
 // LayerNorm output y itself (K <- y token-major, Vt <- y feature-major, the
 // C-layout of xn is the layout c_attn's K / V tiles had).
 template <int NB, class KV>
-__device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2][8]) {
+__device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2][8], const ModelView& M) {
     const int lane = lane_id(), g = lane >> 4;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const int tok = qb[j] * 16 + (lane & 15);
         if constexpr (KV::kSplitK) {  // the lane's 8 values are its A-operand k-elements
-            const Split3 ks = split3(xn[j]);
-            S.KS[qb[j]][0][lane] = ks.h;
-            S.KS[qb[j]][1][lane] = ks.m;
-            S.KS[qb[j]][2][lane] = ks.l;
+            const Split2 kt = split2(xn[j], exp2i(M.attn_ey));
+            S.KS[qb[j]][0][lane] = kt.h;
+            S.KS[qb[j]][1][lane] = kt.m;
             if constexpr (KV::kSplitV) {
-                // the same split values, scattered into V^T's pair-tile order: value k of
-                // lane (g, c) is feature 16 (k >> 2) + 4g + (k & 3) of token 16 b + c
+                // the bf16 three-part split of the values, scattered into V^T's pair-tile
+                // order: value k of lane (g, c) is feature 16 (k >> 2) + 4g + (k & 3) of token 16 b + c
+                const Split3 ks = split3(xn[j]);
                 const int b = qb[j], c = lane & 15;
                 __bf16* vs = reinterpret_cast<__bf16*>(&S.VS[b >> 1][0][0][0]);
 #pragma unroll
@@ -406,7 +407,7 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
 // sum_s e^(s-m) v_s (C-layout).
 template <class KV>
 __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
-                              float& lsum, float (&o)[8]) {
+                              float& lsum, float (&o)[8], const ModelView& M) {
     // The running reference m of a token column moves only when a key tile holds a
     // score more than kSlack above it (always for the first tile with a key): the
     // probabilities are exp(s - m) <= e^kSlack, so the sums cannot overflow, and the
@@ -416,7 +417,10 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     constexpr float kSlack = 32.f;
     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
 #ifndef DPT_ATTN_F32
-    const Split3 qs = split3(q);
+    // scores on fp16 two-part products: keys x 2^attn_ey, queries x 2^attn_eq, and the
+    // exact power of two folded into the 1/sqrt(d) scale
+    const Split2 qs = split2(q, exp2i(M.attn_eq));
+    scale *= exp2i(-(M.attn_ey + M.attn_eq));
     if constexpr (KV::kSplitV) {
         // both products on mfma_x6, key tiles in pairs: per tile S^T = K Q^T, per pair
         // and feature half O^T += V^T P^T with K = the pair's 32 keys (P^T's C-layout of
@@ -438,8 +442,8 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
                     for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
                     continue;
                 }
-                const Split3 ks{S.KS[kt][0][lane], S.KS[kt][1][lane], S.KS[kt][2][lane]};
-                const floatx4 sc = mfma_x6(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
+                const Split2 ks{S.KS[kt][0][lane], S.KS[kt][1][lane]};
+                const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int key = kt * 16 + 4 * g + r;
@@ -487,16 +491,16 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
 #ifndef DPT_ATTN_F32
         // S^T = K Q^T on mfma_x6: the key tile is the A operand (lane (g, c): key
         // 16 kb + c, the lane group's 8 features), Q^T the B operand (q's C-layout)
-        Split3 ks;
+        Split2 ks;
         if constexpr (KV::kSplitK) {
-            ks = Split3{S.KS[kb][0][lane], S.KS[kb][1][lane], S.KS[kb][2][lane]};
+            ks = Split2{S.KS[kb][0][lane], S.KS[kb][1][lane]};
         } else {
             const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
             const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
             const float kv[8] = {k0[0], k0[1], k0[2], k0[3], k1[0], k1[1], k1[2], k1[3]};
-            ks = split3(kv);
+            ks = split2(kv, exp2i(M.attn_ey));
         }
-        const floatx4 sc = mfma_x6(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
+        const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #else
         const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
         const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);

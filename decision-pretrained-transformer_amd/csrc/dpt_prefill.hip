@@ -112,8 +112,8 @@ prefill_kernel(ModelView M, PrefillArgs a) {
         float q[2][8];
         {
             float xn[2][8];
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), u_proj3_n<NB>(W, fs, xn, q),
-                            kv_from_y<NB>(S, qb, xn)));
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), u_proj3_n<NB>(W, fs, xn, q, M),
+                            kv_from_y<NB>(S, qb, xn, M)));
         }
         bar_lds();
         if (nb > 0) {
@@ -122,12 +122,12 @@ prefill_kernel(ModelView M, PrefillArgs a) {
             for (int j = 0; j < 2; ++j) {
                 if (j >= nb) break;
                 float m, l;
-                attend(S, q[j], qb[j], 0, scale, m, l, o[j]);
+                attend(S, q[j], qb[j], 0, scale, m, l, o[j], M);
                 const float inv = 1.0f / l;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) o[j][k] *= inv;
             }
-            DPT_BLOCKS(nb, attn_proj3<NB>(W, fs, o, x));
+            DPT_BLOCKS(nb, attn_proj3<NB>(W, fs, o, x, M));
         }
         bar_lds();  // every read of this layer's K/V is done
         {
