@@ -574,13 +574,15 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         for (int r = 0; r < 8; ++r) pr[r] = __expf(sv[r] - mt);
                         float lt = ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
                         lt = sum_cols(lt);
-                        const Split3 ps = split3(pr);
+                        // P <= 1 here (mt is the exact max): fp16 two-part at 2^kPExp as in attend
+                        const Split2 ps = split2(pr, exp2i(kPExp));
                         const int pp = wave;
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-                        const floatx4 o0 = mfma_x6(Split3{S.kv.VS[pp][0][0][lane], S.kv.VS[pp][0][1][lane],
-                                                          S.kv.VS[pp][0][2][lane]}, ps, zero);
-                        const floatx4 o1 = mfma_x6(Split3{S.kv.VS[pp][1][0][lane], S.kv.VS[pp][1][1][lane],
-                                                          S.kv.VS[pp][1][2][lane]}, ps, zero);
+                        const float down = exp2i(-(M.attn_ey + kPExp));
+                        const floatx4 o0 =
+                            mfma_x3(Split2{S.kv.VS[pp][0][0][lane], S.kv.VS[pp][0][1][lane]}, ps, zero) * down;
+                        const floatx4 o1 =
+                            mfma_x3(Split2{S.kv.VS[pp][1][0][lane], S.kv.VS[pp][1][1][lane]}, ps, zero) * down;
                         if (c == 0) {
                             *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
                             *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;

@@ -31,17 +31,18 @@ typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 // operand tiles of the score product (KS[block][part h|m][lane], y x 2^attn_ey, written
 // once by the lane that computed the key: 2 KB per 16 keys, no split per read).  Values
 // stay fp32 feature-major (Vt).
-// With SPLITV (requires SPLITK) the values are kept as the split A operand of
-// O^T += V^T P^T over a pair of key tiles: VS[pair][feature half][part][lane (g, c)],
-// element j = V[key 16 (2 pair + (j >> 2)) + 4g + (j & 3)][feature 16 half + c] (the
-// lane group's k order of P^T's C-layout over the two tiles), 6 KB per 32 keys.
+// With SPLITV (requires SPLITK) the values are kept as the fp16 two-part A operand of
+// O^T += V^T P^T over a pair of key tiles (y x 2^attn_ey, the keys' split):
+// VS[pair][feature half][part h|m][lane (g, c)], element j = V[key 16 (2 pair + (j >> 2))
+// + 4g + (j & 3)][feature 16 half + c] (the lane group's k order of P^T's C-layout over
+// the two tiles), 4 KB per 32 keys.
 template <int TMAX, bool SPLITK = false, bool SPLITV = false>
 struct KVBuf {
     static_assert(SPLITK || !SPLITV, "split values need split keys");
     static constexpr bool kSplitK = SPLITK, kSplitV = SPLITV;
     float K[SPLITK ? 1 : TMAX][kKStride];
     halfx8 KS[SPLITK ? TMAX / 16 : 1][SPLITK ? 2 : 1][SPLITK ? 64 : 1];  // (16 B when unused)
-    bf16x8 VS[SPLITV ? TMAX / 32 : 1][SPLITV ? 2 : 1][SPLITV ? 3 : 1][SPLITV ? 64 : 1];
+    halfx8 VS[SPLITV ? TMAX / 32 : 1][SPLITV ? 2 : 1][SPLITV ? 2 : 1][SPLITV ? 64 : 1];
     float Vt[SPLITV ? 1 : kE][TMAX + 4];
 };
 #ifndef DPT_ATTN_F32
@@ -151,6 +152,8 @@ __device__ inline floatx4 mfma_x3(const Split2& a, const Split2& b, floatx4 acc)
 }
 // 2^e as a float (|e| < 127)
 __device__ inline float exp2i(int e) { return __int_as_float((e + 127) << 23); }
+// scale of the attention probabilities in P V (P <= e^8 < 2^12, so P x 2^kPExp < 2^14)
+constexpr int kPExp = 2;
 
 // acc + A B over k = 32, smallest part products first
 __device__ inline floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 acc) {
@@ -375,17 +378,15 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
             S.KS[qb[j]][0][lane] = kt.h;
             S.KS[qb[j]][1][lane] = kt.m;
             if constexpr (KV::kSplitV) {
-                // the bf16 three-part split of the values, scattered into V^T's pair-tile
-                // order: value k of lane (g, c) is feature 16 (k >> 2) + 4g + (k & 3) of token 16 b + c
-                const Split3 ks = split3(xn[j]);
+                // the same split parts, scattered into V^T's pair-tile order: value k of
+                // lane (g, c) is feature 16 (k >> 2) + 4g + (k & 3) of token 16 b + c
                 const int b = qb[j], c = lane & 15;
-                __bf16* vs = reinterpret_cast<__bf16*>(&S.VS[b >> 1][0][0][0]);
+                _Float16* vs = reinterpret_cast<_Float16*>(&S.VS[b >> 1][0][0][0]);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    const int off = ((k >> 2) * 3 * 64 + (c >> 2) * 16 + 4 * g + (k & 3)) * 8 + (b & 1) * 4 + (c & 3);
-                    vs[off] = ks.h[k];
-                    vs[off + 64 * 8] = ks.m[k];
-                    vs[off + 2 * 64 * 8] = ks.l[k];
+                    const int off = ((k >> 2) * 2 * 64 + (c >> 2) * 16 + 4 * g + (k & 3)) * 8 + (b & 1) * 4 + (c & 3);
+                    vs[off] = kt.h[k];
+                    vs[off + 64 * 8] = kt.m[k];
                 }
             }
         }
@@ -422,12 +423,14 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     const Split2 qs = split2(q, exp2i(M.attn_eq));
     scale *= exp2i(-(M.attn_ey + M.attn_eq));
     if constexpr (KV::kSplitV) {
-        // both products on mfma_x6, key tiles in pairs: per tile S^T = K Q^T, per pair
+        // both products on mfma_x3, key tiles in pairs: per tile S^T = K Q^T, per pair
         // and feature half O^T += V^T P^T with K = the pair's 32 keys (P^T's C-layout of
         // the two tiles is the B operand as it stands).  An unpaired last tile reads the
         // pair's second tile from LDS with probability 0 (the rollout zeroes VS at launch,
         // so it holds finite values).  The softmax reference moves as in the per-tile
-        // form below (kSlack, one vote per pair).
+        // form below, one vote per pair, but with kSlackP = 8: P <= e^8, so P x 2^kPExp
+        // fits fp16, and o accumulates at scale 2^(attn_ey + kPExp).
+        constexpr float kSlackP = 8.f;
         m = -INFINITY;
         lsum = 0.f;
         floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
@@ -453,7 +456,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
                     mt = fmaxf(mt, sr);
                 }
             }
-            if (__builtin_amdgcn_ballot_w64(mt > m + kSlack)) {  // wave-uniform
+            if (__builtin_amdgcn_ballot_w64(mt > m + kSlackP)) {  // wave-uniform
                 mt = max_cols(mt);
                 const float mn = fmaxf(m, mt);
                 const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
@@ -470,16 +473,17 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
 #pragma unroll
             for (int r = 0; r < 8; ++r) pr[r] = __expf(sv[r] - base);
             lsum += ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
-            const Split3 ps = split3(pr);
+            const Split2 ps = split2(pr, exp2i(kPExp));
             const int pp = kb >> 1;
-            o0 = mfma_x6(Split3{S.VS[pp][0][0][lane], S.VS[pp][0][1][lane], S.VS[pp][0][2][lane]}, ps, o0);
-            o1 = mfma_x6(Split3{S.VS[pp][1][0][lane], S.VS[pp][1][1][lane], S.VS[pp][1][2][lane]}, ps, o1);
+            o0 = mfma_x3(Split2{S.VS[pp][0][0][lane], S.VS[pp][0][1][lane]}, ps, o0);
+            o1 = mfma_x3(Split2{S.VS[pp][1][0][lane], S.VS[pp][1][1][lane]}, ps, o1);
         }
         lsum = sum_cols(lsum);
+        const float down = exp2i(-(M.attn_ey + kPExp));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            o[r] = o0[r];
-            o[4 + r] = o1[r];
+            o[r] = o0[r] * down;
+            o[4 + r] = o1[r] * down;
         }
         return;
     }
