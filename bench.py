@@ -30,10 +30,11 @@ sys.path[:0] = [os.path.join(ROOT, "decision-pretrained-transformer_amd"), ROOT]
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: FP32 matrix 157.3 TFLOP/s (spec)
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: BF16 ~2.5 PFLOP/s dense
-# fp32-accurate products on the bf16 matrix cores (dpt_mfma_fwd.h mfma_x6): one K=32 tile
-# is six v_mfma_f32_16x16x32_bf16 (16 cycles each) instead of eight v_mfma_f32_16x16x4_f32
-# (32 cycles each), so the fp32-equivalent ceiling of those products is 256/96 x the fp32 one
-X6_PEAK_TF = FP32_MFMA_PEAK_TF * 256 / 96
+# fp32-accurate products on the fp16 matrix cores (dpt_mfma_fwd.h mfma_x3, fp16 two-part
+# splits): one K=32 tile is three v_mfma_f32_16x16x32_f16 (16 cycles each) instead of eight
+# v_mfma_f32_16x16x4_f32 (32 cycles each), so the fp32-equivalent ceiling of every product
+# of the DarkRoom forward is 256/48 x the fp32 one
+X3_PEAK_TF = FP32_MFMA_PEAK_TF * 256 / 48
 
 
 def synthetic_state_dict(n_layer, state_dim, action_dim, horizon, seed=0):
@@ -79,11 +80,12 @@ def window_flops(T, n_layer, F, A, E=32, folded=True, split=False):
     """FLOPs of one causal window forward over T tokens (embed, L blocks, ln_f, head):
     per block 2*T*E*(E + E + 4E + 4E) dense with the folded attention the kernels run
     (u = y G + g0 and (sum P y) Wvp; 3E + E for c_attn + c_proj unfolded)
-    + 2 * 2*E * T(T+1)/2 attention.  split=True: (dense, the rest) separately."""
+    + 2 * 2*E * T(T+1)/2 attention.  split=True: (matrix products = dense + attention, the
+    embedding and head) separately."""
     dense = 2 * T * E * ((E if folded else 3 * E) + E + 4 * E + 4 * E)
     attn = 2 * 2 * E * T * (T + 1) // 2
     if split:
-        return n_layer * dense, n_layer * attn + 2 * T * F * E + 2 * E * A
+        return n_layer * (dense + attn), 2 * T * F * E + 2 * E * A
     return n_layer * (dense + attn) + 2 * T * F * E + 2 * E * A
 
 
@@ -269,11 +271,11 @@ def main():
                                  (Heps - 1) * window_flops(1 + H, L, F, 5, folded=False))
         flops = int(fw[0]) * window_flops(1, L, F, 5) + int(fw[1:].sum()) * window_flops(1 + H, L, F, 5)
         achieved = flops / (kern_ms * 1e-3) / 1e12
-        # the ceiling of this mix: dense products (mfma_x6 on the bf16 cores) at X6_PEAK_TF, the
-        # attention (fp32 MFMA) and the rest at the fp32 peak
+        # the ceiling of this mix: the blocks' products (mfma_x3 on the fp16 cores) at X3_PEAK_TF,
+        # the embedding and head (VALU) at the fp32 peak
         parts = [window_flops(1, L, F, 5, split=True), window_flops(1 + H, L, F, 5, split=True)]
         dense = int(fw[0]) * parts[0][0] + int(fw[1:].sum()) * parts[1][0]
-        peak = flops / (dense / X6_PEAK_TF + (flops - dense) / FP32_MFMA_PEAK_TF)
+        peak = flops / (dense / X3_PEAK_TF + (flops - dense) / FP32_MFMA_PEAK_TF)
         traffic = None  # HBM bytes read per launch (rocprofv3 FETCH_SIZE x2, scripts/profile_darkroom.sh)
         pmc = os.path.join(ROOT, "profiles", "pmc_rollout_darkroom.json")
         if os.path.exists(pmc) and count == 4096 and H == 100:
@@ -281,7 +283,7 @@ def main():
         roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": achieved / peak, "traffic": traffic,
                 "peak_fp32_mfma": FP32_MFMA_PEAK_TF, "frac_of_fp32_mfma": achieved / FP32_MFMA_PEAK_TF,
-                "dense_flops_per_launch": dense,
+                "matrix_flops_per_launch": dense,
                 "kernel": "rollout_darkroom_kernel (one launch = one whole online eval)",
                 "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
                 "window_forwards_per_launch": int(fw.sum()),
@@ -289,9 +291,9 @@ def main():
                 "note": "flops = window forwards the kernel ran (one per distinct state per episode) x "
                         "FLOPs of that window with the folded attention; the reference runs one unfolded "
                         "forward per env step (reference_flops_per_launch). peak = the ceiling of this "
-                        "FLOP mix: dense products as fp32-accurate bf16 split products (six "
-                        "16x16x32 bf16 MFMAs per K=32 tile: 157.3 x 256/96 TFLOP/s), attention on the "
-                        "fp32 MFMA (157.3)"}
+                        "FLOP mix: every product of the blocks (dense and attention) as fp32-accurate "
+                        "fp16 two-part split products (three 16x16x32 f16 MFMAs per K=32 tile: "
+                        "157.3 x 256/48 TFLOP/s), embedding and head at the fp32 peak (157.3)"}
     line = {
         "metric": "env-steps/sec/GPU (DPT policy in loop), 5-arm bandit H=500, 1/2/4/8 MI355X",
         "value": value,

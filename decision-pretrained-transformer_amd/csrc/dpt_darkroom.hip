@@ -370,6 +370,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     S.tnext = tt;
                 }
                 bar_lds();
+                DR_STAMP(2 * L + 4);
                 t = S.tnext;
                 if (t >= p.horizon) break;
             }
@@ -749,6 +750,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                         lg[a] = sum_cols(part) + P[pt.head_b + a];
                     }
+                    DR_STAMP(2 * L + 2);
                     if (lane == 0) {
                         double q[kDrA] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #ifdef DPT_EXP_NOCDF  // timing only (wrong results): no softmax cdf
@@ -770,6 +772,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         S.sx = cur_x;
                         S.sy = cur_y;
                     }
+                    DR_STAMP(2 * L + 3);
                 }
             }
             bar_lds();

@@ -29,7 +29,8 @@ names = ["L0:embed+query k/v", "L0:merge+c_proj+mlp (wave 0 view)"]
 for layer in range(1, L - 1):
     names += [f"L{layer}:ln1+c_attn (+prev mlp)", f"L{layer}:attn+c_proj"]
 names += [f"L{L - 1}:ln1+c_attn (+prev mlp)", "tail1:key-tile partials", "tail2:merge+c_proj+mlp chunk",
-          "tail3:head+select+env"]
+          "tail3:barrier after select", "tail3a:part_y+ln_f+head", "tail3b:cdf+select+env (lane 0)",
+          "memo hits + barrier"]
 out = {}
 for N in (256, 512, 4096):
     goals = np.stack(np.unravel_index(np.arange(N) % 100, (10, 10)), 1)
@@ -42,7 +43,7 @@ for N in (256, 512, 4096):
     dt = time.perf_counter() - t0
     buf = (ctypes.c_ulonglong * 32)()
     lib.dpt_debug_dr_stamps(ctypes.addressof(buf), 32, 0)
-    v = np.array(buf[:2 * L + 2], dtype=np.float64) / (Heps * 100)
+    v = np.array(buf[:2 * L + 5], dtype=np.float64) / (Heps * 100)
     res = {n: round(float(x)) for n, x in zip(names, v) if x > 0}
     res["total_cycles_per_step"] = round(float(v.sum()))
     res["wall_s"] = dt
