@@ -1014,17 +1014,32 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 w2b[s] = __ldg(W2 + (size_t)s * kE + 16 + i16);
             }
             floatx4 ht = {0.f, 0.f, 0.f, 0.f};
+#ifdef DPT_EXP_MLPCHAIN  // timing only (wrong results): a 3-deep c_fc chain, 2-deep c_proj
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+                ht = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[s] + w1[s + 3] + w1[(s + 6) & 7], S.xn[i16][4 * s + kq], ht, 0, 0, 0);
+#else
 #pragma unroll
             for (int s = 0; s < 8; ++s)
                 ht = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[s], S.xn[i16][4 * s + kq], ht, 0, 0, 0);
+#endif
             // ht[r] = h^T[unit 16*wave + 4*kq + r][task i16]
             floatx4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
+#ifdef DPT_EXP_MLPCHAIN
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const float hv = gelu_new(ht[s] + ht[s + 2] + PL[PLay::fc_b + wave * 16 + kq * 4 + s]);
+                p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2a[s] + w2a[s + 2], p0, 0, 0, 0);
+                p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2b[s] + w2b[s + 2], p1, 0, 0, 0);
+            }
+#else
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const float hv = gelu_new(ht[s] + PL[PLay::fc_b + wave * 16 + kq * 4 + s]);
                 p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2a[s], p0, 0, 0, 0);
                 p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2b[s], p1, 0, 0, 0);
             }
+#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 S.part[wave][kq * 4 + r][i16] = p0[r];

@@ -24,8 +24,8 @@ def main(stats, mfma, fetch, out):
            "SQ_VALU_MFMA_BUSY_CYCLES": v["SQ_VALU_MFMA_BUSY_CYCLES"],
            "effective_clock_GHz": v["GRBM_GUI_ACTIVE"] / 8 / (ns * 1e-9) / 1e9,
            "mfma_pipe_busy_frac": v["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * v["GRBM_GUI_ACTIVE"] / 8),
-           "note": "busy cycles summed over the 1024 SIMDs: 32 per v_mfma_f32_16x16x4_f32 (attention) and 16 per "
-                   "v_mfma_f32_16x16x32_bf16 (the dense products as bf16 split products, round 2); "
+           "note": "busy cycles summed over the 1024 SIMDs: 16 per v_mfma_f32_16x16x32_f16 (every product of the "
+                   "blocks as fp16 two-part split products, three per K=32 tile, end of round 2); "
                    "GRBM_GUI_ACTIVE is summed over 8 XCDs"}
     if fetch:
         res["hbm_fetch_bytes_corrected"] = 2 * counters(fetch)["FETCH_SIZE"] * 1024
