@@ -597,3 +597,46 @@ def test_rollout_darkroom_workspace_matches_lds_path():
     for t in range(N):
         f = min(first[t] + 1, steps)  # logits of steps <= first[t] were computed on identical windows
         assert_logits(outs[1]["logits"][:f, t], outs[0]["logits"][:f, t])
+
+
+@pytest.mark.parametrize("factor", [1.0 / 64, 4.0, 8.0])
+def test_prefill_fp16_split_scales_follow_the_weights(factor):
+    """The window forwards run every product as fp16 two-part split products whose power-of-two
+    scales come from static bounds on the weights (dpt_abi.hip fwd_scales).  With the block
+    weights scaled by 1/64, 4 or 8 (and the LayerNorm gains by 3 for the large factors, so scores
+    and activations grow too) nothing overflows fp16 and small values keep their precision: against
+    the float64 oracle the MFMA prefill is as accurate as the fp32 position-by-position path (within
+    the logit bar, or within twice the fp32 path's own error where large scores make fp32 itself
+    miss it: factor 8 gives 5.0e-5 vs 3.8e-5, scripts/scale_stress.py)."""
+    import dpt_hip
+    g = golden("forward_darkroom.npz")
+    H, sd, A, L, E = (int(x) for x in g["cfg"])
+    w = {}
+    for k, v in g.items():
+        if not k.startswith("w/"):
+            continue
+        t = v.astype(np.float32).copy()
+        if any(s in k for s in ("c_fc.weight", "c_proj.weight", "c_attn.weight")):
+            t *= factor
+        if factor > 1 and ("ln_1.weight" in k or "ln_2.weight" in k):
+            t *= 3.0
+        w[k[2:]] = t
+    m = dpt_hip.DeviceModel({k: torch.from_numpy(v) for k, v in w.items()}, L, sd, A, 4 * (1 + H))
+    W = O.split_weights(w, L)
+    rs = np.random.RandomState(31)
+    for N, C in ((32, 100), (6, 300)):
+        q = rs.randn(N, sd).astype(np.float32)
+        cs, cn = rs.randn(N, C, sd).astype(np.float32), rs.randn(N, C, sd).astype(np.float32)
+        ca = np.eye(A, dtype=np.float32)[rs.randint(0, A, (N, C))]
+        cr = rs.randn(N, C).astype(np.float32)
+        ref = O.transformer_forward(W, q, cs, ca, cn, cr, test=True)
+        err = {}
+        try:
+            for on in (True, False):
+                dpt_hip.set_prefill(on)
+                lg = m.forward_window(q, cs, ca, cn, cr).cpu().numpy().astype(np.float64)
+                assert np.isfinite(lg).all()
+                err[on] = float((np.abs(lg - ref) / np.maximum(1.0, np.abs(ref))).max())
+        finally:
+            dpt_hip.set_prefill(True)
+        assert err[True] <= max(LOGIT_TOL, 2.0 * err[False]), err
