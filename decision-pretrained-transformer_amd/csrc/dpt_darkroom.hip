@@ -94,7 +94,8 @@ struct alignas(16) DrSmem {
     // per-episode logits memo, one row per grid state (dim * dim <= kMemoStates)
     float memo_lg[kMemoStates][kDrA];
     double memo_q[kMemoStates][kDrA];  // and their selection cdf (cdf_fixed), so a hit selects by 5 compares
-    int memo_ok[kMemoStates];
+    // (no separate valid flag: an empty row holds memo_q[s][0] = -1 and memo_lg[s][0] = NaN, so a
+    // hit is decided by the row's own values, read in one LDS round trip)
     double u_ep[kFwdT];                // this episode's selection uniforms, one per step
     int sx, sy, nfwd, tnext;
 };
@@ -275,7 +276,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         }
         // thread 0's copy of the state and the episode's return (it runs every selection)
         int cur_x = 0, cur_y = 0, cur_ret = 0;
-        for (int i = tid; i < kMemoStates; i += blockDim.x) S.memo_ok[i] = 0;
+        for (int i = tid; i < kMemoStates; i += blockDim.x) {
+            S.memo_q[i][0] = -1.0;
+            S.memo_lg[i][0] = __builtin_nanf("");
+        }
         // the episode's selection uniforms up front, one thread per step (off the serial
         // select chain of thread 0; ordered before their use by the barriers below)
         if (p.sample) {
@@ -358,11 +362,16 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     int tt = t;
                     while (tt < p.horizon) {
                         const int sidx = cur_x * p.dim + cur_y;
-                        if (!S.memo_ok[sidx]) break;
                         float lg[kDrA];
+                        double qv[kDrA];
 #pragma unroll
-                        for (int k = 0; k < kDrA; ++k) lg[k] = S.memo_lg[sidx][k];
-                        finish_step(lg, S.memo_q[sidx], tt, cur_x, cur_y);
+                        for (int k = 0; k < kDrA; ++k) {
+                            lg[k] = S.memo_lg[sidx][k];
+                            qv[k] = S.memo_q[sidx][k];
+                        }
+                        // a stored row: sampling reads its cdf (q[0] >= 0), greedy its logits
+                        if (p.sample ? !(qv[0] >= 0.0) : __builtin_isnan(lg[0])) break;
+                        finish_step(lg, qv, tt, cur_x, cur_y);
                         ++tt;
                     }
                     S.sx = cur_x;
@@ -445,10 +454,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             sdot = fmaf(q[j][4 + r], kc[r], sdot);
                         }
                         sdot = sum_cols(sdot);
-                        const float s0 = sdot * scale;
+                        const float s0 = sdot * (scale * 1.4426950408889634f);  // exp2 domain, as attend's m
                         const float mt = S.l0m[tok], lt = S.l0l[tok];
                         const float mn = fmaxf(mt, s0);
-                        const float ea = __expf(mt - mn), eb = __expf(s0 - mn);
+                        const float ea = __builtin_amdgcn_exp2f(mt - mn), eb = __builtin_amdgcn_exp2f(s0 - mn);
                         const float inv = 1.0f / (lt * ea + eb);
                         floatx4 oa, ob;
                         if constexpr (kWs) {
@@ -765,7 +774,6 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                                 S.memo_lg[sidx][k] = lg[k];
                                 S.memo_q[sidx][k] = q[k];
                             }
-                            S.memo_ok[sidx] = 1;
                         }
                         S.nfwd += 1;
                         finish_step(lg, q, t, sx, sy);

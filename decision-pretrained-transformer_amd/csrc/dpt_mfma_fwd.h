@@ -152,7 +152,7 @@ __device__ inline floatx4 mfma_x3(const Split2& a, const Split2& b, floatx4 acc)
 }
 // 2^e as a float (|e| < 127)
 __device__ inline float exp2i(int e) { return __int_as_float((e + 127) << 23); }
-// scale of the attention probabilities in P V (P <= e^8 < 2^12, so P x 2^kPExp < 2^14)
+// scale of the attention probabilities in P V (P <= 2^8, so P x 2^kPExp < 2^14)
 constexpr int kPExp = 2;
 
 // acc + A B over k = 32, smallest part products first
@@ -404,8 +404,9 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
 
 // Causal flash attention of query block qb over keys [key_lo, 16*qb + c]:
 // per token column a softmax reference m (-inf when no key; never more than
-// kSlack below the column's max), l = sum_s e^(s-m) and the unnormalised o^T =
-// sum_s e^(s-m) v_s (C-layout).
+// kSlack below the column's max), l = sum_s 2^(s-m) and the unnormalised o^T =
+// sum_s 2^(s-m) v_s (C-layout), all in the exp2 domain: s and m are the scores
+// times log2(e) (folded into the scale), so each probability is one v_exp_f32.
 template <class KV>
 __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
                               float& lsum, float (&o)[8], const ModelView& M) {
@@ -417,6 +418,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     // and lsum, which shortens the per-tile chain (the test is one wave vote).
     constexpr float kSlack = 32.f;
     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
+    scale *= 1.4426950408889634f;  // log2(e): the exp2 domain
 #ifndef DPT_ATTN_F32
     // scores on fp16 two-part products: keys x 2^attn_ey, queries x 2^attn_eq, and the
     // exact power of two folded into the 1/sqrt(d) scale
@@ -428,7 +430,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         // the two tiles is the B operand as it stands).  An unpaired last tile reads the
         // pair's second tile from LDS with probability 0 (the rollout zeroes VS at launch,
         // so it holds finite values).  The softmax reference moves as in the per-tile
-        // form below, one vote per pair, but with kSlackP = 8: P <= e^8, so P x 2^kPExp
+        // form below, one vote per pair, but with kSlackP = 8: P <= 2^8, so P x 2^kPExp
         // fits fp16, and o accumulates at scale 2^(attn_ey + kPExp).
         constexpr float kSlackP = 8.f;
         m = -INFINITY;
@@ -459,7 +461,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
             if (__builtin_amdgcn_ballot_w64(mt > m + kSlackP)) {  // wave-uniform
                 mt = max_cols(mt);
                 const float mn = fmaxf(m, mt);
-                const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+                const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
                 lsum *= corr;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -471,7 +473,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
             const float base = m == -INFINITY ? 0.f : m;  // no key yet: keep 0, not NaN
             float pr[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) pr[r] = __expf(sv[r] - base);
+            for (int r = 0; r < 8; ++r) pr[r] = __builtin_amdgcn_exp2f(sv[r] - base);
             lsum += ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
             const Split2 ps = split2(pr, exp2i(kPExp));
             const int pp = kb >> 1;
@@ -529,7 +531,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         if (__builtin_amdgcn_ballot_w64(mt > m + kSlack)) {  // wave-uniform
             mt = max_cols(mt);
             const float mn = fmaxf(m, mt);
-            const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+            const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
             lsum *= corr;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -541,7 +543,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         const float base = m == -INFINITY ? 0.f : m;  // no key yet: keep 0, not NaN
         float pr[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - base);
+        for (int r = 0; r < 4; ++r) pr[r] = __builtin_amdgcn_exp2f(sv[r] - base);
         lsum += (pr[0] + pr[1]) + (pr[2] + pr[3]);
 #ifdef DPT_EXP_NOPV  // timing only (wrong results): no PV product
         o0[0] += pr[0] + pr[1];
