@@ -12,7 +12,7 @@ if [ -d $G/prof_dr_$TAG ]; then
   cp $G/prof_dr_$TAG/pmc_mfma/run_counter_collection.csv $D/darkroom_pmc_mfma.csv
   cp $G/prof_dr_$TAG/pmc_mem/run_counter_collection.csv $D/darkroom_pmc_fetch.csv
 fi
-for w in bandit linear darkroom; do
+for w in bandit linear darkroom darkroom_c5; do
   [ -f $G/bench_$w.log ] && tail -n1 $G/bench_$w.log > $D/bench_$w.json
 done
 [ -f $G/gpu_tests.log ] && cp $G/gpu_tests.log $D/gpu_tests.log.txt
