@@ -77,7 +77,7 @@ using namespace dpt;
 struct dpt_model {
     dpt_model_desc desc;
     float* blob;
-    float* frag;  // the blocks' weights split into bf16 parts in MFMA operand order, attention folded (dpt_mfma_fwd.h Frag3)
+    float* frag;  // the blocks' weights split into fp16 parts in MFMA operand order, attention folded (dpt_mfma_fwd.h Frag3)
     float* l0;    // every block's attention folded (dpt_common.h L0Off)
     ModelView view;
 };

@@ -15,10 +15,10 @@
 // reads feature 16*(s>>2) + 4g + (s&3)), so c_attn, attention, c_proj, c_fc,
 // gelu and mlp.c_proj chain in registers; only K (token-major) and V
 // (feature-major) go through LDS, because every later token reads them.
-// Weights are the A operand, split into bf16 parts and pre-packed per layer in
+// Weights are the A operand, split into fp16 parts and pre-packed per layer in
 // operand order (Frag3, pack_split_kernel) and read through one buffer
-// descriptor; every dense product runs as fp32-accurate split products on the
-// bf16 matrix cores (mfma_x6), the attention on the fp32 MFMA.
+// descriptor; every product (dense and attention) runs as fp32-accurate fp16
+// two-part split products on the fp16 matrix cores (dpt_mfma_fwd.h mfma_x3).
 //
 // Exact restructurings (same arithmetic up to fp32 summation order):
 //  * layer 0: within an episode the context tokens' layer-0 keys/values are
@@ -75,7 +75,7 @@ struct PTop {
 
 // 16-B multiple: the dynamic parameter block P follows it and is read with 16-B loads.
 // kWs (a per-task workspace is given): the layer-0 partials live in the workspace and
-// the freed LDS holds the values as split tiles (both attention products on mfma_x6);
+// the freed LDS holds the values as split pair tiles (P V on mfma_x3);
 // without one they stay here and the values are fp32.
 template <bool kWs>
 struct alignas(16) DrSmem {
@@ -549,7 +549,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 const Split2 pj0 = f3.ld2(Frag3::proj), pj1 = f3.ld2(Frag3::proj + 1);
                 const Split2 fj0 = f3.ld2(Frag3::fc + 2 * wave), fj1 = f3.ld2(Frag3::fc + 2 * wave + 1);
                 // (1) the attention as flash partials (m, l, o): with split values key
-                // tiles 2 wave and 2 wave + 1 (one pair, both products on mfma_x6), else
+                // tiles 2 wave and 2 wave + 1 (one pair, both products on mfma_x3), else
                 // key tiles wave and wave + 4
                 const int nparts = kSplitV ? (qlast >> 1) + 1 : qlast + 1;
                 if constexpr (kSplitV) {
@@ -812,7 +812,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     }
 }
 
-// The model's fragment buffer: the bf16 3-way split weight tiles (Frag3) of every layer.
+// The model's fragment buffer: the fp16 two-part split weight tiles (Frag3) of every layer,
+// W x 2^mlp_ew (c_fc, mlp.c_proj) or W x 2^attn_ew (G, Wvp).
 __global__ void pack_split_kernel(ModelView M, unsigned short* __restrict__ out) {
     const int per_layer = Frag3::tiles * 64 * 8;
     const int total = M.n_layer * per_layer;
@@ -832,24 +833,13 @@ __global__ void pack_split_kernel(ModelView M, unsigned short* __restrict__ out)
             const int ob = (tile - Frag3::mp) >> 2, pair = (tile - Frag3::mp) & 3;
             w = W[LayerOff::mp_w + (32 * pair + kin) * kE + ob * 16 + c];
         }
-        unsigned short* d = out + (size_t)layer * (Frag3::bytes / 2) + ((size_t)tile * 3 * 64 + lane) * 8 + j;
-        {  // fp16 two-part split of W x 2^mlp_ew (MLP) or 2^attn_ew (G, Wvp): Split2
-            const int e = tile >= Frag3::fc ? M.mlp_ew : M.attn_ew;
-            const float ws = w * __int_as_float((e + 127) << 23);
-            const _Float16 h = (_Float16)ws;
-            const _Float16 m = (_Float16)(ws - (float)h);
-            d[0] = __builtin_bit_cast(unsigned short, h);
-            d[64 * 8] = __builtin_bit_cast(unsigned short, m);
-            d[2 * 64 * 8] = 0;
-            continue;
-        }
-        const __bf16 h = (__bf16)w;
-        const float r = w - (float)h;
-        const __bf16 m = (__bf16)r;
-        const __bf16 l = (__bf16)(r - (float)m);
+        unsigned short* d = out + (size_t)layer * (Frag3::bytes / 2) + ((size_t)tile * Frag3::parts * 64 + lane) * 8 + j;
+        const int e = tile >= Frag3::fc ? M.mlp_ew : M.attn_ew;
+        const float ws = w * __int_as_float((e + 127) << 23);
+        const _Float16 h = (_Float16)ws;
+        const _Float16 m = (_Float16)(ws - (float)h);
         d[0] = __builtin_bit_cast(unsigned short, h);
         d[64 * 8] = __builtin_bit_cast(unsigned short, m);
-        d[2 * 64 * 8] = __builtin_bit_cast(unsigned short, l);
     }
 }
 

@@ -24,7 +24,6 @@ struct PL {
     static constexpr int ln1_g = 0, ln1_b = 32, attn_b = 64, proj_b = 160, ln2_g = 192, ln2_b = 224,
                          fc_b = 256, mp_b = 384, size = 416;
 };
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 // This workgroup's keys and values of the current layer, for windows of up to TMAX
 // tokens.  Keys are either fp32 token-major (K) or, with SPLITK, the fp16 two-part A
@@ -46,7 +45,7 @@ struct KVBuf {
     float Vt[SPLITV ? 1 : kE][TMAX + 4];
 };
 #ifndef DPT_ATTN_F32
-constexpr bool kSplitKeys = true;  // scores on mfma_x3 (and, with SPLITV, PV on mfma_x6)
+constexpr bool kSplitKeys = true;  // scores on mfma_x3 (and, with SPLITV, P V too)
 #else
 constexpr bool kSplitKeys = false;
 #endif
@@ -66,66 +65,16 @@ __device__ inline int lane_id() {
     return t & 63;
 }
 
-// ---- fp32 products on the bf16 matrix cores (emulated fp32, "x6").  A value is
-// split exactly into three bf16 parts, v = h + m + l + O(2^-24 v) (each residual is
-// exact in fp32), and a K=32 product W^T x^T is the sum of the six part products
-// whose size is at least 2^-16 of h*h (m*l, l*m, l*l are below fp32's own rounding).
-// One v_mfma_f32_16x16x32_bf16 (16 cycles) does the K=32 work of eight
-// v_mfma_f32_16x16x4_f32 (32 cycles each): six of them take 96 cycles instead of 256.
-// The bf16 products are exact and accumulate in fp32, so the result agrees with the
-// fp32 MFMA chain to fp32 rounding (not bit for bit).  Operand layout: lane (g, c)
-// supplies its 8 C-layout values (features 16*(j>>2) + 4g + (j&3), j = 0..7) as the
-// 8 k-elements of its lane group; the weights are packed with the same k order
-// (Frag3), so the logical k permutation cancels.
-struct Split3 {
-    bf16x8 h, m, l;
-};
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float floatx2 __attribute__((ext_vector_type(2)));
-__device__ inline floatx2 widen_bf16x2(bf16x2 b) {
-    const unsigned u = __builtin_bit_cast(unsigned, b);
-    return floatx2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
-}
-// pairwise: one v_cvt_pk_bf16_f32 (round to nearest even) per part and pair, the
-// residuals by packed subtraction
-__device__ inline Split3 split3(const float (&v)[8]) {
-#ifdef DPT_EXP_SPLIT1  // timing only: hi part alone (wrong results)
-    Split3 t;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        t.h[k] = (__bf16)v[k];
-        t.m[k] = t.h[k];
-        t.l[k] = t.h[k];
-    }
-    return t;
-#endif
-    unsigned hh[4], mm[4], ll[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const floatx2 x = {v[2 * p], v[2 * p + 1]};
-        const bf16x2 h = __builtin_convertvector(x, bf16x2);
-        const floatx2 r = x - widen_bf16x2(h);
-        const bf16x2 m = __builtin_convertvector(r, bf16x2);
-        const floatx2 q = r - widen_bf16x2(m);
-        hh[p] = __builtin_bit_cast(unsigned, h);
-        mm[p] = __builtin_bit_cast(unsigned, m);
-        ll[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(q, bf16x2));
-    }
-    return Split3{__builtin_bit_cast(bf16x8, uint4{hh[0], hh[1], hh[2], hh[3]}),
-                  __builtin_bit_cast(bf16x8, uint4{mm[0], mm[1], mm[2], mm[3]}),
-                  __builtin_bit_cast(bf16x8, uint4{ll[0], ll[1], ll[2], ll[3]})};
-}
-__device__ inline floatx4 mfma_bf16(const bf16x8& a, const bf16x8& b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 // ---- dense products on fp16 two-part splits ("x3"): v = h + m + O(2^-22 v) with
 // h, m fp16 (11-bit significands; the residual is exact in fp32), and a K = 32 product
 // is h_a h_b + h_a m_b + m_a h_b (exact fp16 products, fp32 accumulation) on three
-// v_mfma_f32_16x16x32_f16, half the matrix cycles of mfma_x6.  The dropped terms are
+// v_mfma_f32_16x16x32_f16: 48 matrix cycles per K = 32 tile instead of the 256 of eight
+// v_mfma_f32_16x16x4_f32 (and half those of a bf16 three-part form).  The dropped terms are
 // below 2^-21 of |a||b| per product; weights and activations are scaled by powers of
 // two (ModelView mlp_* / attn_*) so their residuals stay normal fp16 numbers.  Every
-// product of the forward runs this way except the attention's P V (P reaches e^32).
+// product of the forward runs this way (P V with P <= 2^8, see attend).
 typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 struct Split2 {
     halfx8 h, m;
 };
@@ -155,39 +104,28 @@ __device__ inline float exp2i(int e) { return __int_as_float((e + 127) << 23); }
 // scale of the attention probabilities in P V (P <= 2^8, so P x 2^kPExp < 2^14)
 constexpr int kPExp = 2;
 
-// acc + A B over k = 32, smallest part products first
-__device__ inline floatx4 mfma_x6(const Split3& a, const Split3& b, floatx4 acc) {
-    acc = mfma_bf16(a.m, b.m, acc);
-    acc = mfma_bf16(a.h, b.l, acc);
-    acc = mfma_bf16(a.l, b.h, acc);
-    acc = mfma_bf16(a.h, b.m, acc);
-    acc = mfma_bf16(a.m, b.h, acc);
-    return mfma_bf16(a.h, b.h, acc);
-}
 
 // The split weight tiles of one block (the model's fragment buffer, per layer):
-// [tile][part h|m|l][64 lanes][8 bf16], tile element (lane (g, c), j) = W[in][out]
-// with in = 16*(j>>2) + 4g + (j&3) (mp: hidden 32*pair + that) and out = 16*ob + c.
-// The MLP tiles (fc, mp) hold the fp16 two-part split of W x 2^mlp_ew in parts h, m.
+// [tile][part h|m][64 lanes][8 fp16], tile element (lane (g, c), j) = W[in][out] x 2^e
+// with in = 16*(j>>2) + 4g + (j&3) (mp: hidden 32*pair + that) and out = 16*ob + c;
+// e = mlp_ew for the MLP tiles (fc, mp), attn_ew for G and Wvp.
 struct Frag3 {
     static constexpr int attn = 0;   // 2 tiles: G
     static constexpr int proj = 2;   // 2 tiles: Wvp
     static constexpr int fc = 4;     // 8 tiles: c_fc, output chunk ob
     static constexpr int mp = 12;    // [2 ob][4 pairs]: mlp.c_proj over hidden chunks 2p, 2p+1
     static constexpr int tiles = 20;
-    static constexpr int bytes = tiles * 3 * 64 * 16;  // 61,440 per layer
+    static constexpr int parts = 2;
+    static constexpr int bytes = tiles * parts * 64 * 16;  // 40,960 per layer
 };
 struct FragSrc3 {
     __amdgpu_buffer_rsrc_t r;
     int base;  // byte offset of this layer's tiles
-    __device__ bf16x8 ld1(int tile, int part) const {
-        return __builtin_bit_cast(
-            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, base + (tile * 3 + part) * 1024, 0));
+    __device__ halfx8 ld1(int tile, int part) const {
+        return __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(
+                                              r, lane_id() * 16, base + (tile * Frag3::parts + part) * 1024, 0));
     }
-    __device__ Split3 ld(int tile) const { return Split3{ld1(tile, 0), ld1(tile, 1), ld1(tile, 2)}; }
-    __device__ Split2 ld2(int tile) const {
-        return Split2{__builtin_bit_cast(halfx8, ld1(tile, 0)), __builtin_bit_cast(halfx8, ld1(tile, 1))};
-    }
+    __device__ Split2 ld2(int tile) const { return Split2{ld1(tile, 0), ld1(tile, 1)}; }
     __device__ FragSrc3 layer(int l) const { return FragSrc3{r, l * Frag3::bytes}; }
 };
 
@@ -495,7 +433,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
     for (int kb = 0; kb <= qb; ++kb) {
 #ifndef DPT_ATTN_F32
-        // S^T = K Q^T on mfma_x6: the key tile is the A operand (lane (g, c): key
+        // S^T = K Q^T on mfma_x3: the key tile is the A operand (lane (g, c): key
         // 16 kb + c, the lane group's 8 features), Q^T the B operand (q's C-layout)
         Split2 ks;
         if constexpr (KV::kSplitK) {
