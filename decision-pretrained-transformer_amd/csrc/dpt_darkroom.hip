@@ -50,6 +50,15 @@ __device__ unsigned long long g_dr_last;
     } while (0)
 #endif
 
+// (A/B, DPT_EXP_PRIO) wave 0's serial tail and thread 0's memo-hit chain at issue priority 3
+#ifdef DPT_EXP_PRIO
+#define DPT_TAIL_PRIO(p) __builtin_amdgcn_s_setprio(p)
+#else
+#define DPT_TAIL_PRIO(p) \
+    do {                 \
+    } while (0)
+#endif
+
 namespace dpt {
 
 constexpr int kDrA = 5;                     // DarkRoom actions
@@ -359,6 +368,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 // episode (a memo hit needs no forward); the other threads wait at one
                 // barrier for the first state that needs one
                 if (tid == 0) {
+                    DPT_TAIL_PRIO(3);  // the memo-hit chain is the workgroup's critical path
                     int tt = t;
                     while (tt < p.horizon) {
                         const int sidx = cur_x * p.dim + cur_y;
@@ -377,6 +387,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     S.sx = cur_x;
                     S.sy = cur_y;
                     S.tnext = tt;
+                    DPT_TAIL_PRIO(0);
                 }
                 bar_lds();
                 DR_STAMP(2 * L + 4);
@@ -728,6 +739,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 DR_STAMP(2 * L);
                 // (3) wave 0: residual, ln_f, head, selection, env step
                 if (wave == 0) {
+                    // the step's serial tail: issue ahead of the other workgroup's waves on this SIMD
+                    DPT_TAIL_PRIO(3);
                     const int lane = lane_id(), g = lane >> 4;
                     floatx4 ya = ld4(W + PL::mp_b + 4 * g), yb = ld4(W + PL::mp_b + 16 + 4 * g);
 #pragma unroll
@@ -781,6 +794,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         S.sy = cur_y;
                     }
                     DR_STAMP(2 * L + 3);
+                    DPT_TAIL_PRIO(0);
                 }
             }
             bar_lds();
