@@ -189,6 +189,8 @@ def main():
         workload = (f"{A}-arm {'Gaussian' if wl == 'bandit' else 'linear (d=2)'} bandit online eval, DPT sampling "
                     f"policy in the loop, H={H}, {N} tasks/GPU, var={args.var}, L={L} E=32 1 head")
         cfg = {"tasks_per_gpu": N, "horizon": H, "arms": A}
+        # rollout_bandit_kernel: fp32 VALU + v_mfma_f32_16x16x4_f32 products; env arithmetic fp64
+        dtype = "f32 (model: VALU + f32 MFMA) / f64 (env, rewards)"
     else:
         from ctrls.ctrl_darkroom import DarkroomTransformerController
         from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec
@@ -197,7 +199,7 @@ def main():
         dpt_hip.set_darkroom_memo(args.darkroom_memo)
         sd, tmodel = synthetic_state_dict(L, 2, 5, H, seed=0)
         tmodel.load_state_dict({**sd, "transformer.wte.weight": tmodel.transformer.wte.weight}, strict=True)
-        tmodel.cuda()
+        tmodel.cuda().eval()  # as eval.py:152 does
         goals = np.array([(j, i) for j in range(10) for i in range(10)])
         np.random.RandomState(0).shuffle(goals)   # collect_data.py:408-409 order, cycled to N
         goals_all = goals[np.arange(n_total) % 100]
@@ -215,6 +217,11 @@ def main():
         env_steps_per_step = n_total * Heps * H
         workload = f"DarkRoom 10x10 online eval, DPT sampling policy, H=horizon={H}, Heps={Heps}, {N} tasks/GPU"
         cfg = {"tasks_per_gpu": N, "horizon": H, "episodes": Heps}
+        # rollout_darkroom_kernel: every matrix product as fp16 two-part splits on
+        # v_mfma_f32_16x16x32_f16 (h*h + h*m + m*h, fp32 accumulation: about 2^-21 relative per
+        # product); LayerNorm, softmax, gelu, embedding, head in fp32; cdf in fp64
+        dtype = ("f16x2-split MFMA products (fp32 accumulate, ~2^-21/product) + f32 VALU / "
+                 "f64 selection cdf; int32 grid")
 
     for w in range(args.warmup):
         one(w)
@@ -305,7 +312,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32 (model) / f64 (env, rewards)",
+        "dtype": dtype,
         "data": "synthetic: seeded GPT-2-init weights (+0.05 N(0,1)); tasks per SURVEY.md §8(d)",
         "config": dict(workload=workload, parallelism=f"task-sharded x{world}",
                        env_steps_per_step=env_steps_per_step, **cfg),

@@ -51,15 +51,18 @@ def rollin_bandit(env, cov, orig=False):
     return xs[0], us[0], xps[0], rs[0]
 
 
-def rollin_linear_bandit_vec(envs):
-    """collect_data.py:56-80: Thompson-sampling rollout (prior N(0, 1)) through deploy_online_vec."""
+def rollin_linear_bandit_vec(envs, noise=None, policy_noise=None):
+    """collect_data.py:56-80: Thompson-sampling rollout (prior N(0, 1)) through deploy_online_vec.
+    ``noise`` (H, N) reward normals and ``policy_noise`` (H, N, A) posterior normals, optional:
+    the reference's np.random.normal draws, injected (default: Philox)."""
     from ctrls.ctrl_bandit import ThompsonSamplingPolicy
     from evals import eval_bandit
     H = envs[0].H_context
     thmp = ThompsonSamplingPolicy(envs[0], std=envs[0].var, sample=True, prior_mean=0.0, prior_var=1.0,
                                   warm_start=False, batch_size=len(envs))
     vec_env = bandit_env.BanditEnvVec(envs)
-    _, meta = eval_bandit.deploy_online_vec(vec_env, thmp, H, include_meta=True)
+    _, meta = eval_bandit.deploy_online_vec(vec_env, thmp, H, include_meta=True, noise=noise,
+                                            policy_noise=policy_noise)
     return (meta["context_states"], meta["context_actions"], meta["context_next_states"],
             meta["context_rewards"][:, :, 0])
 

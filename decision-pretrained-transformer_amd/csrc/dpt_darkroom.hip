@@ -52,14 +52,8 @@ __device__ unsigned long long g_dr_last;
 
 // wave 0's serial tail and thread 0's memo-hit chain at issue priority 3, ahead of the
 // other workgroup's waves on the same SIMD (only issue order changes: bit-identical;
-// -0.9 % at config 3; DPT_NO_TAIL_PRIO builds it without, for A/B)
-#ifndef DPT_NO_TAIL_PRIO
+// -0.9 % at config 3)
 #define DPT_TAIL_PRIO(p) __builtin_amdgcn_s_setprio(p)
-#else
-#define DPT_TAIL_PRIO(p) \
-    do {                 \
-    } while (0)
-#endif
 
 namespace dpt {
 
@@ -622,24 +616,11 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     for (int h = 0; h < 2; ++h) {
                         const int kt = wave + 4 * h;
                         if (kt > qlast) break;
-#ifndef DPT_ATTN_F32
                         // split key tile x the split query, broadcast to every column
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
                         const Split2 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane]};
                         const floatx4 sc = mfma_x3(ks, split2(qv, exp2i(M.attn_eq)), floatx4{0.f, 0.f, 0.f, 0.f}) *
                                            exp2i(-(M.attn_ey + M.attn_eq));
-#else
-                        const floatx4 k0 = ld4(&S.kv.K[kt * 16 + c][4 * g]);
-                        const floatx4 k1 = ld4(&S.kv.K[kt * 16 + c][16 + 4 * g]);
-                        floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
-                        (void)lane;
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) {
-                            sa = mfma4(k0[s4], qa[s4], sa);
-                            sb = mfma4(k1[s4], qc[s4], sb);
-                        }
-                        const floatx4 sc = sa + sb;
-#endif
                         float sv[4], mt = -INFINITY;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -777,11 +758,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     DR_STAMP(2 * L + 2);
                     if (lane == 0) {
                         double q[kDrA] = {0.0, 0.0, 0.0, 0.0, 0.0};
-#ifdef DPT_EXP_NOCDF  // timing only (wrong results): no softmax cdf
-                        if (p.sample) q[0] = lg[0];
-#else
                         if (p.sample) cdf_fixed<kDrA>(lg, p.temp, q);
-#endif
                         if (p.memo) {
                             const int sidx = sx * p.dim + sy;
 #pragma unroll

@@ -61,18 +61,6 @@ constexpr int kRows = 4;                  // K/V rows (of 8 positions) in flight
 #endif
 constexpr int kYRows = DPT_YROWS;         // y rows in flight per wave (rollout blocks >= 1; 8: -1.5 % vs 4)
 constexpr int kChunks = kFF / 16;         // hidden-unit chunks of the fused c_fc -> mlp.c_proj
-// timing-only diagnostics (wrong results; never in the shipped library): drop the
-// cached positions of block 0's attention or of the y streams
-#ifdef DPT_EXP_NOL0
-#define DPT_EXP_L0POS(p) 0
-#else
-#define DPT_EXP_L0POS(p) (p)
-#endif
-#ifdef DPT_EXP_NOSTREAM
-#define DPT_EXP_YPOS(p) 0
-#else
-#define DPT_EXP_YPOS(p) (p)
-#endif
 #ifndef DPT_DEFAULT_CACHE_BUDGET
 #define DPT_DEFAULT_CACHE_BUDGET (224ll << 20)
 #endif
@@ -916,7 +904,7 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
         if constexpr (L0M > 0) {
             if (li == 0) {  // block 0: every wave takes a share of the tile's cached positions
                 l0_tiles<L0M, TILE>(tokrec(kv, max_pos, tile0, 0, TILE, 0), min(TILE, N - tile0),
-                              DPT_EXP_L0POS(pos), M.wpe, &S.q[0][0], &S.vcur[0][0], PL + PLay::ln1_g,
+                              pos, M.wpe, &S.q[0][0], &S.vcur[0][0], PL + PLay::ln1_g,
                               &S.part[0][0][0], wave, lane);
                 bar_lds();
             }
@@ -940,11 +928,11 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                         (L0M > 0 && l0) ? l0_merge<(L0M > 0 ? L0M : 1)>(&S.part[0][0][0], wave, S.q[wave], S.x[wave], D + rl.base,
                                                              P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
                                                              PL + PLay::ln1_b, lane)
-                        : l0 ? attend_l0<TILE>(reinterpret_cast<const float4*>(tokrec(kv, max_pos, tile0, 0, TILE, wave)), M.wpe, DPT_EXP_L0POS(pos), S.q[wave], S.x[wave],
+                        : l0 ? attend_l0<TILE>(reinterpret_cast<const float4*>(tokrec(kv, max_pos, tile0, 0, TILE, wave)), M.wpe, pos, S.q[wave], S.x[wave],
                                        D + rl.base, P + pl.emb_w + (2 + M.A) * kE, PL + PLay::ln1_g,
                                        PL + PLay::ln1_b, nullptr, lane)
                            // scores y_p . u, output sum_p P_p y_p; y_pos is in S.kcur
-                           : attend_one<true, kYRows, YPS>(yc, yc, DPT_EXP_YPOS(pos), S.q[wave], S.kcur[wave], S.kcur[wave], nullptr,
+                           : attend_one<true, kYRows, YPS>(yc, yc, pos, S.q[wave], S.kcur[wave], S.kcur[wave], nullptr,
                                                       lane, lpin(li));
                     // c_proj (folded Wvp) + residual + ln_2 of this task, in this wave
                     proj_ln_task(o4, D + rl.wvp + li * kE * kE, D + rl.bvp + li * kE, PL + PLay::ln2_g,
@@ -1014,32 +1002,17 @@ __device__ void decode_position(Smem& S, const float* P, const ParamLDS& pl, con
                 w2b[s] = __ldg(W2 + (size_t)s * kE + 16 + i16);
             }
             floatx4 ht = {0.f, 0.f, 0.f, 0.f};
-#ifdef DPT_EXP_MLPCHAIN  // timing only (wrong results): a 3-deep c_fc chain, 2-deep c_proj
-#pragma unroll
-            for (int s = 0; s < 3; ++s)
-                ht = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[s] + w1[s + 3] + w1[(s + 6) & 7], S.xn[i16][4 * s + kq], ht, 0, 0, 0);
-#else
 #pragma unroll
             for (int s = 0; s < 8; ++s)
                 ht = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[s], S.xn[i16][4 * s + kq], ht, 0, 0, 0);
-#endif
             // ht[r] = h^T[unit 16*wave + 4*kq + r][task i16]
             floatx4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
-#ifdef DPT_EXP_MLPCHAIN
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const float hv = gelu_new(ht[s] + ht[s + 2] + PL[PLay::fc_b + wave * 16 + kq * 4 + s]);
-                p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2a[s] + w2a[s + 2], p0, 0, 0, 0);
-                p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2b[s] + w2b[s + 2], p1, 0, 0, 0);
-            }
-#else
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const float hv = gelu_new(ht[s] + PL[PLay::fc_b + wave * 16 + kq * 4 + s]);
                 p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2a[s], p0, 0, 0, 0);
                 p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv, w2b[s], p1, 0, 0, 0);
             }
-#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 S.part[wave][kq * 4 + r][i16] = p0[r];

@@ -44,11 +44,7 @@ struct KVBuf {
     halfx8 VS[SPLITV ? TMAX / 32 : 1][SPLITV ? 2 : 1][SPLITV ? 2 : 1][SPLITV ? 64 : 1];
     float Vt[SPLITV ? 1 : kE][TMAX + 4];
 };
-#ifndef DPT_ATTN_F32
 constexpr bool kSplitKeys = true;  // scores on mfma_x3 (and, with SPLITV, P V too)
-#else
-constexpr bool kSplitKeys = false;
-#endif
 
 __device__ inline floatx4 mfma4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -189,9 +185,6 @@ __device__ inline float gelu_fast(float x) {
     // = x / (1 + 2^(x * (c1 + c2 x^2))), z = sqrt(2/pi)(x + 0.044715 x^3), log2(e) folded in
     const float c1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
     const float c2 = c1 * 0.044715f;
-#ifdef DPT_EXP_NOGELU  // timing only (wrong results)
-    return x * c2;
-#endif
     const float e = __builtin_amdgcn_exp2f(x * fmaf(x * x, c2, c1));
     return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
@@ -357,7 +350,6 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     constexpr float kSlack = 32.f;
     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
     scale *= 1.4426950408889634f;  // log2(e): the exp2 domain
-#ifndef DPT_ATTN_F32
     // scores on fp16 two-part products: keys x 2^attn_ey, queries x 2^attn_eq, and the
     // exact power of two folded into the 1/sqrt(d) scale
     const Split2 qs = split2(q, exp2i(M.attn_eq));
@@ -427,12 +419,10 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         }
         return;
     }
-#endif
     m = -INFINITY;
     lsum = 0.f;
     floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
     for (int kb = 0; kb <= qb; ++kb) {
-#ifndef DPT_ATTN_F32
         // S^T = K Q^T on mfma_x3: the key tile is the A operand (lane (g, c): key
         // 16 kb + c, the lane group's 8 features), Q^T the B operand (q's C-layout)
         Split2 ks;
@@ -445,18 +435,6 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
             ks = split2(kv, exp2i(M.attn_ey));
         }
         const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
-#else
-        const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
-        const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
-        // two independent 4-deep chains (features 0-15 / 16-31) instead of one 8-deep
-        floatx4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            sa = mfma4(k0[s], q[s], sa);
-            sb = mfma4(k1[s], q[4 + s], sb);
-        }
-        const floatx4 sc = sa + sb;
-#endif
         float sv[4];
         float mt = -INFINITY;
 #pragma unroll
@@ -483,17 +461,12 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
 #pragma unroll
         for (int r = 0; r < 4; ++r) pr[r] = __builtin_amdgcn_exp2f(sv[r] - base);
         lsum += (pr[0] + pr[1]) + (pr[2] + pr[3]);
-#ifdef DPT_EXP_NOPV  // timing only (wrong results): no PV product
-        o0[0] += pr[0] + pr[1];
-        o1[0] += pr[2] + pr[3];
-#else
         const floatx4 v0 = ld4(&S.Vt[c][kb * 16 + 4 * g]);
         const floatx4 v1 = ld4(&S.Vt[16 + c][kb * 16 + 4 * g]);
 #pragma unroll
         for (int s = 0; s < 4; ++s) o0 = mfma4(v0[s], pr[s], o0);
 #pragma unroll
         for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
-#endif
     }
     lsum = sum_cols(lsum);
 #pragma unroll

@@ -65,7 +65,7 @@ __device__ double pw_sum(const double* x, size_t stride, int n) {
 }
 
 struct PolicyParams {
-    int N, H, A, policy, online, type, sample, d, C;
+    int N, H, A, policy, online, type, sample, d, C, step0;
     const int32_t* ctx_actions;
     const double* ctx_rewards;
     int64_t first_task;
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
         } else if (P.policy == DPT_POLICY_LINUCB) {
             if (P.C + h == 0) {  // np.random.choice(np.arange(dim)) for an empty context
                 const double u = P.policy_noise ? P.policy_noise[(size_t)i]
-                                                : philox_uniform(P.seed, 0, task, DPT_STREAM_POLICY);
+                                                : philox_uniform(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_POLICY);
                 a = min((int)(u * A), A - 1);
             } else {
                 const double c00 = 1.0 + xtx[0], c01 = xtx[1], c11 = 1.0 + xtx[3];
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
                     double best = -INFINITY;
                     for (int k = 0; k < A; ++k) {
                         const double g = P.policy_noise ? P.policy_noise[((size_t)h * P.N + i) * A + k]
-                                                        : philox_normal(P.seed, h, task, DPT_STREAM_POLICY + k);
+                                                        : philox_normal(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_POLICY + k);
                         const double v = post_m[k] + post_s[k] * g;
                         if (v > best) { best = v; a = k; }
                     }
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
                         double best = -INFINITY;
                         int am = 0;
                         for (int k = 0; k < A; ++k) {
-                            const double g = philox_normal(P.seed, (uint64_t)h * 128 + s, task, DPT_STREAM_POLICY + k);
+                            const double g = philox_normal(P.seed, ((uint64_t)P.step0 + h) * 128 + s, task, DPT_STREAM_POLICY + k);
                             const double v = post_m[k] + post_s[k] * g;
                             if (v > best) { best = v; am = k; }
                         }
@@ -196,10 +196,10 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
         const double mean = mrow[a];
         double r;
         if (P.type == DPT_BANDIT_BERNOULLI) {
-            const double ur = P.noise ? P.noise[(size_t)h * P.N + i] : philox_uniform(P.seed, h, task, DPT_STREAM_REWARD);
+            const double ur = P.noise ? P.noise[(size_t)h * P.N + i] : philox_uniform(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_REWARD);
             r = (ur < mean) ? 1.0 : 0.0;
         } else {
-            const double g = P.noise ? P.noise[(size_t)h * P.N + i] : philox_normal(P.seed, h, task, DPT_STREAM_REWARD);
+            const double g = P.noise ? P.noise[(size_t)h * P.N + i] : philox_normal(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_REWARD);
             r = gaussian_reward(mean, P.var, g);
         }
         append(a, r);
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
 int launch_rollout_policy(const dpt_policy_rollout_args& a, hipStream_t st) {
     PolicyParams P;
     P.N = a.N; P.H = a.H; P.A = a.A; P.policy = a.policy; P.online = a.online; P.type = a.type;
-    P.sample = a.sample; P.d = a.lin_d; P.C = a.C; P.ctx_actions = a.ctx_actions; P.ctx_rewards = a.ctx_rewards;
+    P.sample = a.sample; P.d = a.lin_d; P.C = a.C; P.step0 = a.step0; P.ctx_actions = a.ctx_actions; P.ctx_rewards = a.ctx_rewards;
     P.first_task = a.first_task; P.var = a.var; P.c = a.c;
     P.ts_std = a.ts_std; P.ts_prior_mean = a.ts_prior_mean; P.ts_prior_var = a.ts_prior_var; P.seed = a.seed;
     P.means = a.means; P.arms = a.arms; P.noise = a.noise; P.policy_noise = a.policy_noise; P.lists = a.workspace;

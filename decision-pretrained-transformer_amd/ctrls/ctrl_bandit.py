@@ -134,7 +134,11 @@ class _KernelPolicy(Controller):
 
     Per-step protocol: ``set_batch_numpy_vec(context)`` then ``act_numpy_vec`` runs the
     kernel for one step on that prefix context.  Inside deploy_online_vec the whole loop
-    runs fused instead (evals.eval_bandit).
+    runs fused instead (evals.eval_bandit).  Both draw the policy's own randomness (Thompson
+    posterior normals, LinUCB's first arm) from the controller's stream: step k of the
+    stream is Philox counter k of one seed, so the per-step and fused loops act on the same
+    draws.  ``policy_noise``, optional: callable(counter) -> that step's draws ((N, A)
+    posterior normals, or (N,) uniforms for LinUCB's first arm), injected instead.
     """
 
     policy = None
@@ -147,6 +151,8 @@ class _KernelPolicy(Controller):
         self.env = env
         self.batch_size = batch_size
         self._stream = _SelectStream()
+        self.policy_noise = None
+        self.first_task = 0  # global id of task 0 (a shard's first task): Philox key
 
     def reset(self):
         return
@@ -163,9 +169,9 @@ class _KernelPolicy(Controller):
         ca, cr = self._ctx()
         means = np.zeros((self.batch_size, self.dim_()))  # the one env step's reward is discarded
         seed, ctr = self._stream.next()
-        step_seed = (seed + ctr * 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
-        out = dpt_hip.rollout_policy(self.policy, means, 1, 0.0, seed=step_seed,
-                                     ctx_actions=ca if ca.shape[1] else None,
+        pn = None if self.policy_noise is None else np.asarray(self.policy_noise(ctr), np.float64)
+        out = dpt_hip.rollout_policy(self.policy, means, 1, 0.0, seed=seed, counter=ctr, first_task=self.first_task,
+                                     policy_noise=pn, ctx_actions=ca if ca.shape[1] else None,
                                      ctx_rewards=cr if ca.shape[1] else None, **self.kernel_kwargs())
         a = out["actions"][:, 0].cpu().numpy()
         self.a = _onehot(a, self.dim_())

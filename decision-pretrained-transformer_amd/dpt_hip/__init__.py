@@ -319,8 +319,9 @@ from ._lib import (POLICY_EMP, POLICY_LCB, POLICY_LINUCB, POLICY_OPT, POLICY_THO
 
 def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=True, sample=True, c=1.0,
                    ts_std=0.1, ts_prior_mean=0.5, ts_prior_var=1 / 12.0, arms=None, seed=0, first_task=0,
-                   noise=None, policy_noise=None, ctx_actions=None, ctx_rewards=None):
-    """Fused classical-policy rollout (dpt_rollout_policy); optional prefix context (N, C)."""
+                   noise=None, policy_noise=None, ctx_actions=None, ctx_rewards=None, counter=0):
+    """Fused classical-policy rollout (dpt_rollout_policy); optional prefix context (N, C).
+    ``counter``: the Philox step counter of step 0 (step h draws at counter + h)."""
     dev = device()
     means_d = _dev(means, torch.float64, dev)
     N, A = means_d.shape
@@ -347,7 +348,7 @@ def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=Tr
         N, H, A, int(policy), int(bool(online)), int(bandit_type), int(bool(sample)), d, int(first_task), float(var),
         float(c), float(ts_std), float(ts_prior_mean), float(ts_prior_var), int(seed) & (2 ** 64 - 1),
         _p(means_d).value, opt(arms, torch.float64), opt(noise, torch.float64), opt(policy_noise, torch.float64),
-        _p(ws).value, _p(out["actions"]).value, _p(out["rewards"]).value, _p(out["arm_value"]).value, C, 0,
+        _p(ws).value, _p(out["actions"]).value, _p(out["rewards"]).value, _p(out["arm_value"]).value, C, int(counter),
         opt(ctx_actions, torch.int32), opt(ctx_rewards, torch.float64))
     _lib.call("dpt_rollout_policy", ctypes.byref(args), _stream())
     out["_keep"] = (keep, ws)

@@ -136,7 +136,7 @@ class PolicyRolloutArgs(ctypes.Structure):
                 ("ts_std", _f64), ("ts_prior_mean", _f64), ("ts_prior_var", _f64), ("seed", _u64),
                 ("means", _c_void_p), ("arms", _c_void_p), ("noise", _c_void_p), ("policy_noise", _c_void_p),
                 ("workspace", _c_void_p), ("actions_out", _c_void_p), ("rewards_out", _c_void_p),
-                ("arm_value_out", _c_void_p), ("C", _i32), ("reserved0", _i32), ("ctx_actions", _c_void_p),
+                ("arm_value_out", _c_void_p), ("C", _i32), ("step0", _i32), ("ctx_actions", _c_void_p),
                 ("ctx_rewards", _c_void_p)]
 
 

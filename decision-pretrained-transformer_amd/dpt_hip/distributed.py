@@ -45,6 +45,17 @@ def sharded_online(rollout_fn, means_all, group=None):
     return gather_rows(out["arm_value"], n_total, group), out
 
 
+def _all_reduce(t, group=None):
+    """Sum ``t`` over ranks in place (RCCL for device tensors under ``nccl``; under ``gloo``, the
+    CPU tests' and the one-GPU rehearsal's backend, a device tensor goes through the host)."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        host = t.cpu()
+        dist.all_reduce(host, group=group)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t, group=group)
+
+
 def _regret_max_steps():
     import dpt_hip
     return dpt_hip.regret_max_steps()
@@ -65,14 +76,22 @@ def regret_stats_allreduce(opt_local, lnr_local, n_total, group=None):
     fp64 curves on the GPU take the device passes (dpt_regret_moments); others the torch ops."""
     distributed = dist.is_available() and dist.is_initialized()  # else: one process holds every task
     n = float(n_total)
-    H = lnr_local.shape[1]
-    if lnr_local.is_cuda and lnr_local.dtype == torch.float64 and H <= _regret_max_steps():
+    count, H = lnr_local.shape[0], lnr_local.shape[1]
+    if count == 0:
+        # a rank with no tasks (shard() gives n_total < world ranks one task each): it adds
+        # zero moments but still joins both all_reduces, so the other ranks never block
+        s1 = torch.zeros((2, H), dtype=torch.float64, device=lnr_local.device)
+        if distributed:
+            _all_reduce(s1, group)
+        mean = s1 / n
+        m2 = torch.zeros_like(s1)
+    elif lnr_local.is_cuda and lnr_local.dtype == torch.float64 and H <= _regret_max_steps():
         # device passes (dpt_regret_moments, HIP): one read of the curves each
         import dpt_hip
-        opt = opt_local.reshape(lnr_local.shape[0], -1)[:, 0]
+        opt = opt_local.reshape(count, -1)[:, 0].contiguous()
         s1 = dpt_hip.regret_moments(lnr_local, opt)
         if distributed:
-            dist.all_reduce(s1, group=group)
+            _all_reduce(s1, group)
         mean = s1 / n
         m2 = dpt_hip.regret_moments(lnr_local, opt, dpt_hip._lib.REGRET_CENTRED, mean)
     else:
@@ -80,10 +99,10 @@ def regret_stats_allreduce(opt_local, lnr_local, n_total, group=None):
         cr = torch.cumsum(diff, dim=1)
         s1 = torch.stack([diff.sum(0), cr.sum(0)])
         if distributed:
-            dist.all_reduce(s1, group=group)
+            _all_reduce(s1, group)
         mean = s1 / n
         m2 = torch.stack([((diff - mean[0]) ** 2).sum(0), ((cr - mean[1]) ** 2).sum(0)])
     if distributed:
-        dist.all_reduce(m2, group=group)
+        _all_reduce(m2, group)
     sem = torch.sqrt(m2 / (n - 1.0) / n)
     return dict(subopt_mean=mean[0], subopt_sem=sem[0], regret_mean=mean[1], regret_sem=sem[1])

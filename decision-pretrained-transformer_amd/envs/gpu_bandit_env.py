@@ -44,6 +44,9 @@ class GPUBanditEnv(BaseEnv):
         self.current_step = torch.zeros(n_envs, device=self._device)
         self._seed = None
         self._counter = 0
+        # optional injected draws: callable(step counter) -> (n_envs,) standard normals (the
+        # torch.randn of gpu_bandit_env.py:58) or, bernoulli, uniforms; default: Philox
+        self.noise = None
 
     def get_arm_value(self, actions):
         return torch.sum(self.means * actions, dim=1)
@@ -58,8 +61,9 @@ class GPUBanditEnv(BaseEnv):
         if self._seed is None:
             self._seed = dpt_hip.next_seed()
         code = (dpt_hip.BANDIT_GAUSSIAN if self.type == "uniform" else dpt_hip.BANDIT_BERNOULLI)
-        r, _ = dpt_hip.bandit_step(self.means.double(), a, self.var, code | dpt_hip.BANDIT_F32, seed=self._seed,
-                                   counter=self._counter)
+        g = None if self.noise is None else torch.as_tensor(self.noise(self._counter), dtype=torch.float64)
+        r, _ = dpt_hip.bandit_step(self.means.double(), a, self.var, code | dpt_hip.BANDIT_F32, noise=g,
+                                   seed=self._seed, counter=self._counter)
         self._counter += 1
         return self.state.detach(), r.float()
 

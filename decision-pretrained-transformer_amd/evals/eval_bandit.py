@@ -77,15 +77,27 @@ def _policy_ok(vec_env, controller):
             and getattr(controller, "batch_size", vec_env.num_envs) == vec_env.num_envs)
 
 
-def rollout_policy_fused(vec_env, controller, horizon, noise=None, policy_noise=None, seed=None, first_task=0):
-    """One-launch rollout of a classical controller (dpt_rollout_policy)."""
+def rollout_policy_fused(vec_env, controller, horizon, noise=None, policy_noise=None, seed=None, first_task=None):
+    """One-launch rollout of a classical controller (dpt_rollout_policy).  The policy's draws
+    come from the controller's stream as in its per-step act_numpy_vec (the H counters that
+    loop would consume are consumed here in one go), or from ``controller.policy_noise``;
+    keyed by the global task id (``vec_env.first_task`` for a shard)."""
+    ctr0 = 0
     if isinstance(controller, OptPolicy):
         code, kw = dpt_hip.POLICY_OPT, {}
+        s0 = dpt_hip.next_seed()
     else:
         code, kw = controller.policy, controller.kernel_kwargs()
-    seed = dpt_hip.next_seed() if seed is None else seed
+        s0, ctr0 = controller._stream.next()
+        controller._stream.counter = ctr0 + horizon
+        if policy_noise is None and controller.policy_noise is not None:
+            policy_noise = np.stack([np.asarray(controller.policy_noise(ctr0 + h), np.float64)
+                                     for h in range(horizon)])
+    seed = s0 if seed is None else seed
+    if first_task is None:
+        first_task = getattr(vec_env, "first_task", 0)
     return dpt_hip.rollout_policy(code, vec_env.means_device, horizon, vec_env.var, vec_env.type_code, seed=seed,
-                                  first_task=first_task, noise=noise, policy_noise=policy_noise, **kw)
+                                  first_task=first_task, noise=noise, policy_noise=policy_noise, counter=ctr0, **kw)
 
 
 def deploy_online_vec(vec_env, controller, horizon, include_meta=False, uniforms=None, noise=None,

@@ -162,8 +162,10 @@ def online(eval_trajs, model, Heps, H, n_eval, dim, horizon, permuted=False):
     return all_means_lnr
 
 
-def offline(eval_trajs, model, n_eval, H, dim, permuted=False):
-    """evals/eval_darkroom.py:124-189: expert vs DPT (sampled and greedy) on fixed contexts."""
+def offline(eval_trajs, model, n_eval, H, dim, permuted=False, uniforms=None):
+    """evals/eval_darkroom.py:124-189: expert vs DPT (sampled and greedy) on fixed contexts.
+    ``uniforms`` (H, n_eval), optional: the sampled leg's selection draws (one row per step), as
+    the reference's np.random.choice consumes them; returns the three per-task return arrays."""
     import matplotlib.pyplot as plt
     envs = []
     for i in range(n_eval):
@@ -180,6 +182,8 @@ def offline(eval_trajs, model, n_eval, H, dim, permuted=False):
     res = {"Opt": np.sum(rs_opt, axis=-1)}
     for name, sample in (("Learner", True), ("Learner (greedy)", False)):
         ctrl = DarkroomTransformerController(model, batch_size=n_eval, sample=sample)
+        if sample and uniforms is not None:
+            ctrl.uniforms = lambda k: uniforms[k]
         ctrl.set_batch(dict(batch))
         dm = model.device_model()
         c = (batch["context_states"], batch["context_actions"], batch["context_next_states"],

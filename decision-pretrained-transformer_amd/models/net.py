@@ -134,7 +134,17 @@ class Transformer(nn.Module):
 
     def forward(self, x):
         """models/net.py:41-60: pack [query | context] -> embed -> GPT-2 -> head;
-        last position (test) or positions 1.. (train).  Inference only."""
+        last position (test) or positions 1.. (train).  Inference only: the kernels build
+        no autograd graph, so a forward that autograd would differentiate (training mode,
+        grad enabled, trainable parameters: train.py:286-331) raises instead of returning
+        logits whose ``loss.backward()`` fails later with a generic autograd error.  The
+        reference's inference call sites work unchanged: eval.py:152 calls ``model.eval()``
+        and train.py:265-278 computes its test loss under ``torch.no_grad()``."""
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "Transformer.forward with autograd: the backward pass (train.py:286-331, CE over "
+                "preds[:, 1:]) is not built in this MI355X hot-path package; run inference under "
+                "model.eval() or torch.no_grad()")
         dm = self.device_model()
         query = x["query_states"]
         cs = x.get("context_states")

@@ -290,7 +290,10 @@ typedef struct dpt_policy_rollout_args {
     double* arm_value_out;      /* (N, H) */
     /* optional prefix context (set_batch_numpy_vec): C transitions per task,
      * replayed into the statistics before step 0 (offline eval: C = h, H = 1) */
-    int32_t C, reserved0;
+    int32_t C;
+    int32_t step0;              /* Philox step counter of step 0: step h draws at step0 + h, so a
+                                 * per-step call (H = 1, step0 = h) draws what the fused launch
+                                 * (step0 = 0) draws at step h */
     const int32_t* ctx_actions; /* (N, C) arm indices */
     const double* ctx_rewards;  /* (N, C) */
 } dpt_policy_rollout_args;

@@ -38,3 +38,33 @@ def bandit_rollout(blob, L, A, npos, means, H, var, u, g, sample=True, recompute
     if rc:
         raise ValueError("oracle rollout rejected the shape")
     return dict(actions=acts, rewards=rew, arm_value=av, cum_means=av.T, logits=lg)
+
+
+def darkroom_rollout(blob, L, npos, goals, Heps, horizon, R, u=None, sample=True, perms=None, dim=10, memo=True,
+                     threads=1, want_logits=False):
+    """Same contract as dpt_oracle.darkroom_online_rollout (float64 forward, packed dpt_hip.h
+    blob); u (Heps*horizon, N) or None for greedy.  Also returns ``margin`` (steps, N): the
+    distance of each step's uniform to the nearest interior cdf edge."""
+    lib = load()
+    if not hasattr(lib, "_dr"):
+        P = ctypes.c_void_p
+        i = ctypes.c_int
+        lib.dpt_oracle_darkroom_rollout.restype = i
+        lib.dpt_oracle_darkroom_rollout.argtypes = [P, i, i, P, P, i, i, i, i, i, P, i, i, i, P, P, P, P]
+        lib._dr = True
+    blob = np.ascontiguousarray(blob, np.float32)
+    goals = np.ascontiguousarray(goals, np.int32)
+    N = goals.shape[0]
+    steps = Heps * horizon
+    u = None if u is None else np.ascontiguousarray(np.asarray(u).reshape(steps, N), np.float64)
+    perms = None if perms is None else np.ascontiguousarray(perms, np.int32)
+    rets = np.zeros((N, Heps), np.int32)
+    acts = np.zeros((N, steps), np.int32)
+    margin = np.zeros((steps, N))
+    lg = np.zeros((steps, N, 5), np.float32) if want_logits else None
+    p = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rc = lib.dpt_oracle_darkroom_rollout(p(blob), L, npos, p(goals), p(perms), N, Heps, horizon, R, dim, p(u),
+                                         int(sample), int(memo), int(threads), p(rets), p(acts), p(lg), p(margin))
+    if rc:
+        raise ValueError("oracle darkroom rollout rejected the shape")
+    return dict(returns=rets, actions=acts, logits=lg, margin=margin)

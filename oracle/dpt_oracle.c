@@ -169,3 +169,202 @@ int dpt_oracle_bandit_rollout(const float* blob, int L, int A, int npos, const d
     }
     return rc;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * DarkRoom online evaluation (evals/eval_darkroom.py:20-84 deploy_online_vec with
+ * DarkroomTransformerController, ctrls/ctrl_darkroom.py:23-66, and DarkroomEnvVec.deploy_eval,
+ * envs/darkroom_env.py:151-175), in float64 like oracle/dpt_oracle.py's darkroom_online_rollout.
+ * Episode e runs `horizon` steps from (0, 0); its window is [query = current state | the last
+ * min(e, R) episodes' transitions in order] and every step's logits are the last position of a
+ * full causal forward over that window (models/net.py:41-60).  memo=1 reuses a task's logits
+ * for a state already queried in the same episode (the window is fixed within an episode, so
+ * they are the same numbers); memo=0 re-forwards every step, the reference's algorithm.
+ * ------------------------------------------------------------------------------------------ */
+
+static void layer_norm_d(const double* x, const float* g, const float* b, double* y) {
+    double mean = 0.0, var = 0.0;
+    for (int j = 0; j < E; ++j) mean += x[j];
+    mean /= E;
+    for (int j = 0; j < E; ++j) var += (x[j] - mean) * (x[j] - mean);
+    var /= E;
+    const double rstd = 1.0 / sqrt(var + 1e-5);
+    for (int j = 0; j < E; ++j) y[j] = (x[j] - mean) * rstd * g[j] + b[j];
+}
+
+static void linear_d(const double* x, int in, const float* W, const float* b, int out, double* y) {
+    for (int o = 0; o < out; ++o) y[o] = b[o];
+    for (int k = 0; k < in; ++k) {
+        const double xk = x[k];
+        const float* w = W + (size_t)k * out;
+        for (int o = 0; o < out; ++o) y[o] += xk * (double)w[o];
+    }
+}
+
+/* causal forward over T packed tokens (T x F), logits of position T-1 (5 actions, double) */
+static void window_forward_d(const view_t* v, const double* toks, int T, double* X, double* K, double* V,
+                             double* sc, double* logits) {
+    const int F = v->F;
+    for (int p = 0; p < T; ++p) {
+        double* x = X + (size_t)p * E;
+        for (int o = 0; o < E; ++o) x[o] = v->emb_b[o];
+        for (int k = 0; k < F; ++k) {
+            const double t = toks[(size_t)p * F + k];
+            if (t != 0.0)
+                for (int o = 0; o < E; ++o) x[o] += t * (double)v->emb_w[(size_t)k * E + o];
+        }
+        for (int o = 0; o < E; ++o) x[o] += v->wpe[(size_t)p * E + o];
+    }
+    double xn[E], qkv[3 * E], o[E], t[E], h[FF];
+    for (int l = 0; l < v->L; ++l) {
+        const float* W = v->layers + (size_t)l * LSIZE;
+        const int last = (l == v->L - 1);
+        double* Q = sc + (size_t)T;  /* queries [T][E] after the score row */
+        for (int p = 0; p < T; ++p) {
+            layer_norm_d(X + (size_t)p * E, W + 0, W + 32, xn);
+            linear_d(xn, E, W + 64, W + 3136, 3 * E, qkv);
+            memcpy(Q + (size_t)p * E, qkv, E * sizeof(double));
+            memcpy(K + (size_t)p * E, qkv + E, E * sizeof(double));
+            memcpy(V + (size_t)p * E, qkv + 2 * E, E * sizeof(double));
+        }
+        /* the last block: only position T-1 reaches the head */
+        for (int p = last ? T - 1 : 0; p < T; ++p) {
+            double* x = X + (size_t)p * E;
+            const double* q = Q + (size_t)p * E;
+            double m = -INFINITY, s = 0.0;
+            for (int j = 0; j <= p; ++j) {
+                double d = 0.0;
+                for (int k = 0; k < E; ++k) d += q[k] * K[(size_t)j * E + k];
+                sc[j] = d / sqrt((double)E);
+                if (sc[j] > m) m = sc[j];
+            }
+            for (int j = 0; j <= p; ++j) {
+                sc[j] = exp(sc[j] - m);
+                s += sc[j];
+            }
+            for (int k = 0; k < E; ++k) o[k] = 0.0;
+            for (int j = 0; j <= p; ++j) {
+                const double pj = sc[j] / s;
+                for (int k = 0; k < E; ++k) o[k] += pj * V[(size_t)j * E + k];
+            }
+            linear_d(o, E, W + 3232, W + 4256, E, t);
+            for (int j = 0; j < E; ++j) x[j] += t[j];
+            layer_norm_d(x, W + 4288, W + 4320, xn);
+            linear_d(xn, E, W + 4352, W + 8448, FF, h);
+            for (int j = 0; j < FF; ++j) h[j] = 0.5 * h[j] * (1.0 + tanh(0.7978845608028654 * (h[j] + 0.044715 * h[j] * h[j] * h[j])));
+            linear_d(h, FF, W + 8576, W + 12672, E, t);
+            for (int j = 0; j < E; ++j) x[j] += t[j];
+        }
+    }
+    layer_norm_d(X + (size_t)(T - 1) * E, v->lnf_g, v->lnf_b, xn);
+    linear_d(xn, E, v->head_w, v->head_b, v->A, logits);
+}
+
+/* scipy.special.softmax on float32 logits (temp 1.0: x / 1.0 leaves them unchanged), then
+ * numpy choice: cdf = cumsum(float64(p)) / last, idx = #(cdf <= u).  *margin = distance of u
+ * to the nearest interior cdf edge (the caller flags near-ties). */
+static int select_dr(const float* lg, int sample, double u, double* margin) {
+    int best = 0;
+    *margin = INFINITY;
+    if (!sample) {
+        for (int k = 1; k < 5; ++k)
+            if (lg[k] > lg[best]) best = k;
+        return best;
+    }
+    float m = lg[0], e[5], s = 0.f;
+    for (int k = 1; k < 5; ++k) m = lg[k] > m ? lg[k] : m;
+    for (int k = 0; k < 5; ++k) { e[k] = expf(lg[k] - m); s += e[k]; }
+    double c = 0.0, cdf[5];
+    for (int k = 0; k < 5; ++k) { c += (double)(e[k] / s); cdf[k] = c; }
+    int idx = 0;
+    for (int k = 0; k < 5; ++k) {
+        cdf[k] /= c;
+        idx += (cdf[k] <= u);
+        if (k < 4 && fabs(cdf[k] - u) < *margin) *margin = fabs(cdf[k] - u);
+    }
+    return idx < 5 ? idx : 4;
+}
+
+/* envs/darkroom_env.py:37-55 (+ :100-103): perm, move, clip, reward iff next == goal */
+static void dr_transit(int* x, int* y, int a, const int32_t* perm, const int32_t* goal, int dim, int* r) {
+    if (perm) a = perm[a];
+    *x += (a == 0) - (a == 1);
+    *y += (a == 2) - (a == 3);
+    *x = *x < 0 ? 0 : (*x > dim - 1 ? dim - 1 : *x);
+    *y = *y < 0 ? 0 : (*y > dim - 1 ? dim - 1 : *y);
+    *r = (*x == goal[0] && *y == goal[1]);
+}
+
+/* goals (N,2); perms (N,5) or NULL; u (Heps*horizon, N) or NULL (greedy).  Outputs: returns
+ * (N,Heps); actions (N,Heps*horizon), logits (Heps*horizon,N,5), margin (Heps*horizon,N) or NULL. */
+int dpt_oracle_darkroom_rollout(const float* blob, int L, int npos, const int32_t* goals, const int32_t* perms,
+                                int N, int Heps, int horizon, int R, int dim, const double* u, int sample, int memo,
+                                int nthreads, int32_t* returns, int32_t* actions, float* logits_out,
+                                double* margin_out) {
+    const int Tmax = 1 + R * horizon, F = 10, steps = Heps * horizon;
+    if (Tmax > npos || dim * dim > 4096) return -1;
+    view_t v = make_view(blob, L, 2, 5, npos);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int i = 0; i < N; ++i) {
+        double* toks = (double*)calloc((size_t)Tmax * F, sizeof(double));
+        double* hist = (double*)calloc((size_t)(R + 1) * horizon * F, sizeof(double)); /* ring of episodes */
+        double* X = (double*)malloc(sizeof(double) * (size_t)Tmax * E);
+        double* K = (double*)malloc(sizeof(double) * (size_t)Tmax * E);
+        double* V = (double*)malloc(sizeof(double) * (size_t)Tmax * E);
+        double* sc = (double*)malloc(sizeof(double) * (size_t)Tmax * (E + 1));
+        float* memo_lg = (float*)malloc(sizeof(float) * (size_t)dim * dim * 5);
+        char* seen = (char*)malloc((size_t)dim * dim);
+        const int32_t* perm = perms ? perms + (size_t)i * 5 : NULL;
+        const int32_t* goal = goals + (size_t)i * 2;
+        int nep = 0; /* episodes stored in hist (<= R, oldest first) */
+        for (int e = 0; e < Heps; ++e) {
+            const int C = nep * horizon, T = 1 + C;
+            memcpy(toks + F, hist, sizeof(double) * (size_t)C * F);
+            memset(seen, 0, (size_t)dim * dim);
+            double* cur = hist + (size_t)nep * horizon * F; /* this episode's slot */
+            int x = 0, y = 0, ret = 0;
+            for (int t = 0; t < horizon; ++t) {
+                const int k = e * horizon + t, cell = x * dim + y;
+                float lg[5];
+                if (memo && seen[cell]) {
+                    memcpy(lg, memo_lg + (size_t)cell * 5, sizeof lg);
+                } else {
+                    double lgd[5];
+                    memset(toks, 0, sizeof(double) * F);
+                    toks[0] = x;
+                    toks[1] = y;
+                    window_forward_d(&v, toks, T, X, K, V, sc, lgd);
+                    for (int a = 0; a < 5; ++a) lg[a] = (float)lgd[a];
+                    memcpy(memo_lg + (size_t)cell * 5, lg, sizeof lg);
+                    seen[cell] = 1;
+                }
+                double mg;
+                const int a = select_dr(lg, sample, sample ? u[(size_t)k * N + i] : 0.0, &mg);
+                if (logits_out)
+                    for (int j = 0; j < 5; ++j) logits_out[((size_t)k * N + i) * 5 + j] = lg[j];
+                if (margin_out) margin_out[(size_t)k * N + i] = mg;
+                if (actions) actions[(size_t)i * steps + k] = a;
+                double* tk = cur + (size_t)t * F;
+                memset(tk, 0, sizeof(double) * F);
+                tk[0] = x;
+                tk[1] = y;
+                tk[2 + a] = 1.0;
+                int r;
+                dr_transit(&x, &y, a, perm, goal, dim, &r);
+                tk[7] = x;
+                tk[8] = y;
+                tk[9] = r;
+                ret += r;
+            }
+            returns[(size_t)i * Heps + e] = ret;
+            if (nep < R) {
+                ++nep;
+            } else { /* shift-append (evals/eval_darkroom.py:75-82): drop the oldest episode */
+                memmove(hist, hist + (size_t)horizon * F, sizeof(double) * (size_t)R * horizon * F);
+            }
+        }
+        free(toks); free(hist); free(X); free(K); free(V); free(sc); free(memo_lg); free(seen);
+    }
+    return 0;
+}

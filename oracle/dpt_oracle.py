@@ -39,6 +39,14 @@ def bandit_reward(means, action, g, var):
     return means[np.arange(means.shape[0]), a] + noise
 
 
+def gpu_bandit_reward_f32(means32, action, g32, var):
+    """GPUBanditEnv.transit (envs/gpu_bandit_env.py:53-63): fp32 torch ops
+    ``means[ar, argmax(us)] + torch.randn(N) * var``: the python-float ``var`` is cast to fp32,
+    then one fp32 multiply and one fp32 add (two roundings)."""
+    m = np.asarray(means32, np.float32)[np.arange(len(action)), np.asarray(action)]
+    return m + np.asarray(g32, np.float32) * np.float32(var)
+
+
 def bernoulli_reward(means, action, u):
     """Bernoulli bandit: ``torch.bernoulli(mean)`` == ``u < mean`` (envs/gpu_bandit_env.py:58-61)."""
     means = np.asarray(means, np.float64)
@@ -314,6 +322,36 @@ def darkroom_online_rollout(W, goals, Heps, H, horizon, u, sample=True, perm=Non
                 buf[:, :-1] = buf[:, 1:].copy()
                 buf[:, -1] = v
     return dict(returns=rets, logits=np.stack(logs), actions=np.stack(acts, 1))
+
+
+def darkroom_offline_episode(W, goals, ctx, horizon, u, sample=True, perm=None, dim=10, dtype=np.float64):
+    """One ``DarkroomEnvVec.deploy_eval`` episode of the DPT controller on a FIXED context
+    (evals/eval_darkroom.py:124-189 ``offline``: ``lnr.set_batch(batch)`` then
+    ``vec_env.deploy_eval``; envs/darkroom_env.py:151-175): from (0, 0), every step forwards
+    [query = current state | context], selects (sampled with temp 1.0, or argmax) and steps the
+    grid.  ctx = (cs, ca, cn, cr) with cr (N, C, 1).  Returns rewards (N, horizon) int."""
+    goals = np.asarray(goals)
+    N = goals.shape[0]
+    s = np.zeros((N, 2), np.int64)
+    rews = np.zeros((N, horizon), np.int64)
+    for t in range(horizon):
+        lg = transformer_forward(W, s.astype(np.float64), *ctx, dtype=dtype).astype(np.float32)
+        a = select_actions(lg, u[t] if sample else None, sample, temp=1.0 if sample else None)
+        s, r = darkroom_transit(s, a, goals, dim, perm)
+        rews[:, t] = r
+    return rews
+
+
+def darkroom_opt_returns(goals, horizon, perm=None, dim=10):
+    """The expert leg of the offline eval (evals/eval_darkroom.py:146-150: DarkroomOptPolicy
+    deployed per env, ctrls/ctrl_darkroom.py:10-20): sum of rewards over one episode."""
+    goals = np.asarray(goals)
+    s = np.zeros((goals.shape[0], 2), np.int64)
+    tot = np.zeros(goals.shape[0], np.int64)
+    for _ in range(horizon):
+        s, r = darkroom_transit(s, darkroom_opt_action(s, goals, perm), goals, dim, perm)
+        tot += r
+    return tot
 
 
 def regret_curves(opt, lnr):

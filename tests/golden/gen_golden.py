@@ -57,6 +57,7 @@ def _install_stubs():
     ipy = types.ModuleType("IPython")
     ipy.embed = lambda *a, **k: None
     ipy.get_ipython = lambda: None
+    ipy.version_info = (9, 0, 0)  # matplotlib's backend check returns early for >= 8.24
     sys.modules["IPython"] = ipy
     sk = types.ModuleType("skimage")
     skt = types.ModuleType("skimage.transform")
@@ -248,6 +249,226 @@ def host_surface():
     json.dump({"filenames": cases, "defaults": defaults}, open(os.path.join(OUT, "host_surface.json"), "w"),
               indent=1, sort_keys=True)
     print("F9 host_surface")
+
+
+def fixture_transformer(name, horizon=None):
+    """The reference Transformer (models/net.py:9-60) holding the weights recorded in
+    forward_<name>.npz; a shorter ``horizon`` keeps the first 4(1+horizon) wpe rows (the
+    model the reference builds for that horizon, with the same parameters)."""
+    import numpy as np
+    import torch
+    from net import Transformer
+    g = dict(np.load(os.path.join(OUT, f"forward_{name}.npz")))
+    H, sd_, ad, L, E = (int(x) for x in g["cfg"])
+    horizon = horizon or H
+    m = Transformer(dict(horizon=horizon, state_dim=sd_, action_dim=ad, n_layer=L, n_embd=E, n_head=4,
+                         dropout=0.0, test=True))
+    state = m.state_dict()
+    for k, v in g.items():
+        if k.startswith("w/"):
+            key = k[2:]
+            if key.endswith("wpe.weight"):
+                v = v[: 4 * (1 + horizon)]
+            state[key] = torch.from_numpy(v)
+    m.load_state_dict(state)
+    m.eval()
+    return m
+
+
+def c1():
+    """BASELINE config 1 at its size: 5-arm Gaussian bandit, H=100, 64 tasks, var 0.3 (run_bandit.sh
+    flags).  (a) collect: generate_bandit_histories (collect_data.py:158-182, :221-225) with every
+    draw recorded per env (cov pick, Dirichlet, random arm, the H arm choices and reward normals);
+    (b) eval: the online deploy_online_vec loop (evals/eval_bandit.py:56-103) of the DPT sampling
+    controller (model: forward_bandit5 weights at horizon 100) with its uniforms / normals, plus the
+    Opt leg and the regret curves of evals/eval_bandit.py:169-178."""
+    import numpy as np
+    import scipy.stats
+    import torch
+    import collect_data
+    from envs import bandit_env
+    from ctrls.ctrl_bandit import BanditTransformerController, OptPolicy
+    from evals import eval_bandit
+    N, H, A, var = 64, 100, 5, 0.3
+    out = {}
+    np.random.seed(2024)
+    rec_dir = []
+    real_dir = np.random.dirichlet
+
+    def dirichlet(alpha, _r=real_dir):
+        v = _r(alpha)
+        rec_dir.append(v)
+        return v
+
+    np.random.dirichlet = dirichlet
+    try:
+        with DrawRecorder(np) as rec:
+            trajs = collect_data.generate_bandit_histories(N, dim=A, horizon=H, var=var, n_hists=1, n_samples=1,
+                                                           cov=0.0, type="uniform")
+    finally:
+        np.random.dirichlet = real_dir
+    # per env: uniform(0,1,A) means (bandit_env.sample: no recorded draw), then cov pick + random
+    # arm (plain choices), H choice uniforms and H reward normals
+    assert len(rec.plain) == 2 * N and len(rec.u) == N * H and len(rec.g) == N * H
+    out["collect/means"] = np.stack([t["means"] for t in trajs])
+    out["collect/cov"] = np.array(rec.plain[0::2], np.float64)
+    out["collect/rand_index"] = np.array(rec.plain[1::2], np.int64)
+    out["collect/dirichlet"] = np.stack(rec_dir)
+    out["collect/u"] = np.array(rec.u).reshape(N, H)
+    out["collect/g"] = np.array(rec.g).reshape(N, H)
+    for t in trajs:  # the bandit state is the constant [1] (collect_data.py:41)
+        assert (t["context_states"] == 1).all() and (t["context_next_states"] == 1).all()
+        assert t["context_states"].shape == (H, 1) and t["context_states"].dtype == np.int64
+    out["collect/actions"] = np.stack([t["context_actions"].argmax(-1) for t in trajs]).astype(np.int8)
+    assert np.array_equal(np.eye(A)[out["collect/actions"]], np.stack([t["context_actions"] for t in trajs]))
+    out["collect/rewards"] = np.stack([t["context_rewards"] for t in trajs])
+    out["collect/optimal_action"] = np.stack([t["optimal_action"] for t in trajs])
+    # online eval of the DPT policy on 64 fresh tasks
+    means = np.random.RandomState(12).uniform(0, 1, (N, A))
+    envs = [bandit_env.BanditEnv(m, H, var=var) for m in means]
+    vec = bandit_env.BanditEnvVec(envs)
+    model = fixture_transformer("bandit5", horizon=H)
+    opt = eval_bandit.deploy_online_vec(vec, OptPolicy(envs, batch_size=N), H).T  # evals/eval_bandit.py:123-128
+    ctrl = BanditTransformerController(model, sample=True, batch_size=N)
+    np.random.seed(2025)
+    with DrawRecorder(np) as rec, torch.no_grad():
+        cm, meta = eval_bandit.deploy_online_vec(vec, ctrl, H, include_meta=True)
+    assert (opt == means.max(1, keepdims=True)).all()  # the Opt leg: means[opt_a] every step
+    out.update({"eval/means": means, "eval/cum_means": cm,
+                "eval/actions": meta["context_actions"].argmax(-1), "eval/rewards": meta["context_rewards"][..., 0],
+                "eval/u": np.array(rec.u).reshape(H, N), "eval/g": np.array(rec.g).reshape(H, N),
+                "cfg": np.array([N, H, A]), "var": np.float64(var)})
+    diff = opt - cm.T  # all_means_diff (evals/eval_bandit.py:169)
+    cr = np.cumsum(diff, axis=1)
+    out.update({"eval/subopt_mean": np.mean(diff, axis=0), "eval/subopt_sem": scipy.stats.sem(diff, axis=0),
+                "eval/regret_mean": np.mean(cr, axis=0), "eval/regret_sem": scipy.stats.sem(cr, axis=0)})
+    np.savez_compressed(os.path.join(OUT, "c1_bandit.npz"), **out)
+    print("C1 collect + eval")
+
+
+def gpu_bandit_env():
+    """envs/gpu_bandit_env.py:53-74 on the CPU device with every torch.randn recorded: fp32 rewards
+    mean_rewards + randn * var for 3 steps of 64 tasks at var 0.3 and 1.0, the done flags, the
+    ValueError past H, and deploy_eval's var = 0 rewards."""
+    import numpy as np
+    import torch
+    from envs.gpu_bandit_env import GPUBanditEnv
+    out = {}
+    real_randn = torch.randn
+    for var in (0.3, 1.0):
+        torch.manual_seed(int(var * 10))
+        env = GPUBanditEnv(5, 64, 3, var=var, device=torch.device("cpu"))
+        draws = []
+
+        def randn(*a, _r=real_randn, **k):
+            v = _r(*a, **k)
+            draws.append(v.clone())
+            return v
+
+        torch.randn = randn
+        try:
+            env.reset()
+            acts, rews, dones = [], [], []
+            rs = np.random.RandomState(int(var * 10))
+            for _ in range(3):
+                us = torch.nn.functional.one_hot(torch.from_numpy(rs.randint(0, 5, 64)), 5).float()
+                _, r, done, _ = env.step(us)
+                acts.append(us.argmax(1).numpy())
+                rews.append(r.numpy())
+                dones.append(done.numpy())
+            try:
+                env.step(us)
+                raise AssertionError("no ValueError past H")
+            except ValueError as e:
+                out[f"var{var}/error"] = np.array(str(e))
+        finally:
+            torch.randn = real_randn
+        out.update({f"var{var}/means": env.means.numpy(), f"var{var}/actions": np.stack(acts),
+                    f"var{var}/g": torch.stack(draws).numpy(), f"var{var}/rewards": np.stack(rews),
+                    f"var{var}/done": np.stack(dones)})
+    np.savez_compressed(os.path.join(OUT, "gpu_bandit_env.npz"), **out)
+    print("GPUBanditEnv")
+
+
+def linear_thompson():
+    """collect_data.rollin_linear_bandit_vec (collect_data.py:56-80): the Thompson behaviour policy
+    (prior mean 0, variance 1) on 10-arm linear bandits (lin_d = 2, arms RandomState(1234) as in
+    collect_data.py:230-231) through deploy_online_vec, with the posterior normals and reward
+    normals recorded."""
+    import numpy as np
+    import collect_data
+    from envs import bandit_env
+    N, H, A, d, var = 24, 30, 10, 2, 0.3
+    arms = np.random.RandomState(1234).normal(size=(A, d)) / np.sqrt(d)
+    thetas = np.random.RandomState(5).normal(0, 1, (N, d)) / np.sqrt(d)
+    envs = [bandit_env.LinearBanditEnv(t, arms, H, var=var) for t in thetas]
+    np.random.seed(77)
+    with DrawRecorder(np) as rec:
+        cs, ca, cn, cr = collect_data.rollin_linear_bandit_vec(envs)
+    np.savez_compressed(os.path.join(OUT, "linear_thompson.npz"), arms=arms, theta=thetas,
+                        means=np.stack([e.means for e in envs]), var=np.float64(var),
+                        policy_g=np.stack(rec.garr), g=np.array(rec.g).reshape(H, N),
+                        context_states=cs, context_actions=ca, context_next_states=cn, context_rewards=cr)
+    print("linear Thompson rollin")
+
+
+def darkroom_offline():
+    """evals/eval_darkroom.py:124-189 (offline): the expert's return, the DPT sampled leg (its
+    selection uniforms recorded) and the deterministic greedy leg on fixed contexts, plain and
+    permuted; returns captured at DarkroomEnvVec.deploy_eval / DarkroomEnv.deploy_eval."""
+    import numpy as np
+    import torch
+    import collect_data
+    from envs import darkroom_env
+    from evals import eval_darkroom
+    model = fixture_transformer("darkroom")
+    out = {}
+    for tag, n, H, permuted in (("plain", 8, 30, False), ("permuted", 4, 20, True)):
+        rs = np.random.RandomState(90 + n)
+        np.random.seed(91 + n)
+        trajs = []
+        for i in range(n):
+            if permuted:
+                env = darkroom_env.DarkroomEnvPermuted(10, int(rs.randint(0, 120)), H)
+            else:
+                env = darkroom_env.DarkroomEnv(10, rs.randint(0, 10, 2), H)
+            s, a, ns, r = collect_data.rollin_mdp(env, "uniform")  # collect_data.py:83-111
+            t = {"context_states": s, "context_actions": a, "context_next_states": ns, "context_rewards": r,
+                 "goal": env.goal}
+            if permuted:
+                t["perm_index"] = env.perm_index
+            trajs.append(t)
+        got = {"vec": [], "env": []}
+        real_vec, real_env = darkroom_env.DarkroomEnvVec.deploy_eval, darkroom_env.DarkroomEnv.deploy_eval
+
+        def vec_eval(self, ctrl, _r=real_vec):
+            res = _r(self, ctrl)
+            got["vec"].append(res[3])
+            return res
+
+        def env_eval(self, ctrl, _r=real_env):
+            res = _r(self, ctrl)
+            got["env"].append(res[3])
+            return res
+
+        darkroom_env.DarkroomEnvVec.deploy_eval = vec_eval
+        darkroom_env.DarkroomEnv.deploy_eval = env_eval
+        np.random.seed(93 + n)
+        try:
+            with DrawRecorder(np) as rec, torch.no_grad():
+                eval_darkroom.offline(trajs, model, n_eval=n, H=H, dim=10, permuted=permuted)
+        finally:
+            darkroom_env.DarkroomEnvVec.deploy_eval, darkroom_env.DarkroomEnv.deploy_eval = real_vec, real_env
+        assert len(got["vec"]) == 2 and len(got["env"]) == n and len(rec.u) == n * H
+        for k in ("context_states", "context_actions", "context_next_states", "context_rewards", "goal"):
+            out[f"{tag}/{k}"] = np.stack([t[k] for t in trajs])
+        if permuted:
+            out[f"{tag}/perm_index"] = np.array([t["perm_index"] for t in trajs])
+        out.update({f"{tag}/opt_returns": np.array([np.sum(x) for x in got["env"]]),
+                    f"{tag}/lnr_rewards": np.asarray(got["vec"][0]), f"{tag}/greedy_rewards": np.asarray(got["vec"][1]),
+                    f"{tag}/u": np.array(rec.u).reshape(H, n), f"{tag}/cfg": np.array([n, H, int(permuted)])})
+    np.savez_compressed(os.path.join(OUT, "darkroom_offline.npz"), **out)
+    print("darkroom offline")
 
 
 def main():

@@ -113,6 +113,29 @@ def _stats_worker(rank, port, opt, lnr, q):
 
 
 @pytest.mark.timeout(300)
+def test_gloo_world2_rank_without_tasks():
+    """n_total=1 over 2 ranks: rank 1 owns no task (shard() gives it count 0) and still joins
+    both all_reduces, so the job finishes and rank 0 gets the one task's curves."""
+    rs = np.random.RandomState(2)
+    H = 12
+    opt = np.repeat(rs.uniform(0.5, 1.0, (1, 1)), H, axis=1)
+    lnr = opt - rs.uniform(0, 0.5, (1, H))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, port, opt, lnr, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    stats = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    diff = (opt - lnr)[0]
+    assert np.array_equal(stats["subopt_mean"], diff)
+    assert np.allclose(stats["regret_mean"], np.cumsum(diff), rtol=1e-15, atol=0)
+
+
+@pytest.mark.timeout(300)
 def test_gloo_world2_regret_sem_matches_scipy():
     """regret_stats_allreduce at H=1000 (the linear-bandit horizon) on curves whose cumulative
     regret has a large mean relative to its spread: mean and SEM equal scipy.stats.sem over the

@@ -12,17 +12,21 @@ from oracle import dpt_oracle as O
 pytestmark = pytest.mark.gpu
 
 
-def ref_model(name):
-    """models.net.Transformer loaded (strict) from a reference state_dict fixture."""
+def ref_model(name, horizon=None):
+    """models.net.Transformer loaded (strict) from a reference state_dict fixture; a shorter
+    ``horizon`` keeps the first 4(1+horizon) wpe rows (gen_golden.fixture_transformer)."""
     from models.net import Transformer
     g = golden(f"forward_{name}.npz")
     H, sd, A, L, E = (int(x) for x in g["cfg"])
-    m = Transformer(dict(horizon=H, state_dim=sd, action_dim=A, n_layer=L, n_embd=E, n_head=4, dropout=0.0,
+    horizon = horizon or H
+    m = Transformer(dict(horizon=horizon, state_dim=sd, action_dim=A, n_layer=L, n_embd=E, n_head=4, dropout=0.0,
                          test=True))
-    state = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w/")}
+    state = {k[2:]: torch.from_numpy(v[: 4 * (1 + horizon)] if k.endswith("wpe.weight") else v)
+             for k, v in g.items() if k.startswith("w/")}
     state["transformer.wte.weight"] = m.transformer.wte.weight.detach().clone()
     state["transformer.h.0.attn.bias"] = torch.ones(1)  # transformers 4.5.1 legacy buffer: dropped on load
     m.load_state_dict(state)
+    m.eval()  # as eval.py:152 does
     return g, m
 
 
@@ -85,12 +89,33 @@ def test_generic_loop_equals_fused():
     cm_g = eval_bandit.deploy_online_vec(vec, BanditTransformerController(m, sample=False, batch_size=n), H,
                                          fused=False)
     assert np.array_equal(cm_f, cm_g)
-    # classical policies: per-step prefix-context kernel calls == fused kernel (var=0: no env noise)
-    from ctrls.ctrl_bandit import EmpMeanPolicy, UCBPolicy
-    for mk in (lambda: EmpMeanPolicy(envs[0], online=True, batch_size=n), lambda: UCBPolicy(envs[0], batch_size=n)):
-        a = eval_bandit.deploy_online_vec(vec, mk(), H)
-        b = eval_bandit.deploy_online_vec(vec, mk(), H, fused=False)
-        assert np.array_equal(a, b)
+    # classical policies: per-step prefix-context kernel calls == fused kernel (var=0: no env noise);
+    # Thompson's posterior draws come from the controller's stream in both loops (Philox counter
+    # k of one seed at step k), or from the injected policy_noise
+    from ctrls.ctrl_bandit import EmpMeanPolicy, PessMeanPolicy, ThompsonSamplingPolicy, UCBPolicy
+
+    def thompson(sample, counter=0, pn=None):
+        c = ThompsonSamplingPolicy(envs[0], std=0.3, sample=sample, prior_mean=0.5, prior_var=1 / 12.0,
+                                   batch_size=n)
+        c._stream.seed, c._stream.counter = 777, counter
+        c.policy_noise = pn
+        return c
+
+    pg = np.random.RandomState(4).standard_normal((40, n, 5))
+    for mk in (lambda: EmpMeanPolicy(envs[0], online=True, batch_size=n), lambda: UCBPolicy(envs[0], batch_size=n),
+               lambda: PessMeanPolicy(envs[0], const=0.8, batch_size=n), lambda: thompson(True),
+               lambda: thompson(True, 9), lambda: thompson(False, 3), lambda: thompson(True, 2, lambda k: pg[k])):
+        ca, cb = mk(), mk()
+        a = eval_bandit.deploy_online_vec(vec, ca, H)
+        b = eval_bandit.deploy_online_vec(vec, cb, H, fused=False)
+        assert np.array_equal(a, b), type(ca).__name__
+        assert ca._stream.counter == cb._stream.counter
+    # injected posterior normals are the ones used: equal to the kernel fed them directly
+    import dpt_hip
+    out = dpt_hip.rollout_policy(dpt_hip.POLICY_THOMPSON, r["means"], H, 0.0, ts_std=0.3, ts_prior_mean=0.5,
+                                 ts_prior_var=1 / 12.0, policy_noise=pg[2:2 + H])
+    assert np.array_equal(out["arm_value"].cpu().numpy().T,
+                          eval_bandit.deploy_online_vec(vec, thompson(True, 2, lambda k: pg[k]), H))
 
 
 def test_fused_bandit_uses_controller_stream():
@@ -366,3 +391,136 @@ def test_cli_collect_then_eval(tmp_path, monkeypatch):
         assert len(figs) >= 2, (env, figs)
         for f in figs:
             os.remove(f)
+
+
+def test_c1_collect_and_eval_bit_exact():
+    """BASELINE config 1 at its size (run_bandit.sh flags: 5 arms, var 0.3; 64 tasks, H=100):
+    (a) the collect rollins of all 64 tasks in one dpt_rollin_bandit launch reproduce the
+    reference's generate_bandit_histories draw for draw; (b) eval_bandit.deploy_online_vec with
+    the DPT sampling controller reproduces the reference's cum_means, actions and rewards bit for
+    bit, and the regret curves (evals/eval_bandit.py:169-178) from the device moments equal the
+    reference's within 1e-12."""
+    import dpt_hip
+    from ctrls.ctrl_bandit import BanditTransformerController
+    from dpt_hip.distributed import regret_stats_allreduce
+    from envs.bandit_env import BanditEnv, BanditEnvVec
+    from evals import eval_bandit
+    g = golden("c1_bandit.npz")
+    N, H, A = (int(x) for x in g["cfg"])
+    cov = g["collect/cov"][:, None]
+    p = (1 - cov) * g["collect/dirichlet"] + cov * np.eye(A)[g["collect/rand_index"]]
+    acts, rews = dpt_hip.rollin_bandit(g["collect/means"], p, H, 0.3, uniforms=g["collect/u"].T,
+                                       noise=g["collect/g"].T)
+    assert np.array_equal(acts.cpu().numpy(), g["collect/actions"])
+    assert np.array_equal(rews.cpu().numpy(), g["collect/rewards"])
+    _, m = ref_model("bandit5", horizon=H)
+    envs = [BanditEnv(mu, H, var=float(g["var"])) for mu in g["eval/means"]]
+    vec = BanditEnvVec(envs)
+    for fused in (True, False):
+        ctrl = BanditTransformerController(m, sample=True, batch_size=N)
+        cm, meta = eval_bandit.deploy_online_vec(vec, ctrl, H, include_meta=True, uniforms=g["eval/u"],
+                                                 noise=g["eval/g"], fused=fused)
+        assert np.array_equal(cm, g["eval/cum_means"]), fused
+        assert np.array_equal(meta["context_actions"].argmax(-1), g["eval/actions"]), fused
+        assert np.array_equal(meta["context_rewards"][..., 0], g["eval/rewards"]), fused
+    opt = torch.from_numpy(g["eval/means"].max(1)).cuda()
+    st = regret_stats_allreduce(opt, torch.from_numpy(cm.T.copy()).cuda(), N)
+    for k in ("subopt_mean", "subopt_sem", "regret_mean", "regret_sem"):
+        np.testing.assert_allclose(st[k].cpu().numpy(), g[f"eval/{k}"], rtol=1e-12, atol=1e-15)
+
+
+def test_gpu_bandit_env_fp32_bit_exact():
+    """GPUBanditEnv (envs/gpu_bandit_env.py:53-74) with the reference's torch.randn draws
+    injected: fp32 rewards mean + g * var bit for bit, done flags, ValueError past H."""
+    from envs.gpu_bandit_env import GPUBanditEnv
+    g = golden("gpu_bandit_env.npz")
+    for var in (0.3, 1.0):
+        env = GPUBanditEnv(5, 64, 3, var=var)
+        env.means = torch.from_numpy(g[f"var{var}/means"]).cuda()
+        draws = g[f"var{var}/g"]
+        env.noise = lambda k: draws[k]
+        env.reset()
+        for t in range(3):
+            us = torch.nn.functional.one_hot(torch.from_numpy(g[f"var{var}/actions"][t]).long(), 5).float().cuda()
+            _, r, done, _ = env.step(us)
+            assert r.dtype == torch.float32
+            assert np.array_equal(r.cpu().numpy().view(np.int32), g[f"var{var}/rewards"][t].view(np.int32)), (var, t)
+            assert np.array_equal(done.cpu().numpy(), g[f"var{var}/done"][t])
+        with pytest.raises(ValueError, match=str(g[f"var{var}/error"])):
+            env.step(us)
+
+
+def test_linear_thompson_rollin_bit_exact():
+    """collect_data.rollin_linear_bandit_vec (collect_data.py:56-80: Thompson, prior N(0, 1), 10-arm
+    linear bandits, lin_d = 2) with the reference's posterior and reward normals injected."""
+    import collect_data
+    from envs.bandit_env import LinearBanditEnv
+    g = golden("linear_thompson.npz")
+    H = g["g"].shape[0]
+    envs = [LinearBanditEnv(t, g["arms"], H, var=float(g["var"])) for t in g["theta"]]
+    assert np.array_equal(np.stack([e.means for e in envs]), g["means"])
+    cs, ca, cn, cr = collect_data.rollin_linear_bandit_vec(envs, noise=g["g"], policy_noise=g["policy_g"])
+    for got, k in ((cs, "context_states"), (ca, "context_actions"), (cn, "context_next_states"),
+                   (cr, "context_rewards")):
+        assert np.array_equal(got, g[k]), k
+
+
+@pytest.mark.parametrize("tag", ["plain", "permuted"])
+def test_darkroom_offline_matches_reference(tag):
+    """eval_darkroom.offline (evals/eval_darkroom.py:124-189) on the reference's fixed contexts:
+    the expert's returns, the greedy leg and the sampled leg (its uniforms injected) equal the
+    reference's returns; per-step rewards through the same device episode."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import dpt_hip
+    from ctrls.ctrl_darkroom import DarkroomTransformerController
+    from envs.darkroom_env import DarkroomEnv, DarkroomEnvPermuted, DarkroomEnvVec
+    from evals import eval_darkroom
+    g = golden("darkroom_offline.npz")
+    n, H, permuted = (int(x) for x in g[f"{tag}/cfg"])
+    _, m = ref_model("darkroom")
+    trajs = []
+    for i in range(n):
+        t = {k: g[f"{tag}/{k}"][i] for k in ("context_states", "context_actions", "context_next_states",
+                                              "context_rewards", "goal")}
+        if permuted:
+            t["perm_index"] = int(g[f"{tag}/perm_index"][i])
+        trajs.append(t)
+    u = g[f"{tag}/u"]
+    res = eval_darkroom.offline(trajs, m, n_eval=n, H=H, dim=10, permuted=bool(permuted), uniforms=u)
+    assert np.array_equal(res["Opt"], g[f"{tag}/opt_returns"])
+    assert np.array_equal(res["Learner"], g[f"{tag}/lnr_rewards"].sum(-1))
+    assert np.array_equal(res["Learner (greedy)"], g[f"{tag}/greedy_rewards"].sum(-1))
+    envs = [DarkroomEnvPermuted(10, t["perm_index"], H) if permuted else DarkroomEnv(10, t["goal"], H)
+            for t in trajs]
+    vec = DarkroomEnvVec(envs)
+    dev = dpt_hip.device()
+    ctx = (torch.tensor(g[f"{tag}/context_states"], dtype=torch.float32, device=dev),
+           torch.tensor(g[f"{tag}/context_actions"], dtype=torch.float32, device=dev),
+           torch.tensor(g[f"{tag}/context_next_states"], dtype=torch.float32, device=dev),
+           torch.tensor(g[f"{tag}/context_rewards"], dtype=torch.float32, device=dev))
+    for sample, key in ((True, "lnr_rewards"), (False, "greedy_rewards")):
+        ctrl = DarkroomTransformerController(m, batch_size=n, sample=sample)
+        ctrl.uniforms = lambda k: u[k]
+        _, _, _, er = eval_darkroom._episode_device(m.device_model(), ctrl, vec, ctx, H)
+        assert np.array_equal(er.cpu().numpy(), g[f"{tag}/{key}"]), key
+
+
+def test_training_mode_no_grad_test_loss_loop():
+    """train.py:265-278 computes its test loss with the model in training mode under no_grad:
+    that works and gives the eval-mode predictions (test=False, preds[:, 1:], net.py:60); the
+    training step itself (grad enabled) raises NotImplementedError naming the backward."""
+    g, m = ref_model("bandit5")
+    m.test = False
+    b = {"query_states": torch.from_numpy(g["T8/query"]).float(), "zeros": torch.zeros(16, 7),
+         "context_states": torch.from_numpy(g["T8/cs"]).float(), "context_actions": torch.from_numpy(g["T8/ca"]).float(),
+         "context_next_states": torch.from_numpy(g["T8/cn"]).float(),
+         "context_rewards": torch.from_numpy(g["T8/cr"]).float()}
+    ref = g["T8/preds_train"]
+    m.train()
+    with torch.no_grad():
+        out = m(b).cpu().numpy()
+    assert out.shape == ref.shape
+    assert (np.abs(out - ref) <= 1e-5 * np.maximum(1, np.abs(ref))).all()
+    with pytest.raises(NotImplementedError, match="backward"):
+        m(b)

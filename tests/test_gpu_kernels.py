@@ -459,17 +459,33 @@ def test_rollout_bernoulli_philox_vs_oracle():
         assert set(np.unique(out["rewards"].cpu().numpy())) <= {0.0, 1.0}
 
 
-@pytest.mark.parametrize("A,H,var", [(5, 500, 0.3), (20, 1000, 0.3)])
-def test_rollout_full_config_sampled_tasks(A, H, var):
+def sampled_tasks(N, tile=8, n_random=40, seed=0):
+    """>= 64 tasks of an N-task launch: every slot of the first two tiles (the two workgroups the
+    dispatcher puts side by side), the last (possibly partial) tile, and random ones."""
+    rs = np.random.RandomState(seed)
+    last = (N - 1) // tile * tile
+    t = np.concatenate([np.arange(min(N, 2 * tile)), np.arange(last, N), rs.choice(N, n_random, replace=False)])
+    return np.unique(t)
+
+
+def first_tie(margin, bar=1e-5):
+    """First step whose uniform lies within ``bar`` of a cdf edge (len(margin) if none)."""
+    tie = np.nonzero(margin < bar)[0]
+    return int(tie[0]) if tie.size else len(margin)
+
+
+@pytest.mark.parametrize("A,H,var,N", [(5, 500, 0.3, 4096), (20, 1000, 0.3, 4096), (5, 500, 0.3, 4093)])
+def test_rollout_full_config_sampled_tasks(A, H, var, N):
     """BASELINE configs 2 (5 arms, H=500) and 4 (20 arms, H=1000; one GPU's 4096-task shard) at full
-    size: the fused rollout over 4096 tasks agrees, on sampled tasks spread over the tiles, with the C
+    size, and config 2 with a partial last tile (4093 tasks): the fused rollout agrees, on >= 64
+    sampled tasks (every slot of the first two tiles, the last tile, random ones), with the C
     oracle fed the same Philox draws -- logits within 1e-5 at every step and actions / arm values
     exactly, each task up to its first near-tie draw (a uniform within 1e-5 of a cdf edge)."""
     import bench
     import dpt_hip
     from oracle import c_oracle
     dh()
-    N, seed, L = 4096, 31337, 4
+    seed, L = 31337, 4
     sd, _ = bench.synthetic_state_dict(L, 1, A, H)
     m = dpt_hip.DeviceModel(sd, L, 1, A, 4 * (1 + H))
     if A == 5:
@@ -481,55 +497,98 @@ def test_rollout_full_config_sampled_tasks(A, H, var):
     acts = out["actions"].cpu().numpy()
     av = out["arm_value"].cpu().numpy()
     assert np.array_equal(av, means[np.arange(N)[:, None], acts])
-    tasks = np.array([0, 7, 8, 2049, 4095])
+    tasks = sampled_tasks(N)
+    assert len(tasks) >= 64
     u = np.stack([philox_np.uniform(seed, h, tasks, dpt_hip.STREAM_SELECT) for h in range(H)])
     g = np.stack([philox_np.normal(seed, h, tasks, dpt_hip.STREAM_REWARD) for h in range(H)])
     blob = dpt_hip.pack_weights(sd, L).numpy()
-    ref = c_oracle.bandit_rollout(blob, L, A, 4 * (1 + H), means[tasks], H, var, u, g, True, False, 4,
+    ref = c_oracle.bandit_rollout(blob, L, A, 4 * (1 + H), means[tasks], H, var, u, g, True, False, 16,
                                   want_logits=True)
     lg = out["logits"].cpu().numpy()[:, tasks]
     margin = O.boundary_margin(O.softmax_f32(ref["logits"], 1.0), u)  # (H, n)
+    full = 0
     for j, t in enumerate(tasks):
-        tie = np.nonzero(margin[:, j] < 1e-5)[0]
-        k = int(tie[0]) if tie.size else H - 1  # steps 0..k agree; a near-tie may flip step k's action
-        assert_logits(lg[:k + 1, j], ref["logits"][:k + 1, j])
-        n = k if tie.size else H
+        n = first_tie(margin[:, j])  # steps 0..n-1 agree exactly; a near-tie may flip step n's action
+        full += n == H
+        assert_logits(lg[:min(n + 1, H), j], ref["logits"][:min(n + 1, H), j])
         assert np.array_equal(acts[t, :n], ref["actions"][j, :n]), t
         assert np.array_equal(av[t, :n], ref["arm_value"][j, :n]), t
+    assert full >= len(tasks) // 2  # most tasks never meet a near-tie: compared over all H steps
+
+
+def check_darkroom_tasks(out, tasks, ref, Heps, horizon):
+    """Device rollout rows ``tasks`` against the C oracle's rows (same order): logits within 1e-5,
+    actions exactly and per-episode returns exactly, each task up to its first near-tie draw."""
+    steps = Heps * horizon
+    lg = out["logits"].cpu().numpy()[:, tasks]
+    acts = out["actions"].cpu().numpy()[tasks]
+    rets = out["returns"].cpu().numpy()[tasks]
+    full = 0
+    for j in range(len(tasks)):
+        n = first_tie(ref["margin"][:, j])
+        full += n == steps
+        assert_logits(lg[:min(n + 1, steps), j], ref["logits"][:min(n + 1, steps), j])
+        assert np.array_equal(acts[j, :n], ref["actions"][j, :n]), tasks[j]
+        assert np.array_equal(rets[j, :n // horizon], ref["returns"][j, :n // horizon]), tasks[j]
+    return full
+
+
+def darkroom_config(N_total, seed=0):
+    """SURVEY.md 8(d) C3 / C5 task set: the 100 grid cells in collect_data.py:408-409's
+    RandomState(0) shuffle order, cycled over the global task ids."""
+    goals = np.array([(j, i) for j in range(10) for i in range(10)])
+    np.random.RandomState(0).shuffle(goals)
+    return goals[np.arange(N_total) % 100]
 
 
 def test_rollout_darkroom_full_config3_sampled_tasks():
     """BASELINE config 3 at full size (4096 tasks, Heps=40, horizon=100, goals in collect_data.py's
-    shuffled order, logits memo on): sampled tasks agree with the float64 numpy oracle fed the same
-    Philox draws -- logits within 1e-5, actions and per-episode returns exactly, each task up to its
-    first near-tie draw."""
+    shuffled order, logits memo on): 64 sampled tasks agree with the float64 C oracle fed the same
+    Philox draws -- logits within 1e-5, actions and per-episode returns exactly, each task up to
+    its first near-tie draw."""
     import bench
     import dpt_hip
+    from oracle import c_oracle
     d = dh()
     N, Heps, horizon, seed, ctr, L = 4096, 40, 100, 99, 3, 4
     sd, _ = bench.synthetic_state_dict(L, 2, 5, horizon)
     m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + horizon))
-    goals = np.array([(j, i) for j in range(10) for i in range(10)])
-    np.random.RandomState(0).shuffle(goals)
-    goals = goals[np.arange(N) % 100]
+    goals = darkroom_config(N)
     out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, counter=ctr, want_actions=True, want_logits=True)
-    tasks = np.array([0, 1337, 4095])
+    tasks = sampled_tasks(N, tile=1, n_random=60)
     steps = Heps * horizon
     u = np.stack([philox_np.uniform(seed, ctr + k, tasks, d.STREAM_SELECT) for k in range(steps)])
-    W = O.split_weights({k: v.numpy() for k, v in sd.items()}, L)
-    ref = O.darkroom_online_rollout(W, goals[tasks], Heps, horizon, horizon, u.reshape(Heps, horizon, -1), True)
-    lg = out["logits"].cpu().numpy()[:, tasks]
-    acts = out["actions"].cpu().numpy()[tasks]
-    rets = out["returns"].cpu().numpy()[tasks]
-    margin = O.boundary_margin(O.softmax_f32(ref["logits"], 1.0), u)  # (steps, n)
-    for j in range(len(tasks)):
-        tie = np.nonzero(margin[:, j] < 1e-5)[0]
-        k = int(tie[0]) if tie.size else steps - 1
-        assert_logits(lg[:k + 1, j], ref["logits"][:k + 1, j])
-        n = k if tie.size else steps
-        assert np.array_equal(acts[j, :n], ref["actions"][j, :n])
-        full_eps = (k // horizon) if tie.size else Heps
-        assert np.array_equal(rets[j, :full_eps], ref["returns"][j, :full_eps])
+    ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + horizon), goals[tasks], Heps,
+                                    horizon, 1, u, True, threads=16, want_logits=True)
+    assert len(tasks) >= 64
+    assert check_darkroom_tasks(out, tasks, ref, Heps, horizon) >= len(tasks) // 2
+
+
+@pytest.mark.parametrize("first_task", [0, 57344])
+def test_rollout_darkroom_config5_shard(first_task):
+    """BASELINE config 5 (DarkRoom, 65,536 tasks over 8 GPUs): one GPU's 8,192-task shard, the first
+    and the last rank's, as bench.py runs it (goals of the global ids, Philox keyed by the global
+    task id, C3 weights, 40 episodes, memo on): 64 sampled tasks of both halves of the shard agree
+    with the float64 C oracle fed the same draws."""
+    import bench
+    import dpt_hip
+    from oracle import c_oracle
+    d = dh()
+    N, Heps, horizon, seed, L = 8192, 40, 100, 1234, 4
+    sd, _ = bench.synthetic_state_dict(L, 2, 5, horizon)
+    m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + horizon))
+    goals = darkroom_config(65536)[first_task:first_task + N]
+    out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, first_task=first_task, want_actions=True,
+                             want_logits=True)
+    rs = np.random.RandomState(first_task)
+    tasks = np.unique(np.concatenate([[0, 1, 4095, 4096, 8191], rs.choice(4096, 30, replace=False),
+                                      4096 + rs.choice(4096, 30, replace=False)]))
+    steps = Heps * horizon
+    u = np.stack([philox_np.uniform(seed, k, first_task + tasks, d.STREAM_SELECT) for k in range(steps)])
+    ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + horizon), goals[tasks], Heps,
+                                    horizon, 1, u, True, threads=16, want_logits=True)
+    assert len(tasks) >= 64
+    assert check_darkroom_tasks(out, tasks, ref, Heps, horizon) >= len(tasks) // 2
 
 
 def test_empty_batches():
@@ -640,3 +699,39 @@ def test_prefill_fp16_split_scales_follow_the_weights(factor):
         finally:
             dpt_hip.set_prefill(True)
         assert err[True] <= max(LOGIT_TOL, 2.0 * err[False]), err
+
+
+def test_rollout_darkroom_dim12_workspace_without_state_table():
+    """dim = 12 (144 grid cells > the 128-row state table): with the workspace but no per-state
+    query table the kernel re-embeds block 0 and takes the query token's key / value through
+    its own branch.  Workspace on vs off agree within the logit bar up to the first differing
+    sampled action, and sampled tasks agree with the float64 C oracle fed the same draws."""
+    import dpt_hip
+    from oracle import c_oracle
+    d = dh()
+    g, m, _ = model_from_golden("darkroom")
+    N, Heps, horizon, R, dim, seed = 256, 5, 40, 2, 12, 21
+    goals = np.random.RandomState(12).randint(0, dim, (N, 2))
+    outs = []
+    try:
+        for on in (False, True):
+            dpt_hip.set_darkroom_workspace(on)
+            o = m.rollout_darkroom(goals, Heps, horizon, R, dim=dim, seed=seed, want_actions=True, want_logits=True)
+            outs.append(o)
+    finally:
+        dpt_hip.set_darkroom_workspace(True)
+    steps = Heps * horizon
+    a0, a1 = (o["actions"].cpu().numpy() for o in outs)
+    diff = a0 != a1
+    first = np.where(diff.any(1), diff.argmax(1), steps)
+    assert (first < steps).mean() <= 0.02
+    l0, l1 = (o["logits"].cpu().numpy() for o in outs)
+    for t in range(N):
+        f = min(first[t] + 1, steps)
+        assert_logits(l1[:f, t], l0[:f, t])
+    tasks = np.arange(0, N, 17)
+    u = np.stack([philox_np.uniform(seed, k, tasks, d.STREAM_SELECT) for k in range(steps)])
+    w = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w/")}
+    ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(w, 4).numpy(), 4, 404, goals[tasks], Heps, horizon, R, u,
+                                    True, dim=dim, threads=16, want_logits=True)
+    check_darkroom_tasks(outs[1], tasks, ref, Heps, horizon)

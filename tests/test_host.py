@@ -44,3 +44,44 @@ def test_run_scripts_parse():
     p.add_argument("--seed", type=int, default=0)
     a = vars(p.parse_args(ev))
     assert a["shuffle"] is True and a["layer"] == 4 and a["epoch"] == 50
+
+
+def _tiny_transformer():
+    from models.net import Transformer
+    return Transformer(dict(horizon=4, state_dim=1, action_dim=5, n_layer=2, n_embd=32, n_head=1, dropout=0.0,
+                            test=False))
+
+
+def _tiny_batch():
+    import torch
+    return {"query_states": torch.ones(2, 1), "zeros": torch.zeros(2, 7), "context_states": torch.ones(2, 3, 1),
+            "context_actions": torch.eye(5)[[0, 1, 2]].expand(2, 3, 5), "context_next_states": torch.ones(2, 3, 1),
+            "context_rewards": torch.zeros(2, 3, 1)}
+
+
+def test_training_forward_names_the_missing_backward():
+    """train.py:286-331 (model in training mode, grad enabled) fails at the forward with a
+    NotImplementedError naming the unbuilt backward, not later inside loss.backward()."""
+    import pytest
+    m = _tiny_transformer()
+    assert m.training
+    with pytest.raises(NotImplementedError, match="backward"):
+        m(_tiny_batch())
+
+
+def test_inference_forward_is_not_guarded():
+    """The no-grad test-loss loop (train.py:265-278) and eval mode (eval.py:152) reach the device
+    path; on this CPU-only container that path raises because there is no GPU, not the guard."""
+    import pytest
+    import torch
+    m = _tiny_transformer()
+    for ctx in ("no_grad", "eval"):
+        if ctx == "eval":
+            m.eval()
+        with (torch.no_grad() if ctx == "no_grad" else torch.enable_grad()):
+            try:
+                m(_tiny_batch())
+            except NotImplementedError as e:  # pragma: no cover - the guard must not fire
+                pytest.fail(f"{ctx}: {e}")
+            except Exception:
+                pass  # no GPU here: dpt_hip refuses to run, as it must

@@ -149,3 +149,83 @@ def test_baseline_offline_and_linucb():
                                   first_u_idx=g["lin/first_action"])
     assert np.array_equal(out["actions"], g["lin/actions"])
     assert np.array_equal(out["cum_means"], g["lin/cum_means"])
+
+
+def test_c1_collect_and_eval_match_reference():
+    """BASELINE config 1 at its size (64 tasks, H=100, 5 arms, var 0.3): the reference's
+    generate_bandit_histories and the DPT online eval with its regret curves."""
+    g = golden("c1_bandit.npz")
+    N, H, A = (int(x) for x in g["cfg"])
+    for i in range(N):
+        _, us, _, rs = O.rollin_bandit(g["collect/means"][i], g["collect/cov"][i], g["collect/dirichlet"][i],
+                                       g["collect/rand_index"][i], g["collect/u"][i], g["collect/g"][i], 0.3)
+        assert np.array_equal(us.argmax(-1), g["collect/actions"][i]), i
+        assert np.array_equal(rs, g["collect/rewards"][i]), i
+    assert np.array_equal(g["collect/optimal_action"].argmax(-1), g["collect/means"].argmax(-1))
+    _, W = weights("bandit5")
+    out = O.bandit_online_rollout(W, g["eval/means"], H, float(g["var"]), g["eval/u"], g["eval/g"], True)
+    assert np.array_equal(out["actions"], g["eval/actions"])
+    assert np.array_equal(out["cum_means"], g["eval/cum_means"])
+    assert np.array_equal(out["rewards"], g["eval/rewards"])
+    opt = np.repeat(g["eval/means"].max(1, keepdims=True), H, axis=1)
+    st = O.regret_curves(opt, g["eval/cum_means"].T)
+    for k in ("subopt_mean", "subopt_sem", "regret_mean", "regret_sem"):
+        np.testing.assert_allclose(st[k], g[f"eval/{k}"], rtol=1e-12, atol=1e-15)
+
+
+def test_gpu_bandit_env_rewards_bit_exact():
+    g = golden("gpu_bandit_env.npz")
+    for var in (0.3, 1.0):
+        for t in range(3):
+            r = O.gpu_bandit_reward_f32(g[f"var{var}/means"], g[f"var{var}/actions"][t], g[f"var{var}/g"][t], var)
+            assert r.dtype == np.float32
+            assert np.array_equal(r.view(np.int32), g[f"var{var}/rewards"][t].view(np.int32)), (var, t)
+        assert g[f"var{var}/done"][-1].all() and not g[f"var{var}/done"][:-1].any()
+
+
+def test_linear_thompson_rollin_matches_reference():
+    g = golden("linear_thompson.npz")
+    H = g["g"].shape[0]
+    assert np.array_equal(O.linear_means(g["arms"], g["theta"]), g["means"])
+    out = O.bandit_policy_rollout("thompson", g["means"], H, float(g["var"]), g["g"],
+                                  ts=dict(std=float(g["var"]), prior_mean=0.0, prior_var=1.0), ts_g=g["policy_g"])
+    assert np.array_equal(out["actions"], g["context_actions"].argmax(-1))
+    assert np.array_equal(out["rewards"], g["context_rewards"])
+
+
+@pytest.mark.parametrize("tag", ["plain", "permuted"])
+def test_darkroom_offline_matches_reference(tag):
+    g = golden("darkroom_offline.npz")
+    _, W = weights("darkroom")
+    n, H, permuted = (int(x) for x in g[f"{tag}/cfg"])
+    perm = O.perm_table()[g[f"{tag}/perm_index"]] if permuted else None
+    goals = g[f"{tag}/goal"]
+    ctx = (g[f"{tag}/context_states"].astype(np.float64), g[f"{tag}/context_actions"],
+           g[f"{tag}/context_next_states"].astype(np.float64), g[f"{tag}/context_rewards"][..., None].astype(np.float64))
+    assert np.array_equal(O.darkroom_opt_returns(goals, H, perm), g[f"{tag}/opt_returns"])
+    greedy = O.darkroom_offline_episode(W, goals, ctx, H, None, sample=False, perm=perm)
+    assert np.array_equal(greedy, g[f"{tag}/greedy_rewards"])
+    lnr = O.darkroom_offline_episode(W, goals, ctx, H, g[f"{tag}/u"], sample=True, perm=perm)
+    assert np.array_equal(lnr, g[f"{tag}/lnr_rewards"])
+
+
+@pytest.mark.parametrize("tag", ["sample", "greedy", "permuted"])
+def test_c_darkroom_oracle_matches_reference(tag):
+    """The float64 C restatement of the DarkRoom online eval (oracle/dpt_oracle.c, the full-size
+    checker of the GPU tests) against the reference's recorded rollouts, memo on and off."""
+    import torch
+    from oracle import c_oracle
+    import dpt_hip
+    g = golden(f"rollout_darkroom_{tag}.npz")
+    fw, _ = weights("darkroom")
+    n, Heps, H, horizon, sample = (int(x) for x in g["cfg"])
+    sd = {k[2:]: torch.from_numpy(v) for k, v in fw.items() if k.startswith("w/")}
+    blob = dpt_hip.pack_weights(sd, 4).numpy()
+    perm = O.perm_table()[g["perm_index"]] if tag == "permuted" else None
+    u = g["u"].reshape(Heps * horizon, n) if sample else None
+    outs = [c_oracle.darkroom_rollout(blob, 4, 404, g["goals"], Heps, horizon, H // horizon, u, bool(sample), perm,
+                                      memo=memo, threads=2, want_logits=True) for memo in (False, True)]
+    for o in outs:
+        assert np.abs(o["logits"] - g["logits"]).max() <= 1e-5
+        assert np.array_equal(o["returns"], g["returns"])
+    assert np.array_equal(outs[0]["actions"], outs[1]["actions"])
