@@ -53,9 +53,11 @@ class _Stream:
         return self.seed, c
 
 
-def _device_rewards(means, action_idx, var, type_code, stream, first_task=0):
+def _device_rewards(means, action_idx, var, type_code, stream, first_task=0, noise=None):
     seed, ctr = stream.next()
-    r, _ = dpt_hip.bandit_step(means, action_idx, var, type_code, seed=seed, counter=ctr, first_task=first_task)
+    g = None if noise is None else np.asarray(noise(ctr), np.float64).reshape(-1)
+    r, _ = dpt_hip.bandit_step(means, action_idx, var, type_code, noise=g, seed=seed, counter=ctr,
+                               first_task=first_task)
     return r.cpu().numpy()
 
 
@@ -122,6 +124,9 @@ class BanditEnvVec(BaseEnv):
         self.du = envs[0].du
         self._means_d = None
         self._stream = _Stream()
+        # optional injected draws: callable(step counter) -> (N,) standard normals (or uniforms,
+        # bernoulli): the np.random.normal of BanditEnv.transit per env; default: Philox
+        self.noise = None
 
     # ------------------------------------------------------------------ device state
     @property
@@ -153,7 +158,7 @@ class BanditEnvVec(BaseEnv):
         if any(env.current_step >= env.H for env in self._envs):
             raise ValueError("Episode has already ended")
         a = np.argmax(np.asarray(actions), axis=-1)
-        rews = _device_rewards(self.means_device, a, self.var, self.type_code, self._stream)
+        rews = _device_rewards(self.means_device, a, self.var, self.type_code, self._stream, noise=self.noise)
         next_obs, dones = [], []
         for env in self._envs:
             env.current_step += 1

@@ -123,6 +123,28 @@ def deploy_online_vec(vec_env, controller, horizon, include_meta=False, uniforms
                 "context_rewards": out["rewards"].cpu().numpy()[..., None]}
         return cum_means, meta
 
+    # the reference's per-step loop; injected draws are handed to the env / controller hooks
+    # (step h uses row h), which read them by their own stream counters
+    hooks = []
+
+    def hook(obj, attr, rows):
+        if rows is not None and hasattr(obj, attr):
+            c0 = obj._stream.counter
+            hooks.append((obj, attr, getattr(obj, attr)))
+            setattr(obj, attr, lambda k, _r=rows, _c=c0: _r[k - _c])
+
+    hook(vec_env, "noise", noise)
+    hook(controller, "uniforms", uniforms)
+    hook(controller, "policy_noise", policy_noise)
+    try:
+        return _deploy_online_steps(vec_env, controller, horizon, include_meta)
+    finally:
+        for obj, attr, old in hooks:
+            setattr(obj, attr, old)
+
+
+def _deploy_online_steps(vec_env, controller, horizon, include_meta):
+    num_envs = vec_env.num_envs
     context_states = np.zeros((num_envs, horizon, vec_env.dx))
     context_actions = np.zeros((num_envs, horizon, vec_env.du))
     context_next_states = np.zeros((num_envs, horizon, vec_env.dx))

@@ -459,7 +459,7 @@ def test_rollout_bernoulli_philox_vs_oracle():
         assert set(np.unique(out["rewards"].cpu().numpy())) <= {0.0, 1.0}
 
 
-def sampled_tasks(N, tile=8, n_random=40, seed=0):
+def sampled_tasks(N, tile=8, n_random=48, seed=0):
     """>= 64 tasks of an N-task launch: every slot of the first two tiles (the two workgroups the
     dispatcher puts side by side), the last (possibly partial) tile, and random ones."""
     rs = np.random.RandomState(seed)
@@ -555,7 +555,7 @@ def test_rollout_darkroom_full_config3_sampled_tasks():
     m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + horizon))
     goals = darkroom_config(N)
     out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, counter=ctr, want_actions=True, want_logits=True)
-    tasks = sampled_tasks(N, tile=1, n_random=60)
+    tasks = sampled_tasks(N, tile=1, n_random=64)
     steps = Heps * horizon
     u = np.stack([philox_np.uniform(seed, ctr + k, tasks, d.STREAM_SELECT) for k in range(steps)])
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + horizon), goals[tasks], Heps,
@@ -581,8 +581,8 @@ def test_rollout_darkroom_config5_shard(first_task):
     out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, first_task=first_task, want_actions=True,
                              want_logits=True)
     rs = np.random.RandomState(first_task)
-    tasks = np.unique(np.concatenate([[0, 1, 4095, 4096, 8191], rs.choice(4096, 30, replace=False),
-                                      4096 + rs.choice(4096, 30, replace=False)]))
+    tasks = np.unique(np.concatenate([[0, 1, 4095, 4096, 8191], rs.choice(4096, 32, replace=False),
+                                      4096 + rs.choice(4096, 32, replace=False)]))
     steps = Heps * horizon
     u = np.stack([philox_np.uniform(seed, k, first_task + tasks, d.STREAM_SELECT) for k in range(steps)])
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + horizon), goals[tasks], Heps,
