@@ -704,9 +704,13 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * wave + 1) * 16 + 4 * g) * up) * down;
                         float gv[8];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            gv[r] = gelu_fast(h0[r]);
-                            gv[4 + r] = gelu_fast(h1[r]);
+                        for (int r = 0; r < 4; r += 2) {
+                            const floatx2 g0 = gelu_fast2(floatx2{h0[r], h0[r + 1]});
+                            const floatx2 g1 = gelu_fast2(floatx2{h1[r], h1[r + 1]});
+                            gv[r] = g0.x;
+                            gv[r + 1] = g0.y;
+                            gv[4 + r] = g1.x;
+                            gv[4 + r + 1] = g1.y;
                         }
                         const Split2 gs = split2(gv, xs_scale);
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};

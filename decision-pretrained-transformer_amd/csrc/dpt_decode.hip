@@ -518,7 +518,7 @@ __device__ __attribute__((always_inline)) inline float4 attend_l0(const float4* 
 // weighted wpe sum one [32 x 16 positions] x [16 x 16 tasks] product; everything else
 // is per-(position, task) scalar work, one element per lane and register.  Wave w
 // takes the tiles w, w + 8, ...; its partial softmax state per task (m, l, the scalar
-// sums, the arm sums and the wpe sum) goes to part[w][task][48] for l0_merge.
+// sums, the arm sums and the wpe sum) goes to part[w][task][kL0Part] for l0_merge.
 constexpr int kL0Part = 64;  // floats per (wave, task) partial of l0_tiles (36 + NA <= 64)
 
 template <int NA, int TILE>

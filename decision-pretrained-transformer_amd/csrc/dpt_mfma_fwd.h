@@ -75,14 +75,22 @@ struct Split2 {
     halfx8 h, m;
 };
 __device__ inline Split2 split2(const float (&v)[8], float scale) {
+    // m = f16(x - h) (x = v scale) as one fma of the f32 value and the f16 h, rounded once to f16: the
+    // compiler emits v_fma_mix{lo,hi}_f16 (built with -fno-slp-vectorize; h is not converted
+    // back to fp32 first).  x - h is exact in fp32, so m equals f16(f32(x - h)).
+    // (an opaque 1.0 multiplier keeps the fma from folding into a plain subtraction, which
+    // would lose the mixed-precision form)
+    float one = 1.0f;
+    asm volatile("" : "+s"(one));
     unsigned hh[4], mm[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const floatx2 x = floatx2{v[2 * p], v[2 * p + 1]} * floatx2{scale, scale};
         const halfx2 h = __builtin_convertvector(x, halfx2);
-        const floatx2 r = x - __builtin_convertvector(h, floatx2);
+        const halfx2 m = {(_Float16)__builtin_fmaf(x.x, one, -(float)h.x),
+                          (_Float16)__builtin_fmaf(x.y, one, -(float)h.y)};
         hh[p] = __builtin_bit_cast(unsigned, h);
-        mm[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, halfx2));
+        mm[p] = __builtin_bit_cast(unsigned, m);
     }
     return Split2{__builtin_bit_cast(halfx8, uint4{hh[0], hh[1], hh[2], hh[3]}),
                   __builtin_bit_cast(halfx8, uint4{mm[0], mm[1], mm[2], mm[3]})};
@@ -180,6 +188,16 @@ __device__ inline void ln_cols(const float (&v)[8], float (&out)[8], const float
     out[4] = o2.x; out[5] = o2.y; out[6] = o3.x; out[7] = o3.y;
 }
 
+// gelu_fast on a pair: the same operations in the same order on v_pk_{mul,fma,add}_f32 (each
+// half rounded like the scalar op: bit-identical), with the two transcendentals per value
+__device__ inline floatx2 gelu_fast2(floatx2 x) {
+    const float c1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+    const float c2 = c1 * 0.044715f;
+    const floatx2 t = __builtin_elementwise_fma(x * x, floatx2{c2, c2}, floatx2{c1, c1}) * x;
+    const floatx2 d = floatx2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + floatx2{1.0f, 1.0f};
+    return x * floatx2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
 __device__ inline float gelu_fast(float x) {
     // gelu_new (transformers/activations.py:65): 0.5x(1 + tanh(z)) = x * sigmoid(2z)
     // = x / (1 + 2^(x * (c1 + c2 x^2))), z = sqrt(2/pi)(x + 0.044715 x^3), log2(e) folded in
@@ -222,9 +240,12 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
         for (int j = 0; j < NB; ++j) {
             const floatx4 h0 = mfma_x3(wf0, xs[j], fb0) * down, h1 = mfma_x3(wf1, xs[j], fb1) * down;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                gv[j][r] = gelu_fast(h0[r]);
-                gv[j][4 + r] = gelu_fast(h1[r]);
+            for (int r = 0; r < 4; r += 2) {
+                const floatx2 g0 = gelu_fast2(floatx2{h0[r], h0[r + 1]}), g1 = gelu_fast2(floatx2{h1[r], h1[r + 1]});
+                gv[j][r] = g0.x;
+                gv[j][r + 1] = g0.y;
+                gv[j][4 + r] = g1.x;
+                gv[j][4 + r + 1] = g1.y;
             }
         }
         if (p + 1 < kFF / 32) {

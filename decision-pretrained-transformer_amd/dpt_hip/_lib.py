@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdpt_hip.so")
+# DPT_HIP_LIB: another build's file name in this directory (A/B runs of kernel variants)
+LIB_PATH = os.path.join(_HERE, os.environ.get("DPT_HIP_LIB", "libdpt_hip.so"))
 ABI_VERSION = 4
 
 DPT_OK = 0

@@ -148,8 +148,12 @@ int dpt_prefill_max_window(const dpt_model* model, int32_t* tokens_out_host);
  * Exact incremental form of the growing-window forward used by the bandit
  * online loop (evals/eval_bandit.py:70-89): the query token is identical at
  * every step, so positions 0..h-1 are unchanged between steps h-1 and h and
- * their keys/values can be cached.  Cache layout [2][n_layer][N'][max_pos][E],
- * N' = N rounded up to a multiple of 16 (whole decode tiles).                 */
+ * their keys/values can be cached.  dpt_kvcache_numel sizes the buffer for
+ * [2][n_layer][N'][max_pos][E] floats, N' = N rounded up to a multiple of 16.
+ * Only dpt_rollout_bandit lays it out with the padded N' stride (whole decode
+ * tiles; its own per-position records); dpt_decode_step and the
+ * long-window dpt_forward_window use [2][n_layer][N][max_pos][E] (V half at
+ * n_layer*N*max_pos*E) and simply leave the padding unused.                   */
 int dpt_kvcache_numel(const dpt_model* model, int32_t N, int32_t max_pos, int64_t* numel_out_host);
 /* one decode position for all N tasks: token (N,F) packed features of position
  * `pos` (pos 0 is the query token), appends K/V at `pos`, logits (N,A) of it.  */

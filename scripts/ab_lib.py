@@ -52,7 +52,15 @@ def child(lib):
             torch.cuda.synchronize()
             if rnd > 0:
                 ts.append(a.elapsed_time(b))
-        print(json.dumps({"lib": lib, "ms": ts, "checksum": float(out["returns"].sum())}))
+        # bit-identity digest: actions and logits of a smaller launch (AB_DIGEST=0 skips it)
+        digest = None
+        if os.environ.get("AB_DIGEST", "1") == "1":
+            import hashlib
+            o = m.rollout_darkroom(goals[:512], 6, 100, 1, seed=77, want_actions=True, want_logits=True)
+            h = hashlib.sha1(o["actions"].cpu().numpy().tobytes())
+            h.update(o["logits"].cpu().numpy().tobytes())
+            digest = h.hexdigest()[:16]
+        print(json.dumps({"lib": lib, "ms": ts, "checksum": float(out["returns"].sum()), "digest": digest}))
         return
     sd, _ = bench.synthetic_state_dict(4, 1, A, H)
     m = dpt_hip.DeviceModel(sd, 4, 1, A, 4 * (1 + H))
@@ -82,7 +90,7 @@ if __name__ == "__main__":
                                  text=True, timeout=300).stdout.strip().splitlines()[-1]
             d = json.loads(out)
             res[lib] += d["ms"]
-            chk[lib] = d["checksum"]
+            chk[lib] = (d["checksum"], d.get("digest"))
     H, N = int(os.environ.get("AB_H", "500")), int(os.environ.get("AB_N", "4096"))
     sys.path[:0] = [ROOT]
     import bench
