@@ -69,6 +69,11 @@ int set_block0_mfma(int);
 int regret_max_steps();
 int64_t regret_workspace_numel(int N, int H);
 int launch_regret_moments(const double*, const double*, int, int, int, const double*, double*, double*, hipStream_t);
+int train_forward(const TrDims&, const float*, const float*, float*, float*, hipStream_t);
+int train_backward(const TrDims&, const float*, const float*, float*, const float*, float*, hipStream_t);
+int64_t train_workspace_numel(const TrDims&);
+int64_t train_blob_numel(const TrDims&);
+int train_dims_check(const TrDims&);
 
 }  // namespace dpt
 
@@ -474,6 +479,50 @@ int dpt_rollout_darkroom(const dpt_model* m, const dpt_darkroom_rollout_args* a,
         return DPT_EUNSUPPORTED;
     }
     return launch_rollout_darkroom(m->view, m->frag, *a, S(stream));
+}
+
+static int train_dims(const dpt_train_desc* d, TrDims& o) {
+    REQUIRE(d != nullptr, "null train desc");
+    REQUIRE(d->n_layer >= 1 && d->n_layer <= 64 && d->n_embd >= 1 && d->n_embd <= 1024 && d->state_dim >= 1 &&
+                d->action_dim >= 1 && d->n_positions >= 1 && d->batch >= 1 && d->window >= 1 &&
+                d->window <= d->n_positions,
+            "train desc: n_layer=%d n_embd=%d sd=%d A=%d n_positions=%d batch=%d window=%d", d->n_layer, d->n_embd,
+            d->state_dim, d->action_dim, d->n_positions, d->batch, d->window);
+    o = TrDims{d->n_layer, d->n_embd, 2 * d->state_dim + d->action_dim + 1, d->action_dim, d->batch, d->window,
+               d->n_positions};
+    return train_dims_check(o);
+}
+
+int dpt_train_blob_numel(const dpt_train_desc* d, int64_t* numel) {
+    TrDims t;
+    if (int rc = train_dims(d, t)) return rc;
+    REQUIRE(numel, "null numel");
+    *numel = train_blob_numel(t);
+    return DPT_OK;
+}
+
+int dpt_train_workspace_numel(const dpt_train_desc* d, int64_t* numel) {
+    TrDims t;
+    if (int rc = train_dims(d, t)) return rc;
+    REQUIRE(numel, "null numel");
+    *numel = train_workspace_numel(t);
+    return DPT_OK;
+}
+
+int dpt_train_forward(const dpt_train_desc* d, const float* blob, const float* tokens, float* ws, float* preds,
+                      void* stream) {
+    TrDims t;
+    if (int rc = train_dims(d, t)) return rc;
+    REQUIRE(blob && tokens && ws && preds, "null pointer");
+    return train_forward(t, blob, tokens, ws, preds, S(stream));
+}
+
+int dpt_train_backward(const dpt_train_desc* d, const float* blob, const float* tokens, float* ws,
+                       const float* dpreds, float* dblob, void* stream) {
+    TrDims t;
+    if (int rc = train_dims(d, t)) return rc;
+    REQUIRE(blob && tokens && ws && dpreds && dblob, "null pointer");
+    return train_backward(t, blob, tokens, ws, dpreds, dblob, S(stream));
 }
 
 }  // extern "C"

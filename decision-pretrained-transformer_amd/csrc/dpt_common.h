@@ -243,6 +243,14 @@ __device__ inline int select_from_cdf(const double* q, double u) {
 // sum_s P_s v_s = (sum_s P_s y_s) Wv + bv.  Used by the bandit rollout
 // (dpt_decode.hip) and the MFMA window forwards (dpt_mfma_fwd.h).  All
 // matrices [in][out], E x E.
+// Dimensions of the generic-width training forward / backward (dpt_train.hip): layers, width,
+// token features, actions, sequences, tokens per sequence, wpe rows.
+struct TrDims {
+    int L, E, F, A, B, T, npos;
+    __host__ __device__ int R() const { return B * T; }
+    __host__ __device__ int64_t layer_size() const { return 12ll * E * E + 13ll * E; }
+};
+
 struct L0Off {
     static constexpr int G = 0;                 // Wq Wk^T: u = xn G + g0 = Wk q
     static constexpr int g0 = G + kE * kE;      // Wk bq

@@ -1,0 +1,540 @@
+// Training forward / backward of the DPT Transformer (models/net.py:9-60 with test=False:
+// preds at every position; train.py:286-331 trains on preds[:, 1:] with CrossEntropyLoss(sum)
+// and AdamW).  SURVEY.md 8(f) row 4.  Generic in the model width (any n_embd, FF = 4 n_embd,
+// one head as net.py:29 forces) and the window, all fp32:
+//
+//   forward : embed_transition + wpe -> n_layer x [ln_1, c_attn, causal softmax(QK^T/sqrt(E)) V,
+//             c_proj + residual, ln_2, c_fc, gelu_new, mlp.c_proj + residual] -> ln_f -> head,
+//             saving what the backward needs (the residual stream, LayerNorm statistics, q/k/v,
+//             the attention probabilities, the MLP pre-activations) in a caller workspace;
+//   backward: dL/dpreds -> every parameter's gradient in the packed blob layout of dpt_hip.h,
+//             with fixed-order (deterministic) reductions over the B*T rows.
+//
+// The kernels are plain row / element kernels: at the reference's widths (E = 32, FF = 128) a
+// training step is dominated by launch count and the O(T^2) attention, not by dense products,
+// and one code path serves every width (the fused rollout kernels are specialised for E = 32).
+// The same forward serves dpt_forward_window for models of other widths (inference).
+#include "dpt_common.h"
+
+namespace dpt {
+
+constexpr int kTrThreads = 256;
+constexpr int kTrRowsPerChunk = 256;  // rows per partial of the weight-gradient reductions
+
+
+// offsets of one layer in the packed blob (dpt_hip.h: [ln1 g b][c_attn W b][c_proj W b][ln2 g b][c_fc W b][mlp.c_proj W b])
+struct TrLayer {
+    int64_t ln1_g, ln1_b, attn_w, attn_b, proj_w, proj_b, ln2_g, ln2_b, fc_w, fc_b, mp_w, mp_b;
+    __host__ __device__ static TrLayer make(int64_t base, int E) {
+        TrLayer o;
+        int64_t p = base;
+        o.ln1_g = p; p += E;
+        o.ln1_b = p; p += E;
+        o.attn_w = p; p += 3ll * E * E;
+        o.attn_b = p; p += 3 * E;
+        o.proj_w = p; p += (int64_t)E * E;
+        o.proj_b = p; p += E;
+        o.ln2_g = p; p += E;
+        o.ln2_b = p; p += E;
+        o.fc_w = p; p += 4ll * E * E;
+        o.fc_b = p; p += 4 * E;
+        o.mp_w = p; p += 4ll * E * E;
+        o.mp_b = p;
+        return o;
+    }
+};
+
+struct TrBlob {  // offsets of the model-level parameters
+    int64_t emb_w, emb_b, wpe, layers, lnf_g, lnf_b, head_w, head_b, total;
+    __host__ __device__ static TrBlob make(const TrDims& d) {
+        TrBlob b;
+        int64_t p = 0;
+        b.emb_w = p; p += (int64_t)d.F * d.E;
+        b.emb_b = p; p += d.E;
+        b.wpe = p; p += (int64_t)d.npos * d.E;
+        b.layers = p; p += d.L * d.layer_size();
+        b.lnf_g = p; p += d.E;
+        b.lnf_b = p; p += d.E;
+        b.head_w = p; p += (int64_t)d.E * d.A;
+        b.head_b = p; p += d.A;
+        b.total = p;
+        return b;
+    }
+};
+
+// Workspace (floats): the forward's saved activations, then the backward's scratch.
+struct TrWs {
+    int64_t x, y1, st1, qkv, P, o, x2, y2, st2, hpre, yf, stf;  // x: [L+1][R][E]; per-layer arrays [L][...]
+    int64_t dx, dx2, dqkv, dout, dh, dy, dS, part, total;
+    __host__ __device__ static int64_t nchunks(const TrDims& d) { return (d.R() + kTrRowsPerChunk - 1) / kTrRowsPerChunk; }
+    __host__ __device__ static TrWs make(const TrDims& d) {
+        TrWs w;
+        const int64_t R = d.R(), E = d.E, L = d.L, TT = (int64_t)d.B * d.T * d.T;
+        int64_t p = 0;
+        w.x = p; p += (L + 1) * R * E;
+        w.y1 = p; p += L * R * E;
+        w.st1 = p; p += L * R * 2;
+        w.qkv = p; p += L * R * 3 * E;
+        w.P = p; p += L * TT;
+        w.o = p; p += L * R * E;
+        w.x2 = p; p += L * R * E;
+        w.y2 = p; p += L * R * E;
+        w.st2 = p; p += L * R * 2;
+        w.hpre = p; p += L * R * 4 * E;
+        w.yf = p; p += R * E;
+        w.stf = p; p += R * 2;
+        w.dx = p; p += R * E;
+        w.dx2 = p; p += R * E;
+        w.dqkv = p; p += R * 3 * E;
+        w.dout = p; p += R * E;
+        w.dh = p; p += R * 4 * E;
+        w.dy = p; p += R * E;
+        w.dS = p; p += TT;
+        const int64_t wmax = std::max<int64_t>(4 * E * E + 4 * E, (int64_t)(d.F + 1) * E);
+        w.part = p; p += nchunks(d) * std::max<int64_t>(wmax, (int64_t)(E + 1) * d.A);
+        w.total = p;
+        return w;
+    }
+};
+
+__device__ inline float tr_gelu(float x) {  // gelu_new (transformers/activations.py:65), accurate tanhf
+    return 0.5f * x * (1.0f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
+}
+__device__ inline float tr_gelu_grad(float x) {
+    const float c = 0.7978845608028654f, a = 0.044715f;
+    const float th = tanhf(c * (x + a * x * x * x));
+    return 0.5f * (1.0f + th) + 0.5f * x * (1.0f - th * th) * c * (1.0f + 3.0f * a * x * x);
+}
+
+// order this wave's LDS writes before its later LDS reads of other lanes' entries
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+__device__ inline float wave_max(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+    return v;
+}
+
+// x[r][e] = embed_transition(tok[r]) + wpe[t]   (models/net.py:52-54 + GPT2Model inputs_embeds + wpe)
+__global__ void tr_embed(const float* __restrict__ tok, const float* __restrict__ blob, TrDims d, TrBlob b,
+                         float* __restrict__ x) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)d.R() * d.E) return;
+    const int r = (int)(i / d.E), e = (int)(i % d.E), t = r % d.T;
+    float acc = blob[b.emb_b + e];
+    for (int f = 0; f < d.F; ++f) acc = fmaf(tok[(int64_t)r * d.F + f], blob[b.emb_w + (int64_t)f * d.E + e], acc);
+    x[i] = acc + blob[b.wpe + (int64_t)t * d.E + e];
+}
+
+// LayerNorm over E (eps 1e-5), one wave per row; saves (mean, rstd)
+__global__ void tr_layernorm(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ bb,
+                             int R, int E, float* __restrict__ y, float* __restrict__ st) {
+    const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= R) return;
+    const float* xr = x + (int64_t)row * E;
+    float s = 0.f;
+    for (int e = lane; e < E; e += 64) s += xr[e];
+    const float mean = wave_sum(s) / E;
+    float q = 0.f;
+    for (int e = lane; e < E; e += 64) q += (xr[e] - mean) * (xr[e] - mean);
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / E + 1e-5f);
+    for (int e = lane; e < E; e += 64) y[(int64_t)row * E + e] = (xr[e] - mean) * rstd * g[e] + bb[e];
+    if (lane == 0) {
+        st[2 * row] = mean;
+        st[2 * row + 1] = rstd;
+    }
+}
+
+// Y[r][o] = bias[o] + sum_i act(X[r][i]) W[i][o] (+ res[r][o]); act = gelu_new when gelu != 0
+__global__ void tr_linear(const float* __restrict__ X, const float* __restrict__ W, const float* __restrict__ bias,
+                          const float* __restrict__ res, int R, int IN, int OUT, int gelu, float* __restrict__ Y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)R * OUT) return;
+    const int r = (int)(i / OUT), o = (int)(i % OUT);
+    const float* xr = X + (int64_t)r * IN;
+    float acc = bias[o];
+    for (int k = 0; k < IN; ++k) acc = fmaf(gelu ? tr_gelu(xr[k]) : xr[k], W[(int64_t)k * OUT + o], acc);
+    Y[i] = res ? acc + res[i] : acc;
+}
+
+// causal single-head attention, one wave per (task, query t): P[b][t][j] = softmax_j(q_t k_j / sqrt(E)),
+// j <= t, and o_t = sum_j P[b][t][j] v_j.  qkv rows [q | k | v] (c_attn output).
+__global__ void tr_attn_fwd(const float* __restrict__ qkv, TrDims d, float* __restrict__ P, float* __restrict__ O) {
+    extern __shared__ float sm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (blockDim.x / 64) + wave;
+    if (row >= d.R()) return;
+    const int E = d.E, T = d.T, b = row / T, t = row % T;
+    float* pr = sm + (size_t)wave * (T + E);
+    float* q = pr + T;
+    const float* base = qkv + (int64_t)b * T * 3 * E;
+    for (int e = lane; e < E; e += 64) q[e] = base[(int64_t)t * 3 * E + e];
+    wave_lds_sync();
+    const float scale = 1.0f / sqrtf((float)E);
+    float m = -INFINITY;
+    for (int j = lane; j <= t; j += 64) {
+        const float* k = base + (int64_t)j * 3 * E + E;
+        float s = 0.f;
+        for (int e = 0; e < E; ++e) s = fmaf(q[e], k[e], s);
+        s *= scale;
+        pr[j] = s;
+        m = fmaxf(m, s);
+    }
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = lane; j <= t; j += 64) {
+        const float p = expf(pr[j] - m);
+        pr[j] = p;
+        l += p;
+    }
+    const float inv = 1.0f / wave_sum(l);
+    float* prow = P + ((int64_t)b * T + t) * T;
+    for (int j = lane; j <= t; j += 64) {
+        const float p = pr[j] * inv;
+        pr[j] = p;
+        prow[j] = p;
+    }
+    wave_lds_sync();
+    for (int e = lane; e < E; e += 64) {
+        float acc = 0.f;
+        for (int j = 0; j <= t; ++j) acc = fmaf(pr[j], base[(int64_t)j * 3 * E + 2 * E + e], acc);
+        O[(int64_t)row * E + e] = acc;
+    }
+}
+
+// ------------------------------------------------------------------------------ backward
+
+// dX[r][i] = sum_o dY[r][o] W[i][o], times gelu'(hpre[r][i]) when hpre is given, plus add[r][i]
+__global__ void tr_linear_bwd_data(const float* __restrict__ dY, const float* __restrict__ W, int R, int IN, int OUT,
+                                   const float* __restrict__ hpre, const float* __restrict__ add,
+                                   float* __restrict__ dX) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)R * IN) return;
+    const int r = (int)(i / IN), k = (int)(i % IN);
+    const float* dy = dY + (int64_t)r * OUT;
+    const float* w = W + (int64_t)k * OUT;
+    float acc = 0.f;
+    for (int o = 0; o < OUT; ++o) acc = fmaf(dy[o], w[o], acc);
+    if (hpre) acc *= tr_gelu_grad(hpre[i]);
+    dX[i] = add ? acc + add[i] : acc;
+}
+
+// partial weight gradients over one chunk of rows: part[c][i][o] = sum_r act(X[r][i]) dY[r][o] for
+// i < IN and part[c][IN][o] = sum_r dY[r][o] (the bias); act = gelu_new when gelu != 0.
+// grid (chunks, ceil((IN+1)*OUT / threads)); X may be null for a bias-only reduction.
+__global__ void tr_wgrad_part(const float* __restrict__ X, const float* __restrict__ dY, int R, int IN, int OUT,
+                              int gelu, float* __restrict__ part) {
+    const int c = blockIdx.x;
+    const int k = blockIdx.y * blockDim.x + threadIdx.x;
+    if (k >= (IN + 1) * OUT) return;
+    const int i = k / OUT, o = k % OUT;
+    const int r0 = c * kTrRowsPerChunk, r1 = min(R, r0 + kTrRowsPerChunk);
+    float acc = 0.f;
+    if (i < IN) {
+        for (int r = r0; r < r1; ++r) {
+            const float xv = X[(int64_t)r * IN + i];
+            acc = fmaf(gelu ? tr_gelu(xv) : xv, dY[(int64_t)r * OUT + o], acc);
+        }
+    } else {
+        for (int r = r0; r < r1; ++r) acc += dY[(int64_t)r * OUT + o];
+    }
+    part[(int64_t)c * (IN + 1) * OUT + k] = acc;
+}
+
+// dW (IN x OUT, the blob's [in][out] layout) and db (OUT) = the chunk partials summed in chunk order
+__global__ void tr_wgrad_reduce(const float* __restrict__ part, int nch, int IN, int OUT, float* __restrict__ dW,
+                                float* __restrict__ db) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= (IN + 1) * OUT) return;
+    float acc = 0.f;
+    for (int c = 0; c < nch; ++c) acc += part[(int64_t)c * (IN + 1) * OUT + k];
+    if (k < IN * OUT) {
+        if (dW) dW[k] = acc;
+    } else if (db) {
+        db[k - IN * OUT] = acc;
+    }
+}
+
+// LayerNorm backward, one wave per row: n = (x - mean) rstd, dn = dy g,
+// dx = rstd (dn - mean(dn) - n mean(dn n)) (+ add)
+__global__ void tr_layernorm_bwd(const float* __restrict__ x, const float* __restrict__ st,
+                                 const float* __restrict__ g, const float* __restrict__ dy, int R, int E,
+                                 const float* __restrict__ add, float* __restrict__ dx) {
+    const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= R) return;
+    const float mean = st[2 * row], rstd = st[2 * row + 1];
+    const float* xr = x + (int64_t)row * E;
+    const float* dr = dy + (int64_t)row * E;
+    float s1 = 0.f, s2 = 0.f;
+    for (int e = lane; e < E; e += 64) {
+        const float n = (xr[e] - mean) * rstd, dn = dr[e] * g[e];
+        s1 += dn;
+        s2 += dn * n;
+    }
+    s1 = wave_sum(s1) / E;
+    s2 = wave_sum(s2) / E;
+    for (int e = lane; e < E; e += 64) {
+        const float n = (xr[e] - mean) * rstd, dn = dr[e] * g[e];
+        const float v = rstd * (dn - s1 - n * s2);
+        const int64_t i = (int64_t)row * E + e;
+        dx[i] = add ? v + add[i] : v;
+    }
+}
+
+// LayerNorm parameter gradients, chunk partials: part[c][0][e] = sum_r dy n, part[c][1][e] = sum_r dy
+__global__ void tr_ln_param_part(const float* __restrict__ x, const float* __restrict__ st,
+                                 const float* __restrict__ dy, int R, int E, float* __restrict__ part) {
+    const int c = blockIdx.x, e = blockIdx.y * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const int r0 = c * kTrRowsPerChunk, r1 = min(R, r0 + kTrRowsPerChunk);
+    float sg = 0.f, sb = 0.f;
+    for (int r = r0; r < r1; ++r) {
+        const float n = (x[(int64_t)r * E + e] - st[2 * r]) * st[2 * r + 1];
+        const float v = dy[(int64_t)r * E + e];
+        sg = fmaf(v, n, sg);
+        sb += v;
+    }
+    part[(int64_t)c * 2 * E + e] = sg;
+    part[(int64_t)c * 2 * E + E + e] = sb;
+}
+
+// attention backward, one wave per (task, query t): D_t = sum_e dO_t O_t,
+// dS[b][t][j] = P[b][t][j] (dO_t . v_j - D_t) for j <= t
+__global__ void tr_attn_bwd_ds(const float* __restrict__ qkv, const float* __restrict__ P,
+                               const float* __restrict__ O, const float* __restrict__ dO, TrDims d,
+                               float* __restrict__ dS) {
+    extern __shared__ float sm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (blockDim.x / 64) + wave;
+    if (row >= d.R()) return;
+    const int E = d.E, T = d.T, b = row / T, t = row % T;
+    float* go = sm + (size_t)wave * E;
+    float dd = 0.f;
+    for (int e = lane; e < E; e += 64) {
+        const float v = dO[(int64_t)row * E + e];
+        go[e] = v;
+        dd = fmaf(v, O[(int64_t)row * E + e], dd);
+    }
+    dd = wave_sum(dd);
+    wave_lds_sync();
+    const float* base = qkv + (int64_t)b * T * 3 * E;
+    const int64_t pr = ((int64_t)b * T + t) * T;
+    for (int j = lane; j <= t; j += 64) {
+        const float* v = base + (int64_t)j * 3 * E + 2 * E;
+        float dp = 0.f;
+        for (int e = 0; e < E; ++e) dp = fmaf(go[e], v[e], dp);
+        dS[pr + j] = P[pr + j] * (dp - dd);
+    }
+}
+
+// dq_t = sum_{j <= t} dS[t][j] k_j / sqrt(E) into dqkv[r][0:E]; thread per (row, e)
+__global__ void tr_attn_bwd_dq(const float* __restrict__ qkv, const float* __restrict__ dS, TrDims d,
+                               float* __restrict__ dqkv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)d.R() * d.E) return;
+    const int E = d.E, T = d.T, row = (int)(i / E), e = (int)(i % E), b = row / T, t = row % T;
+    const float* base = qkv + (int64_t)b * T * 3 * E + E + e;
+    const float* ds = dS + ((int64_t)b * T + t) * T;
+    float acc = 0.f;
+    for (int j = 0; j <= t; ++j) acc = fmaf(ds[j], base[(int64_t)j * 3 * E], acc);
+    dqkv[(int64_t)row * 3 * E + e] = acc / sqrtf((float)E);
+}
+
+// dk_j = sum_{t >= j} dS[t][j] q_t / sqrt(E), dv_j = sum_{t >= j} P[t][j] dO_t into dqkv[r][E:3E]
+__global__ void tr_attn_bwd_dkv(const float* __restrict__ qkv, const float* __restrict__ P,
+                                const float* __restrict__ dS, const float* __restrict__ dO, TrDims d,
+                                float* __restrict__ dqkv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)d.R() * d.E) return;
+    const int E = d.E, T = d.T, row = (int)(i / E), e = (int)(i % E), b = row / T, j = row % T;
+    const float* q = qkv + (int64_t)b * T * 3 * E + e;
+    const float* go = dO + (int64_t)b * T * E + e;
+    const int64_t col = (int64_t)b * T * T + j;
+    float ak = 0.f, av = 0.f;
+    for (int t = j; t < T; ++t) {
+        ak = fmaf(dS[col + (int64_t)t * T], q[(int64_t)t * 3 * E], ak);
+        av = fmaf(P[col + (int64_t)t * T], go[(int64_t)t * E], av);
+    }
+    dqkv[(int64_t)row * 3 * E + E + e] = ak / sqrtf((float)E);
+    dqkv[(int64_t)row * 3 * E + 2 * E + e] = av;
+}
+
+// dwpe[t][e] = sum_b dx[b][t][e]
+__global__ void tr_wpe_grad(const float* __restrict__ dx, TrDims d, float* __restrict__ dwpe) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)d.T * d.E) return;
+    float acc = 0.f;
+    for (int b = 0; b < d.B; ++b) acc += dx[(int64_t)b * d.T * d.E + i];
+    dwpe[i] = acc;
+}
+
+// ------------------------------------------------------------------------------ host side
+
+static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + kTrThreads - 1) / kTrThreads); }
+
+static int launched(const char* what) { return check_hip(hipGetLastError(), what); }
+
+int train_dims_check(const TrDims& d) {
+    if (d.L < 1 || d.E < 1 || d.E > 1024 || d.F < 1 || d.A < 1 || d.B < 1 || d.T < 1 || d.T > d.npos ||
+        (int64_t)d.B * d.T > (1ll << 26)) {
+        set_error(DPT_EINVAL, "train dims: L=%d E=%d F=%d A=%d B=%d T=%d npos=%d", d.L, d.E, d.F, d.A, d.B, d.T,
+                  d.npos);
+        return DPT_EINVAL;
+    }
+    return DPT_OK;
+}
+
+int64_t train_workspace_numel(const TrDims& d) { return TrWs::make(d).total; }
+int64_t train_blob_numel(const TrDims& d) { return TrBlob::make(d).total; }
+
+static int wgrad(const float* X, const float* dY, int R, int IN, int OUT, int gelu, float* part, float* dW,
+                 float* db, hipStream_t st) {
+    const int nch = (R + kTrRowsPerChunk - 1) / kTrRowsPerChunk;
+    hipLaunchKernelGGL(tr_wgrad_part, dim3(nch, blocks_for((int64_t)(IN + 1) * OUT)), dim3(kTrThreads), 0, st, X, dY,
+                       R, IN, OUT, gelu, part);
+    hipLaunchKernelGGL(tr_wgrad_reduce, dim3(blocks_for((int64_t)(IN + 1) * OUT)), dim3(kTrThreads), 0, st, part, nch,
+                       IN, OUT, dW, db);
+    return launched("tr_wgrad");
+}
+
+static int ln_param_grad(const float* x, const float* stt, const float* dy, int R, int E, float* part, float* dg,
+                         float* db, hipStream_t st) {
+    const int nch = (R + kTrRowsPerChunk - 1) / kTrRowsPerChunk;
+    hipLaunchKernelGGL(tr_ln_param_part, dim3(nch, blocks_for(E)), dim3(kTrThreads), 0, st, x, stt, dy, R, E, part);
+    // the (2, E) partials reduce like a bias-only weight gradient: IN = 1, OUT = E, [sum dy n | sum dy]
+    hipLaunchKernelGGL(tr_wgrad_reduce, dim3(blocks_for(2 * E)), dim3(kTrThreads), 0, st, part, nch, 1, E, dg, db);
+    return launched("tr_ln_param");
+}
+
+int train_forward(const TrDims& d, const float* blob, const float* tok, float* ws, float* preds, hipStream_t st) {
+    if (int rc = train_dims_check(d)) return rc;
+    const TrBlob B = TrBlob::make(d);
+    const TrWs W = TrWs::make(d);
+    const int R = d.R(), E = d.E;
+    const int64_t RE = (int64_t)R * E, TT = (int64_t)d.B * d.T * d.T;
+    const int rows_per_block = kTrThreads / 64;
+    const size_t attn_lds = sizeof(float) * rows_per_block * (size_t)(d.T + E);
+    if (attn_lds > 160 * 1024) {
+        set_error(DPT_EUNSUPPORTED, "train forward: window T=%d too long for the attention kernel", d.T);
+        return DPT_EUNSUPPORTED;
+    }
+    if (attn_lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)tr_attn_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)attn_lds);
+    hipLaunchKernelGGL(tr_embed, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, tok, blob, d, B, ws + W.x);
+    for (int l = 0; l < d.L; ++l) {
+        const TrLayer P = TrLayer::make(B.layers + l * d.layer_size(), E);
+        const float* x = ws + W.x + l * RE;
+        float* y1 = ws + W.y1 + l * RE;
+        float* st1 = ws + W.st1 + (int64_t)l * R * 2;
+        float* qkv = ws + W.qkv + l * RE * 3;
+        float* Pm = ws + W.P + l * TT;
+        float* o = ws + W.o + l * RE;
+        float* x2 = ws + W.x2 + l * RE;
+        float* y2 = ws + W.y2 + l * RE;
+        float* st2 = ws + W.st2 + (int64_t)l * R * 2;
+        float* hpre = ws + W.hpre + l * RE * 4;
+        float* xn = ws + W.x + (l + 1) * RE;
+        hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x,
+                           blob + P.ln1_g, blob + P.ln1_b, R, E, y1, st1);
+        hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 3)), dim3(kTrThreads), 0, st, y1, blob + P.attn_w,
+                           blob + P.attn_b, nullptr, R, E, 3 * E, 0, qkv);
+        hipLaunchKernelGGL(tr_attn_fwd, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), attn_lds, st,
+                           qkv, d, Pm, o);
+        hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, o, blob + P.proj_w, blob + P.proj_b,
+                           x, R, E, E, 0, x2);
+        hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x2,
+                           blob + P.ln2_g, blob + P.ln2_b, R, E, y2, st2);
+        hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, y2, blob + P.fc_w,
+                           blob + P.fc_b, nullptr, R, E, 4 * E, 0, hpre);
+        hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, hpre, blob + P.mp_w, blob + P.mp_b,
+                           x2, R, 4 * E, E, 1, xn);
+        if (int rc = launched("train forward layer")) return rc;
+    }
+    hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st,
+                       ws + W.x + d.L * RE, blob + B.lnf_g, blob + B.lnf_b, R, E, ws + W.yf, ws + W.stf);
+    hipLaunchKernelGGL(tr_linear, dim3(blocks_for((int64_t)R * d.A)), dim3(kTrThreads), 0, st, ws + W.yf,
+                       blob + B.head_w, blob + B.head_b, nullptr, R, E, d.A, 0, preds);
+    return launched("train forward head");
+}
+
+int train_backward(const TrDims& d, const float* blob, const float* tok, float* ws, const float* dpreds,
+                   float* dblob, hipStream_t st) {
+    if (int rc = train_dims_check(d)) return rc;
+    const TrBlob B = TrBlob::make(d);
+    const TrWs W = TrWs::make(d);
+    const int R = d.R(), E = d.E;
+    const int64_t RE = (int64_t)R * E, TT = (int64_t)d.B * d.T * d.T;
+    const int rows_per_block = kTrThreads / 64;
+    const unsigned row_blocks = (R + rows_per_block - 1) / rows_per_block;
+    float* part = ws + W.part;
+    float* dx = ws + W.dx;
+    float* dx2 = ws + W.dx2;
+    float* dy = ws + W.dy;
+    if (int rc = check_hip(hipMemsetAsync(dblob, 0, sizeof(float) * B.total, st), "dblob memset")) return rc;
+    // head: preds = yf head_w + head_b
+    if (int rc = wgrad(ws + W.yf, dpreds, R, E, d.A, 0, part, dblob + B.head_w, dblob + B.head_b, st)) return rc;
+    hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dpreds, blob + B.head_w, R, E,
+                       d.A, nullptr, nullptr, dy);
+    // ln_f
+    if (int rc = ln_param_grad(ws + W.x + d.L * RE, ws + W.stf, dy, R, E, part, dblob + B.lnf_g, dblob + B.lnf_b, st))
+        return rc;
+    hipLaunchKernelGGL(tr_layernorm_bwd, dim3(row_blocks), dim3(kTrThreads), 0, st, ws + W.x + d.L * RE, ws + W.stf,
+                       blob + B.lnf_g, dy, R, E, nullptr, dx);
+    const size_t ds_lds = sizeof(float) * rows_per_block * (size_t)E;
+    for (int l = d.L - 1; l >= 0; --l) {
+        const TrLayer P = TrLayer::make(B.layers + l * d.layer_size(), E);
+        const TrLayer G = TrLayer::make(B.layers + l * d.layer_size(), E);  // same offsets in dblob
+        const float* x = ws + W.x + l * RE;
+        const float* y1 = ws + W.y1 + l * RE;
+        const float* st1 = ws + W.st1 + (int64_t)l * R * 2;
+        const float* qkv = ws + W.qkv + l * RE * 3;
+        const float* Pm = ws + W.P + l * TT;
+        const float* o = ws + W.o + l * RE;
+        const float* x2 = ws + W.x2 + l * RE;
+        const float* y2 = ws + W.y2 + l * RE;
+        const float* st2 = ws + W.st2 + (int64_t)l * R * 2;
+        const float* hpre = ws + W.hpre + l * RE * 4;
+        float* dh = ws + W.dh;
+        float* dqkv = ws + W.dqkv;
+        float* dout = ws + W.dout;
+        float* dS = ws + W.dS;
+        // MLP: x_{l+1} = x2 + gelu(hpre) W_mp + b_mp, hpre = y2 W_fc + b_fc
+        if (int rc = wgrad(hpre, dx, R, 4 * E, E, 1, part, dblob + G.mp_w, dblob + G.mp_b, st)) return rc;
+        hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, dx, blob + P.mp_w, R,
+                           4 * E, E, hpre, nullptr, dh);
+        if (int rc = wgrad(y2, dh, R, E, 4 * E, 0, part, dblob + G.fc_w, dblob + G.fc_b, st)) return rc;
+        hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dh, blob + P.fc_w, R, E,
+                           4 * E, nullptr, nullptr, dy);
+        if (int rc = ln_param_grad(x2, st2, dy, R, E, part, dblob + G.ln2_g, dblob + G.ln2_b, st)) return rc;
+        hipLaunchKernelGGL(tr_layernorm_bwd, dim3(row_blocks), dim3(kTrThreads), 0, st, x2, st2, blob + P.ln2_g, dy, R, E,
+                           dx, dx2);
+        // attention: x2 = x + o W_proj + b_proj
+        if (int rc = wgrad(o, dx2, R, E, E, 0, part, dblob + G.proj_w, dblob + G.proj_b, st)) return rc;
+        hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dx2, blob + P.proj_w, R, E,
+                           E, nullptr, nullptr, dout);
+        hipLaunchKernelGGL(tr_attn_bwd_ds, dim3(row_blocks), dim3(kTrThreads), ds_lds, st, qkv, Pm, o, dout, d, dS);
+        hipLaunchKernelGGL(tr_attn_bwd_dq, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, dS, d, dqkv);
+        hipLaunchKernelGGL(tr_attn_bwd_dkv, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, Pm, dS, dout, d, dqkv);
+        if (int rc = wgrad(y1, dqkv, R, E, 3 * E, 0, part, dblob + G.attn_w, dblob + G.attn_b, st)) return rc;
+        hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dqkv, blob + P.attn_w, R, E,
+                           3 * E, nullptr, nullptr, dy);
+        if (int rc = ln_param_grad(x, st1, dy, R, E, part, dblob + G.ln1_g, dblob + G.ln1_b, st)) return rc;
+        hipLaunchKernelGGL(tr_layernorm_bwd, dim3(row_blocks), dim3(kTrThreads), 0, st, x, st1, blob + P.ln1_g, dy, R, E,
+                           dx2, dx);
+        if (int rc = launched("train backward layer")) return rc;
+    }
+    // embedding: x0 = tok emb_w + emb_b + wpe[t]
+    if (int rc = wgrad(tok, dx, R, d.F, E, 0, part, dblob + B.emb_w, dblob + B.emb_b, st)) return rc;
+    hipLaunchKernelGGL(tr_wpe_grad, dim3(blocks_for((int64_t)d.T * E)), dim3(kTrThreads), 0, st, dx, d, dblob + B.wpe);
+    return launched("train backward embed");
+}
+
+}  // namespace dpt

@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DPT_HIP_LIB: another build's file name in this directory (A/B runs of kernel variants)
 LIB_PATH = os.path.join(_HERE, os.environ.get("DPT_HIP_LIB", "libdpt_hip.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 DPT_OK = 0
 DPT_EINVAL = -1
@@ -172,3 +172,16 @@ SIGNATURES["dpt_regret_workspace_numel"] = (_i32, [_i32, _i32, ctypes.POINTER(_i
 SIGNATURES["dpt_regret_moments"] = (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,
                                            _c_void_p, _c_void_p])
 SIGNATURES["dpt_darkroom_workspace_numel"] = (_i32, [_i32, ctypes.POINTER(_i64)])
+
+
+class TrainDesc(ctypes.Structure):
+    _fields_ = [("n_layer", _i32), ("n_embd", _i32), ("state_dim", _i32), ("action_dim", _i32),
+                ("n_positions", _i32), ("batch", _i32), ("window", _i32), ("reserved", _i32)]
+
+
+SIGNATURES["dpt_train_blob_numel"] = (_i32, [ctypes.POINTER(TrainDesc), ctypes.POINTER(_i64)])
+SIGNATURES["dpt_train_workspace_numel"] = (_i32, [ctypes.POINTER(TrainDesc), ctypes.POINTER(_i64)])
+SIGNATURES["dpt_train_forward"] = (_i32, [ctypes.POINTER(TrainDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                          _c_void_p])
+SIGNATURES["dpt_train_backward"] = (_i32, [ctypes.POINTER(TrainDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                           _c_void_p, _c_void_p])

@@ -1,0 +1,126 @@
+"""Training forward / backward through libdpt_hip (dpt_train_forward / dpt_train_backward).
+
+``TransformerFunction`` is the autograd node of ``models.net.Transformer.forward`` when autograd
+needs it (train.py:286-331: ``loss.backward()`` then ``AdamW.step()``) and the forward of models
+whose width the fused kernels are not built for (any ``n_embd``).  The parameters enter in the
+packed blob order of include/dpt_hip.h; the gradients come back in that order and are mapped to
+the reference's parameter shapes (nn.Linear weights are stored [out][in] by torch and [in][out]
+in the blob).  Everything runs on the device; the library owns no memory here (the workspace
+holding the forward's saved activations is a torch tensor kept on the autograd context).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from . import _p, _stream, device
+
+GRAD_BACKWARD = "dpt_train_backward"
+
+
+def param_list(model):
+    """The Transformer's parameters in blob order (pack_weights): embed_transition, wpe, the
+    blocks' [ln_1, c_attn, c_proj, ln_2, c_fc, mlp.c_proj] weight/bias pairs, ln_f, pred_actions."""
+    t = model.transformer
+    ps = [model.embed_transition.weight, model.embed_transition.bias, t.wpe.weight]
+    for blk in t.h:
+        ps += [blk.ln_1.weight, blk.ln_1.bias, blk.attn.c_attn.weight, blk.attn.c_attn.bias,
+               blk.attn.c_proj.weight, blk.attn.c_proj.bias, blk.ln_2.weight, blk.ln_2.bias,
+               blk.mlp.c_fc.weight, blk.mlp.c_fc.bias, blk.mlp.c_proj.weight, blk.mlp.c_proj.bias]
+    ps += [t.ln_f.weight, t.ln_f.bias, model.pred_actions.weight, model.pred_actions.bias]
+    return ps
+
+
+def pack_params(params, dev=None):
+    """Flatten the parameters (blob order) into one fp32 vector on ``dev`` (default: the
+    parameters' own device).  The nn.Linear weights (the first and the second-to-last
+    parameter) are stored [out][in] by torch and [in][out] in the blob."""
+    n = len(params)
+    parts = []
+    for i, p in enumerate(params):
+        v = p.detach()
+        if i in (0, n - 2):
+            v = v.t()
+        parts.append(v.to(device=dev or v.device, dtype=torch.float32).contiguous().reshape(-1))
+    return torch.cat(parts)
+
+
+def _on_device(*tensors):
+    """Every pointer handed to the library must be device memory (a host pointer would fault)."""
+    for t in tensors:
+        if not (isinstance(t, torch.Tensor) and t.is_cuda and t.is_contiguous() and t.dtype == torch.float32):
+            raise ValueError("dpt_hip.train: expected contiguous fp32 device tensors")
+
+
+def unpack_grads(dblob, params):
+    """Split a gradient blob into per-parameter gradients shaped like ``params``."""
+    out, off, n = [], 0, len(params)
+    for i, p in enumerate(params):
+        k = p.numel()
+        g = dblob[off:off + k]
+        off += k
+        if i in (0, n - 2):
+            g = g.reshape(p.shape[1], p.shape[0]).t()
+        out.append(g.reshape(p.shape).to(p.dtype))
+    if off != dblob.numel():
+        raise ValueError(f"gradient blob {dblob.numel()} != parameters {off}")
+    return out
+
+
+def desc(n_layer, n_embd, state_dim, action_dim, n_positions, batch, window):
+    return _lib.TrainDesc(n_layer, n_embd, state_dim, action_dim, n_positions, batch, window, 0)
+
+
+def _numel(fn, d):
+    n = ctypes.c_int64()
+    _lib.call(fn, ctypes.byref(d), ctypes.byref(n))
+    return n.value
+
+
+def forward(d, blob, tokens):
+    """preds (batch, window, A) at every position + the workspace the backward needs."""
+    dev = device()
+    _on_device(blob, tokens)
+    if tokens.shape != (d.batch, d.window, 2 * d.state_dim + d.action_dim + 1):
+        raise ValueError(f"tokens {tuple(tokens.shape)} do not match the description")
+    ws = torch.empty(_numel("dpt_train_workspace_numel", d), dtype=torch.float32, device=dev)
+    preds = torch.empty((d.batch, d.window, d.action_dim), dtype=torch.float32, device=dev)
+    _lib.call("dpt_train_forward", ctypes.byref(d), _p(blob), _p(tokens), _p(ws), _p(preds), _stream())
+    return preds, ws
+
+
+def backward(d, blob, tokens, ws, dpreds):
+    """dL/dblob (packed order) from dL/dpreds (batch, window, A)."""
+    dblob = torch.empty(_numel("dpt_train_blob_numel", d), dtype=torch.float32, device=blob.device)
+    dp = dpreds.to(torch.float32).contiguous()
+    _on_device(blob, tokens, ws, dp)
+    if dp.shape != (d.batch, d.window, d.action_dim):
+        raise ValueError(f"dpreds {tuple(dp.shape)} do not match the description")
+    _lib.call(GRAD_BACKWARD, ctypes.byref(d), _p(blob), _p(tokens), _p(ws), _p(dp), _p(dblob), _stream())
+    return dblob
+
+
+class TransformerFunction(torch.autograd.Function):
+    """preds (B, T, A) = Transformer(tokens) at every position, with the HIP backward."""
+
+    @staticmethod
+    def forward(ctx, tokens, dims, *params):
+        d = desc(*dims)
+        dev = device()
+        blob = pack_params(params, dev)
+        if blob.numel() != _numel("dpt_train_blob_numel", d):
+            raise ValueError("parameter shapes do not match the model description")
+        tok = tokens.to(device=dev, dtype=torch.float32).contiguous()
+        preds, ws = forward(d, blob, tok)
+        if any(ctx.needs_input_grad[2:]):
+            ctx.d, ctx.blob, ctx.tok, ctx.ws = d, blob, tok, ws
+            ctx.params_meta = [(p.shape, p.dtype, p.device) for p in params]
+        return preds
+
+    @staticmethod
+    def backward(ctx, dpreds):
+        dblob = backward(ctx.d, ctx.blob, ctx.tok, ctx.ws, dpreds)
+        shapes = [torch.empty(s, dtype=dt, device="meta") for s, dt, _ in ctx.params_meta]
+        grads = [g.to(dv) for g, (_, _, dv) in zip(unpack_grads(dblob, shapes), ctx.params_meta)]
+        ctx.ws = None  # the saved activations are not needed again
+        return (None, None) + tuple(g if need else None for g, need in zip(grads, ctx.needs_input_grad[2:]))

@@ -45,6 +45,7 @@ def _fused_ok(vec_env, controller, horizon):
     from models.net import Transformer
     return (isinstance(controller, BanditTransformerController) and isinstance(vec_env, BanditEnvVec)
             and isinstance(controller.model, Transformer) and controller.model.state_dim == 1
+            and controller.model.n_embd == dpt_hip.E
             and controller.batch_size == vec_env.num_envs and horizon <= controller.model.n_positions)
 
 

@@ -23,7 +23,8 @@ device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
 def _device_ok(vec_env, controller):
     from models.net import Transformer
     return (isinstance(controller, DarkroomTransformerController) and isinstance(vec_env, DarkroomEnvVec)
-            and isinstance(controller.model, Transformer) and controller.batch_size == vec_env.num_envs)
+            and isinstance(controller.model, Transformer) and controller.model.n_embd == dpt_hip.E
+            and controller.batch_size == vec_env.num_envs)
 
 
 def _episode_device(dm, ctrl, vec_env, ctx, horizon):

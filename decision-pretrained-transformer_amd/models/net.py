@@ -132,19 +132,46 @@ class Transformer(nn.Module):
             self._dev_sig = sig
         return self._dev_model
 
+    def _tokens(self, x):
+        """The packed sequences of models/net.py:42-54: [query | 0_A | 0_sd | 0] then the context
+        transitions [s, a, s', r] -> (B, T, 2 sd + A + 1) fp32 on the device."""
+        dev = dpt_hip.device()
+        q = x["query_states"].to(dev, torch.float32)
+        B = q.shape[0]
+        first = torch.cat([q, torch.zeros((B, self.action_dim + self.state_dim + 1), device=dev)], dim=1)[:, None]
+        cs = x.get("context_states")
+        if cs is None or cs.shape[1] == 0:
+            return first.contiguous()
+        C = cs.shape[1]
+        ctx = torch.cat([cs.to(dev, torch.float32), x["context_actions"].to(dev, torch.float32),
+                         x["context_next_states"].to(dev, torch.float32),
+                         x["context_rewards"].to(dev, torch.float32).reshape(B, C, 1)], dim=2)
+        return torch.cat([first, ctx], dim=1).contiguous()
+
+    def _forward_generic(self, x):
+        """The generic-width path (dpt_hip.train): preds at every position from
+        dpt_train_forward, differentiable through dpt_train_backward (the HIP backward of the
+        whole model).  Used when autograd needs the graph and for widths other than 32."""
+        from dpt_hip import train as tr
+        tok = self._tokens(x)
+        dims = (self.n_layer, self.n_embd, self.state_dim, self.action_dim, self.n_positions, tok.shape[0],
+                tok.shape[1])
+        preds = tr.TransformerFunction.apply(tok, dims, *tr.param_list(self))
+        return preds[:, -1, :] if self.test else preds[:, 1:, :]
+
     def forward(self, x):
         """models/net.py:41-60: pack [query | context] -> embed -> GPT-2 -> head;
-        last position (test) or positions 1.. (train).  Inference only: the kernels build
-        no autograd graph, so a forward that autograd would differentiate (training mode,
-        grad enabled, trainable parameters: train.py:286-331) raises instead of returning
-        logits whose ``loss.backward()`` fails later with a generic autograd error.  The
-        reference's inference call sites work unchanged: eval.py:152 calls ``model.eval()``
-        and train.py:265-278 computes its test loss under ``torch.no_grad()``."""
-        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                "Transformer.forward with autograd: the backward pass (train.py:286-331, CE over "
-                "preds[:, 1:]) is not built in this MI355X hot-path package; run inference under "
-                "model.eval() or torch.no_grad()")
+        last position (test) or positions 1.. (train).
+
+        When autograd would differentiate the call (training mode, grad enabled, trainable
+        parameters: train.py:286-331) the forward and backward run through the HIP training
+        kernels (dpt_hip.train.TransformerFunction): ``loss.backward()`` fills every
+        parameter's ``.grad`` and the reference's AdamW step works unchanged.  Inference
+        (eval.py:152 ``model.eval()``; train.py:265-278's test loss under ``torch.no_grad()``)
+        takes the fused kernels at width 32 and the generic kernels at other widths."""
+        if (self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())) \
+                or self.n_embd != dpt_hip.E:
+            return self._forward_generic(x)
         dm = self.device_model()
         query = x["query_states"]
         cs = x.get("context_states")

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 4
+#define DPT_ABI_VERSION 5
 
 /* error codes (mapped to the reference's Python exceptions by dpt_hip/_lib.py) */
 #define DPT_OK 0
@@ -358,6 +358,29 @@ int dpt_regret_max_steps(int32_t* steps_out_host);
 int dpt_regret_workspace_numel(int32_t N, int32_t H, int64_t* numel_out_host);
 int dpt_regret_moments(const double* arm_value, const double* opt, int32_t N, int32_t H, int32_t mode,
                        const double* mean, double* workspace, double* out, void* stream);
+
+/* ------------------------------------------------------------------ training
+ * Replaces the autograd of Transformer.forward with test=False (models/net.py:41-60: preds at
+ * positions 1..T-1) inside train.py:286-331 (CrossEntropyLoss(sum) over preds[:, 1:], AdamW).
+ * Any n_embd (FF = 4 n_embd, one head as net.py:29 forces), fp32.  The weights are a packed
+ * blob in the dpt_weights_numel layout with this desc's width (dpt_train_blob_numel floats);
+ * tokens (batch, window, 2 sd + A + 1) are the packed sequences of net.py:42-54.
+ * dpt_train_forward writes preds (batch, window, A) at EVERY position (position 0 included) and
+ * keeps in `workspace` what the backward needs; dpt_train_backward takes dL/dpreds (batch,
+ * window, A) -- zero at positions the loss does not use -- and writes every parameter's
+ * gradient into dblob (same layout; wpe rows >= window are zero).  Reductions over the
+ * batch * window rows run in a fixed order: the gradients are deterministic.               */
+typedef struct dpt_train_desc {
+    int32_t n_layer, n_embd, state_dim, action_dim, n_positions;
+    int32_t batch, window;        /* sequences and tokens per sequence (1 + context length) */
+    int32_t reserved;
+} dpt_train_desc;
+int dpt_train_blob_numel(const dpt_train_desc* desc_host, int64_t* numel_out_host);
+int dpt_train_workspace_numel(const dpt_train_desc* desc_host, int64_t* numel_out_host);
+int dpt_train_forward(const dpt_train_desc* desc_host, const float* blob, const float* tokens, float* workspace,
+                      float* preds, void* stream);
+int dpt_train_backward(const dpt_train_desc* desc_host, const float* blob, const float* tokens, float* workspace,
+                       const float* dpreds, float* dblob, void* stream);
 
 #ifdef __cplusplus
 }

@@ -471,6 +471,64 @@ def darkroom_offline():
     print("darkroom offline")
 
 
+def train_grads():
+    """train.py:286-331 on the reference model: preds = model(batch) with test=False
+    (models/net.py:56-60, positions 1..T-1), CrossEntropyLoss(reduction='sum') against the optimal
+    action repeated over the positions, loss.backward().  Recorded: loss, preds and every
+    parameter's gradient, in fp32 (the reference as it runs) and with the same model in float64
+    (the truth the fp32 results are measured against).  Two models: DarkRoom (sd 2, A 5) with a
+    30-transition context, and the 5-arm bandit one with 20."""
+    import numpy as np
+    import torch
+    out = {}
+    for name, C, B in (("darkroom", 30, 4), ("bandit5", 20, 3)):
+        rs = np.random.RandomState(300 + C)
+        model = fixture_transformer(name)
+        sd_, ad = model.config["state_dim"], model.config["action_dim"]
+        if name == "darkroom":
+            batch = {"query_states": rs.randint(0, 10, (B, sd_)), "context_states": rs.randint(0, 10, (B, C, sd_)),
+                     "context_actions": np.eye(ad)[rs.randint(0, ad, (B, C))],
+                     "context_next_states": rs.randint(0, 10, (B, C, sd_)),
+                     "context_rewards": (rs.uniform(size=(B, C, 1)) < 0.2)}
+        else:
+            batch = {"query_states": np.ones((B, 1)), "context_states": np.ones((B, C, 1)),
+                     "context_actions": np.eye(ad)[rs.randint(0, ad, (B, C))],
+                     "context_next_states": np.ones((B, C, 1)), "context_rewards": rs.normal(0.5, 0.5, (B, C, 1))}
+        batch = {k: np.asarray(v, np.float64) for k, v in batch.items()}
+        batch["zeros"] = np.zeros((B, sd_ ** 2 + ad + 1))
+        opt = np.eye(ad)[rs.randint(0, ad, B)]
+        for k, v in batch.items():
+            out[f"{name}/{k}"] = v
+        out[f"{name}/optimal_actions"] = opt
+        for tag, dt in (("f32", torch.float32), ("f64", torch.float64)):
+            m = model.to(dt)
+            m.test = False
+            m.train()
+            m.zero_grad()
+            tb = {k: torch.tensor(v, dtype=dt) for k, v in batch.items()}
+            pred = m(tb)                                             # train.py:302
+            true = torch.tensor(opt, dtype=dt).unsqueeze(1).repeat(1, pred.shape[1], 1)
+            loss = torch.nn.CrossEntropyLoss(reduction="sum")(pred.reshape(-1, ad), true.reshape(-1, ad))
+            loss.backward()                                          # train.py:309
+            out[f"{name}/{tag}/loss"] = np.float64(loss.item())
+            out[f"{name}/{tag}/preds"] = pred.detach().numpy()
+            for k, p in m.named_parameters():
+                if p.grad is not None and not k.endswith("wte.weight"):
+                    gv = p.grad.detach().numpy()
+                    if k.endswith("wpe.weight"):  # rows >= T get no gradient: keep the first T
+                        assert not gv[C + 1:].any()
+                        gv = gv[:C + 1]
+                    out[f"{name}/{tag}/grad/{k}"] = gv
+        # keep the float64 gradients; of the fp32 run only its error against them (per parameter,
+        # relative to the largest float64 entry), the scale a fp32 implementation is held to
+        for k in [k for k in out if k.startswith(f"{name}/f32/grad/")]:
+            ref = out[k.replace("/f32/", "/f64/")]
+            out[k.replace("/grad/", "/grad_err/")] = np.float64(np.abs(out.pop(k) - ref).max() / np.abs(ref).max())
+        model.float()
+    np.savez_compressed(os.path.join(OUT, "train_grads.npz"), **out)
+    print("train grads")
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit("reference checkout not present; fixtures are committed")

@@ -229,3 +229,25 @@ def test_c_darkroom_oracle_matches_reference(tag):
         assert np.abs(o["logits"] - g["logits"]).max() <= 1e-5
         assert np.array_equal(o["returns"], g["returns"])
     assert np.array_equal(outs[0]["actions"], outs[1]["actions"])
+
+
+@pytest.mark.parametrize("name", ["darkroom", "bandit5"])
+def test_torch_oracle_gradients_match_reference(name):
+    """oracle/dpt_oracle_torch.py (float64 autograd of the restated forward, the checker of the
+    HIP training kernels) against the gradients recorded from the reference's train.py loss."""
+    from oracle import dpt_oracle_torch as OT
+    g = golden("train_grads.npz")
+    fw = golden(f"forward_{name}.npz")
+    H, sd, A, L, _ = (int(x) for x in fw["cfg"])
+    w = {k[2:]: v for k, v in fw.items() if k.startswith("w/")}
+    batch = {k: g[f"{name}/{k}"] for k in ("query_states", "context_states", "context_actions",
+                                           "context_next_states", "context_rewards", "optimal_actions")}
+    loss, preds, gr = OT.grads(w, batch, L, sd, A)
+    assert abs(loss - float(g[f"{name}/f64/loss"])) <= 1e-10 * abs(loss)
+    assert np.abs(preds - g[f"{name}/f64/preds"]).max() <= 1e-12
+    for k, v in gr.items():
+        ref = g[f"{name}/f64/grad/{k}"]
+        got = v[:ref.shape[0]] if k.endswith("wpe.weight") else v
+        if k.endswith("wpe.weight"):
+            assert not v[ref.shape[0]:].any()
+        assert np.abs(got - ref).max() <= 1e-10 * max(1e-30, np.abs(ref).max()), k
