@@ -414,7 +414,7 @@ int dpt_rollout_policy(const dpt_policy_rollout_args* a, void* stream) {
     REQUIRE(a->policy >= DPT_POLICY_OPT && a->policy <= DPT_POLICY_LINUCB, "policy=%d", a->policy);
     REQUIRE(a->policy == DPT_POLICY_OPT || a->policy == DPT_POLICY_LINUCB || a->workspace,
             "policy %d needs the per-arm workspace", a->policy);
-    REQUIRE(a->policy != DPT_POLICY_LINUCB || (a->arms && a->lin_d >= 1 && a->lin_d <= 2), "LinUCB needs arms, d<=2");
+    REQUIRE(a->policy != DPT_POLICY_LINUCB || (a->arms && a->lin_d >= 1 && a->lin_d <= 8), "LinUCB needs arms, d<=8");
     if (a->type != DPT_BANDIT_GAUSSIAN && a->type != DPT_BANDIT_BERNOULLI) {
         set_error(DPT_EUNSUPPORTED, "bandit type %d", a->type);
         return DPT_EUNSUPPORTED;

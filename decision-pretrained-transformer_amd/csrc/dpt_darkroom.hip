@@ -302,8 +302,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b), u_proj3_n<NB>(P, split0, xn, q, M),
-                           kv_from_y<NB>(S.kv, qb, xn, M)));
+            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
+                           u_proj_kv3_n<NB>(P, split0, xn, q, S.kv, qb, M)));
             if (p.ws) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -496,7 +496,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     float xn[2][8];
                     if (!last) {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       u_proj3_n<NB>(W, split0.layer(layer), xn, q, M), kv_from_y<NB>(S.kv, qb, xn, M)));
+                                       u_proj_kv3_n<NB>(W, split0.layer(layer), xn, q, S.kv, qb, M)));
                     } else {
                         // the last layer needs q only for token T-1 (block qlast)
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(S.kv, qb, xn, M)));

@@ -271,15 +271,13 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
 }
 
 // u = xn G + g0 of the NB blocks (the folded c_attn: only its q part) on fp16 two-part
-// products (mfma_x3) at scale 2^(attn_ew + attn_ey), scaled back exactly
+// products (mfma_x3) at scale 2^(attn_ew + attn_ey), scaled back exactly; xs = the blocks'
+// LayerNorm outputs split at 2^attn_ey
 template <int NB>
-__device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8],
+__device__ inline void u_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&xs)[2], float (&q)[2][8],
                                  const ModelView& M) {
     const int g = lane_id() >> 4;
     const float up = exp2i(M.attn_ew + M.attn_ey), down = exp2i(-(M.attn_ew + M.attn_ey));
-    Split2 xs[2];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
         const Split2 w = f3.ld2(Frag3::attn + ob);
@@ -291,6 +289,14 @@ __device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float
             for (int r = 0; r < 4; ++r) q[j][ob * 4 + r] = acc[r];
         }
     }
+}
+template <int NB>
+__device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8],
+                                 const ModelView& M) {
+    Split2 xs[2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
+    u_proj3_s<NB>(W, f3, xs, q, M);
 }
 
 // attn_proj on mfma_x3: x^T += Wvp^T o^T + bvp (o, a convex combination of the values y,
@@ -318,17 +324,18 @@ __device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const floa
 
 // Folded attention input of the NB blocks qb[]: keys and values are the
 // LayerNorm output y itself (K <- y token-major, Vt <- y feature-major, the
-// C-layout of xn is the layout c_attn's K / V tiles had).
+// C-layout of xn is the layout c_attn's K / V tiles had).  With split keys the
+// split of y at 2^attn_ey (xs, the lane's 8 values are its A-operand k-elements) is
+// what goes to LDS.
 template <int NB, class KV>
-__device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2][8], const ModelView& M) {
+__device__ inline void kv_store(KV& S, const int (&qb)[2], const float (&xn)[2][8], const Split2 (&xs)[2]) {
     const int lane = lane_id(), g = lane >> 4;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const int tok = qb[j] * 16 + (lane & 15);
-        if constexpr (KV::kSplitK) {  // the lane's 8 values are its A-operand k-elements
-            const Split2 kt = split2(xn[j], exp2i(M.attn_ey));
-            S.KS[qb[j]][0][lane] = kt.h;
-            S.KS[qb[j]][1][lane] = kt.m;
+        if constexpr (KV::kSplitK) {
+            S.KS[qb[j]][0][lane] = xs[j].h;
+            S.KS[qb[j]][1][lane] = xs[j].m;
             if constexpr (KV::kSplitV) {
                 // the same split parts, scattered into V^T's pair-tile order: value k of
                 // lane (g, c) is feature 16 (k >> 2) + 4g + (k & 3) of token 16 b + c
@@ -337,8 +344,8 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const int off = ((k >> 2) * 2 * 64 + (c >> 2) * 16 + 4 * g + (k & 3)) * 8 + (b & 1) * 4 + (c & 3);
-                    vs[off] = kt.h[k];
-                    vs[off + 64 * 8] = kt.m[k];
+                    vs[off] = xs[j].h[k];
+                    vs[off + 64 * 8] = xs[j].m[k];
                 }
             }
         }
@@ -352,6 +359,26 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
                 for (int r = 0; r < 4; ++r) S.Vt[16 * blk + 4 * g + r][tok] = xn[j][4 * blk + r];
         }
     }
+}
+template <int NB, class KV>
+__device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2][8], const ModelView& M) {
+    Split2 xs[2];
+    if constexpr (KV::kSplitK) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
+    }
+    kv_store<NB>(S, qb, xn, xs);
+}
+// both of the above from one split of xn (the u projection's B operand and the keys / values
+// are the same LayerNorm output at the same scale)
+template <int NB, class KV>
+__device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8],
+                                    KV& S, const int (&qb)[2], const ModelView& M) {
+    Split2 xs[2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
+    u_proj3_s<NB>(W, f3, xs, q, M);
+    kv_store<NB>(S, qb, xn, xs);
 }
 
 // Causal flash attention of query block qb over keys [key_lo, 16*qb + c]:

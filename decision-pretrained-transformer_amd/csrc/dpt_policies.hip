@@ -64,6 +64,8 @@ __device__ double pw_sum(const double* x, size_t stride, int n) {
     return lvl2(x, a) + lvl2(x + (size_t)a * stride, n - a);
 }
 
+constexpr int kMaxD = 8;  // LinUCB feature dimension (lin_d) supported
+
 struct PolicyParams {
     int N, H, A, policy, online, type, sample, d, C, step0;
     const int32_t* ctx_actions;
@@ -89,8 +91,10 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
     const double* mrow = P.means + (size_t)i * A;
     int cnt[kMaxA];
     for (int k = 0; k < A; ++k) cnt[k] = 0;
-    // LinUCB running design: X^T X (d x d, d <= 2) and X^T r
-    double xtx[4] = {0, 0, 0, 0}, xtr[2] = {0, 0};
+    // LinUCB running design: X^T X (d x d, d <= kMaxD, row-major) and X^T r
+    double xtx[kMaxD * kMaxD], xtr[kMaxD];
+    for (int k = 0; k < kMaxD * kMaxD; ++k) xtx[k] = 0.0;
+    for (int k = 0; k < kMaxD; ++k) xtr[k] = 0.0;
     int opt = 0;
     for (int k = 1; k < A; ++k)
         if (mrow[k] > mrow[opt]) opt = k;
@@ -100,9 +104,11 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
         if (P.lists) P.lists[a * lstride + (size_t)cnt[a] * P.N + i] = r;
         ++cnt[a];
         if (P.policy == DPT_POLICY_LINUCB) {
-            const double x0 = P.arms[a * P.d], x1 = P.d > 1 ? P.arms[a * P.d + 1] : 0.0;
-            xtx[0] += x0 * x0; xtx[1] += x0 * x1; xtx[3] += x1 * x1;
-            xtr[0] += x0 * r; xtr[1] += x1 * r;
+            const double* x = P.arms + (size_t)a * P.d;
+            for (int p = 0; p < P.d; ++p) {
+                xtr[p] += x[p] * r;
+                for (int q = 0; q < P.d; ++q) xtx[p * kMaxD + q] += x[p] * x[q];
+            }
         }
     };
     for (int c = 0; c < P.C; ++c)  // prefix context (set_batch_numpy_vec), time order
@@ -116,8 +122,8 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
                 const double u = P.policy_noise ? P.policy_noise[(size_t)i]
                                                 : philox_uniform(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_POLICY);
                 a = min((int)(u * A), A - 1);
-            } else {
-                const double c00 = 1.0 + xtx[0], c01 = xtx[1], c11 = 1.0 + xtx[3];
+            } else if (P.d <= 2) {  // closed-form 2 x 2 inverse
+                const double c00 = 1.0 + xtx[0], c01 = xtx[1], c11 = 1.0 + xtx[kMaxD + 1];
                 const double det = c00 * c11 - c01 * c01;
                 const double i00 = c11 / det, i01 = -c01 / det, i11 = c00 / det;
                 const double t0 = i00 * xtr[0] + i01 * xtr[1], t1 = i01 * xtr[0] + i11 * xtr[1];
@@ -126,6 +132,52 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
                     const double x0 = P.arms[k * P.d], x1 = P.d > 1 ? P.arms[k * P.d + 1] : 0.0;
                     const double q = x0 * (i00 * x0 + i01 * x1) + x1 * (i01 * x0 + i11 * x1);
                     const double v = (t0 * x0 + t1 * x1) + P.c * sqrt(q);
+                    if (v > best) { best = v; a = k; }
+                }
+            } else {
+                // cov_inv = inv(I + X^T X) by Gauss-Jordan (cov is symmetric positive definite, so no
+                // pivoting), theta = cov_inv X^T r, value = theta . x + c sqrt(x cov_inv x)
+                // (ctrls/ctrl_bandit.py:505-522; LAPACK's inverse rounds differently: equal up to
+                // near-ties of the arm values)
+                const int d = P.d;
+                double m[kMaxD * kMaxD], inv[kMaxD * kMaxD];
+                for (int p = 0; p < d; ++p)
+                    for (int q = 0; q < d; ++q) {
+                        m[p * kMaxD + q] = xtx[p * kMaxD + q] + (p == q ? 1.0 : 0.0);
+                        inv[p * kMaxD + q] = p == q ? 1.0 : 0.0;
+                    }
+                for (int c = 0; c < d; ++c) {
+                    const double piv = 1.0 / m[c * kMaxD + c];
+                    for (int q = 0; q < d; ++q) {
+                        m[c * kMaxD + q] *= piv;
+                        inv[c * kMaxD + q] *= piv;
+                    }
+                    for (int p = 0; p < d; ++p) {
+                        if (p == c) continue;
+                        const double f = m[p * kMaxD + c];
+                        for (int q = 0; q < d; ++q) {
+                            m[p * kMaxD + q] -= f * m[c * kMaxD + q];
+                            inv[p * kMaxD + q] -= f * inv[c * kMaxD + q];
+                        }
+                    }
+                }
+                double theta[kMaxD];
+                for (int p = 0; p < d; ++p) {
+                    double t = 0.0;
+                    for (int q = 0; q < d; ++q) t += inv[p * kMaxD + q] * xtr[q];
+                    theta[p] = t;
+                }
+                double best = -INFINITY;
+                for (int k = 0; k < A; ++k) {
+                    const double* x = P.arms + (size_t)k * d;
+                    double tv = 0.0, qv = 0.0;
+                    for (int p = 0; p < d; ++p) {
+                        tv += theta[p] * x[p];
+                        double s = 0.0;
+                        for (int q = 0; q < d; ++q) s += inv[p * kMaxD + q] * x[q];
+                        qv += x[p] * s;
+                    }
+                    const double v = tv + P.c * sqrt(qv);
                     if (v > best) { best = v; a = k; }
                 }
             }

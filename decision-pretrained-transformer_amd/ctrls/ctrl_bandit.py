@@ -234,7 +234,7 @@ class ThompsonSamplingPolicy(_KernelPolicy):
 
 
 class LinUCBPolicy(_KernelPolicy):
-    """LinUCB over fixed arm features (ctrls/ctrl_bandit.py:447-528); lin_d <= 2."""
+    """LinUCB over fixed arm features (ctrls/ctrl_bandit.py:447-528); lin_d <= 8."""
 
     policy = dpt_hip.POLICY_LINUCB
 

@@ -264,7 +264,7 @@ int dpt_rollout_bandit(const dpt_model* model, const dpt_bandit_rollout_args* ar
  *   DPT_POLICY_UCB      UCBPolicy(c)         :318-380
  *   DPT_POLICY_THOMPSON ThompsonSampling     :122-251 (std, prior_mean, prior_var; sample 0 = 100-draw vote)
  *   DPT_POLICY_LCB      PessMeanPolicy(c)    :255-314
- *   DPT_POLICY_LINUCB   LinUCBPolicy(c)      :447-528 (arms (A, lin_d), lin_d <= 2)
+ *   DPT_POLICY_LINUCB   LinUCBPolicy(c)      :447-528 (arms (A, lin_d), lin_d <= 8)
  * Per-arm statistics are recomputed each step from the per-arm reward lists in
  * numpy's fp64 pairwise-summation order, as the reference does, so action
  * indices match it bit for bit given the same draws.  policy_noise: Thompson

@@ -86,8 +86,11 @@ if __name__ == "__main__":
     chk = {}
     for rnd in range(int(os.environ.get("AB_ROUNDS", "2"))):
         for lib in sys.argv[1:]:
-            out = subprocess.run([sys.executable, __file__, "--child", lib], check=True, capture_output=True,
-                                 text=True, timeout=300).stdout.strip().splitlines()[-1]
+            cp = subprocess.run([sys.executable, __file__, "--child", lib], capture_output=True, text=True,
+                                timeout=300)
+            if cp.returncode:
+                sys.exit(f"{lib}: child failed ({cp.returncode})\n{cp.stderr[-3000:]}")
+            out = cp.stdout.strip().splitlines()[-1]
             d = json.loads(out)
             res[lib] += d["ms"]
             chk[lib] = (d["checksum"], d.get("digest"))

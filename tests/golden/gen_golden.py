@@ -529,6 +529,30 @@ def train_grads():
     print("train grads")
 
 
+def linucb_d4():
+    """LinUCB (ctrls/ctrl_bandit.py:447-528) on 12-arm linear bandits with lin_d = 4 (the --lin_d
+    flag, common_args.py:15-16), through eval_linear_bandit.deploy_online_vec with every draw
+    recorded (the random first arm, the reward normals)."""
+    import numpy as np
+    from envs import bandit_env
+    from ctrls import ctrl_bandit as cb
+    from evals import eval_linear_bandit
+    N, H, A, d, var = 64, 20, 12, 4, 0.3
+    arms = np.random.RandomState(1234).normal(size=(A, d)) / np.sqrt(d)   # collect_data.py:230-231
+    thetas = np.random.RandomState(17).normal(0, 1, (N, d)) / np.sqrt(d)
+    envs = [bandit_env.LinearBanditEnv(t, arms, H, var=var) for t in thetas]
+    vec = bandit_env.BanditEnvVec(envs)
+    np.random.seed(19)
+    with DrawRecorder(np) as rec:
+        cm, meta = eval_linear_bandit.deploy_online_vec(vec, cb.LinUCBPolicy(envs[0], const=1.0, batch_size=N), H,
+                                                        include_meta=True)
+    np.savez_compressed(os.path.join(OUT, "linucb_d4.npz"), means=np.stack([e.means for e in envs]), arms=arms,
+                        theta=thetas,
+                        cum_means=cm, actions=meta["context_actions"].argmax(-1), g=np.array(rec.g).reshape(H, N),
+                        first_action=np.asarray(rec.plain[0]))
+    print("LinUCB d=4")
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit("reference checkout not present; fixtures are committed")

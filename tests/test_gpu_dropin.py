@@ -202,6 +202,34 @@ def test_baseline_offline_prefix_and_linucb():
     assert np.array_equal(acts[:, 0], g["lin/first_action"])
 
 
+def test_linucb_d4_kernel_and_drop_in():
+    """LinUCB at lin_d = 4 (Gauss-Jordan inverse in the kernel, LAPACK's np.linalg.inv in the
+    reference): the first (random) arm exactly, the later arms equal up to near-ties of the arm
+    values (>= 99 % of the decisions, as at lin_d = 2), through the kernel and through
+    eval_linear_bandit.deploy_online_vec with the reference's draws injected."""
+    import dpt_hip
+    from ctrls.ctrl_bandit import LinUCBPolicy
+    from envs.bandit_env import BanditEnvVec, LinearBanditEnv
+    from evals import eval_linear_bandit
+    g = golden("linucb_d4.npz")
+    A = g["arms"].shape[0]
+    H = g["g"].shape[0]
+    u = (g["first_action"] + 0.5) / A
+    out = dpt_hip.rollout_policy(dpt_hip.POLICY_LINUCB, g["means"], H, 0.3, c=1.0, arms=g["arms"], noise=g["g"],
+                                 policy_noise=u)
+    acts = out["actions"].cpu().numpy()
+    assert np.array_equal(acts[:, 0], g["first_action"])
+    assert (acts == g["actions"]).mean() >= 0.99
+    envs = [LinearBanditEnv(t, g["arms"], H, var=0.3) for t in g["theta"]]
+    assert np.array_equal(np.stack([e.means for e in envs]), g["means"])
+    vec = BanditEnvVec(envs)
+    ctrl = LinUCBPolicy(envs[0], const=1.0, batch_size=len(envs))
+    pn = np.zeros((H, len(envs)))
+    pn[0] = u
+    cm, meta = eval_linear_bandit.deploy_online_vec(vec, ctrl, H, include_meta=True, noise=g["g"], policy_noise=pn)
+    assert (meta["context_actions"].argmax(-1) == g["actions"]).mean() >= 0.99
+
+
 def test_online_and_offline_eval_run():
     import matplotlib
     matplotlib.use("Agg")

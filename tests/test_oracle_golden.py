@@ -251,3 +251,13 @@ def test_torch_oracle_gradients_match_reference(name):
         if k.endswith("wpe.weight"):
             assert not v[ref.shape[0]:].any()
         assert np.abs(got - ref).max() <= 1e-10 * max(1e-30, np.abs(ref).max()), k
+
+
+def test_linucb_d4_matches_reference():
+    """LinUCB with lin_d = 4 (np.linalg.inv in the oracle, as in the reference)."""
+    g = golden("linucb_d4.npz")
+    H = g["g"].shape[0]
+    out = O.bandit_policy_rollout("linucb", g["means"], H, 0.3, g["g"], c=1.0, arms=g["arms"],
+                                  first_u_idx=g["first_action"])
+    assert np.array_equal(out["actions"], g["actions"])
+    assert np.array_equal(out["cum_means"], g["cum_means"])
