@@ -5,8 +5,8 @@
 // The query (current state) changes every step, so each step is a full causal
 // forward over the window [query, context transitions...] (models/net.py:41-60);
 // the prediction is the LAST position.  That is matrix-core work: one workgroup
-// owns one task for all Heps x horizon steps, and each wave owns 16 tokens of
-// the window (T <= 128).
+// owns one task for all Heps x horizon steps, and each wave owns two 16-token
+// blocks of the window (4 waves for T <= 128, 8 waves for T <= 256: DrGeom).
 //
 // Dataflow is transposed (features x tokens): a wave keeps x^T of its 16
 // tokens in registers as MFMA 16x16x4 C-layout fragments -- lane (g = l>>4,
@@ -78,12 +78,21 @@ struct PTop {
     }
 };
 
+// Window geometry of the kernel built with NW waves: 2 NW blocks of 16 tokens (NW = 4: windows
+// of up to 128 tokens, two workgroups per CU; NW = 8: up to 256, one per CU).
+template <int NW>
+struct DrGeom {
+    static constexpr int kWaves = NW, kBlk = 2 * NW, kT = 16 * kBlk;
+    static constexpr int kWsPerTask = 3 * kBlk * 64 * 8;  // [x | u | layer-0 partial o] per task
+};
+
 // 16-B multiple: the dynamic parameter block P follows it and is read with 16-B loads.
 // kWs (a per-task workspace is given): the layer-0 partials live in the workspace and
 // the freed LDS holds the values as split pair tiles (P V on mfma_x3);
 // without one they stay here and the values are fp32.
-template <bool kWs>
+template <bool kWs, int NW>
 struct alignas(16) DrSmem {
+    static constexpr int kFwdT = DrGeom<NW>::kT, kFwdBlocks = DrGeom<NW>::kBlk;
     KVBuf<kFwdT, kSplitKeys, kSplitKeys && kWs> kv;
     int2 ctx[kFwdT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
     int2 cur[kFwdT];   // this episode's transitions
@@ -133,12 +142,15 @@ struct DarkroomParams {
 // re-projecting; only the query token (position 0) is recomputed.  Layout per task:
 // [x | u | o][block][lane][8] fp32, each lane's 8 C-layout values contiguous (2 x 16 B);
 // o is the layer-0 episode partial (the prologue's attention over keys 1..t).
-// The workspace starts with the per-state table (kDrTab floats), then the task caches.
-constexpr int kDrWsPerTask = 3 * kFwdBlocks * 64 * 8;  // [x | u | layer-0 partial o]
+// The workspace starts with the per-state table (kDrTab floats), then the task caches (sized
+// for the largest geometry, dpt_darkroom_workspace_numel; a launch uses its own stride).
 constexpr int kDrTabPerState = 2 * 4 * 8;
 constexpr int kDrTab = kMemoStates * kDrTabPerState;
+constexpr int kDrMaxWaves = 8;
+template <int NW>
 __device__ inline float* l0_cache(const DarkroomParams& p, int task, int which, int blk) {
-    return p.ws + kDrTab + (size_t)task * kDrWsPerTask + ((size_t)(which * kFwdBlocks + blk) * 64 + lane_id()) * 8;
+    return p.ws + kDrTab + (size_t)task * DrGeom<NW>::kWsPerTask +
+           ((size_t)(which * DrGeom<NW>::kBlk + blk) * 64 + lane_id()) * 8;
 }
 __device__ inline void ws_store(float* d, const float (&v)[8]) {
     *reinterpret_cast<floatx4*>(d) = floatx4{v[0], v[1], v[2], v[3]};
@@ -231,10 +243,10 @@ __global__ void __launch_bounds__(64) state_tables_kernel(ModelView M, int dim, 
     }
 }
 
-template <bool kWs>
-__global__ void __launch_bounds__(kFwdWaves * 64, 2)
+template <bool kWs, int NW>
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1)
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
-    __shared__ DrSmem<kWs> S;
+    __shared__ DrSmem<kWs, NW> S;
     constexpr bool kSplitV = decltype(S.kv)::kSplitV;
     extern __shared__ float P[];
     const int task = blockIdx.x;
@@ -308,8 +320,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     if (j >= nb) break;
-                    ws_store(l0_cache(p, task, 0, qb[j]), x[j]);
-                    ws_store(l0_cache(p, task, 1, qb[j]), q[j]);
+                    ws_store(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
+                    ws_store(l0_cache<NW>(p, task, 1, qb[j]), q[j]);
                 }
             }
             bar_lds();
@@ -320,7 +332,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 attend(S.kv, q[j], qb[j], 1, scale, m, l, o, M);
                 const int lane = lane_id();
                 if constexpr (kWs) {
-                    ws_store(l0_cache(p, task, 2, qb[j]), o);
+                    ws_store(l0_cache<NW>(p, task, 2, qb[j]), o);
                 } else {
                     *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][0]) = {o[0], o[1], o[2], o[3]};
                     *reinterpret_cast<floatx4*>(&S.l0o[qb[j]][lane][4]) = {o[4], o[5], o[6], o[7]};
@@ -402,11 +414,11 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     if (j >= nb) break;
-                    ws_load(l0_cache(p, task, 1, qb[j]), q[j]);
+                    ws_load(l0_cache<NW>(p, task, 1, qb[j]), q[j]);
                     if (qb[j] == 0 && !p.tab) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
                     else
                         ws_load(qb[j] == 0 && col0 ? p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 8 * (lane_id() >> 4)
-                                                   : l0_cache(p, task, 0, qb[j]),
+                                                   : l0_cache<NW>(p, task, 0, qb[j]),
                                 x[j]);
                 }
             } else {
@@ -468,7 +480,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         const float inv = 1.0f / (lt * ea + eb);
                         floatx4 oa, ob;
                         if constexpr (kWs) {
-                            const float* po = l0_cache(p, task, 2, qb[j]);
+                            const float* po = l0_cache<NW>(p, task, 2, qb[j]);
                             oa = ld4(po);
                             ob = ld4(po + 4);
                         } else {
@@ -551,13 +563,16 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 const float* W = P + (L - 1) * PL::size;
                 const FragSrc3 f3 = split0.layer(L - 1);
                 // this wave's tail weight tiles (c_proj, c_fc of hidden chunks 2 wave and
-                // 2 wave + 1), in flight across the first barrier
-                static_assert(kFF / 32 == kFwdWaves, "one pair of hidden chunks per wave");
+                // 2 wave + 1), in flight across the first barrier; the MLP runs on waves
+                // 0..kMlpWaves-1 (with 8 waves the upper four only take key tiles in (1))
+                constexpr int kMlpWaves = kFF / 32;
+                static_assert(kMlpWaves == 4 && NW >= kMlpWaves, "one pair of hidden chunks per MLP wave");
+                const int hw = wave & (kMlpWaves - 1);
                 const Split2 pj0 = f3.ld2(Frag3::proj), pj1 = f3.ld2(Frag3::proj + 1);
-                const Split2 fj0 = f3.ld2(Frag3::fc + 2 * wave), fj1 = f3.ld2(Frag3::fc + 2 * wave + 1);
+                const Split2 fj0 = f3.ld2(Frag3::fc + 2 * hw), fj1 = f3.ld2(Frag3::fc + 2 * hw + 1);
                 // (1) the attention as flash partials (m, l, o): with split values key
                 // tiles 2 wave and 2 wave + 1 (one pair, both products on mfma_x3), else
-                // key tiles wave and wave + 4
+                // key tiles wave and wave + NW
                 const int nparts = kSplitV ? (qlast >> 1) + 1 : qlast + 1;
                 if constexpr (kSplitV) {
                     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
@@ -614,7 +629,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const int kt = wave + 4 * h;
+                        const int kt = wave + NW * h;
                         if (kt > qlast) break;
                         // split key tile x the split query, broadcast to every column
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
@@ -652,10 +667,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 }
                 bar_lds();
                 DR_STAMP(2 * L - 1);
-                // (2) every wave: merge the partials, c_proj + residual, ln_2, then
-                // MLP hidden chunks wave and wave+4
+                // (2) every MLP wave: merge the partials, c_proj + residual, ln_2, then
+                // MLP hidden chunks 2 wave and 2 wave + 1
                 float xl[8];
-                {
+                if (NW == kMlpWaves || wave < kMlpWaves) {
                     const int g = lane_id() >> 4;
                     float mx = -INFINITY;
                     for (int w = 0; w < nparts; ++w) mx = fmaxf(mx, S.part_m[w]);
@@ -699,9 +714,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         const float xs_scale = exp2i(M.mlp_ex), up = exp2i(M.mlp_ew + M.mlp_ex),
                                     down = exp2i(-(M.mlp_ew + M.mlp_ex));
                         const Split2 xs = split2(xn, xs_scale);
-                        const floatx4 h0 = mfma_x3(fj0, xs, ld4(W + PL::fc_b + 2 * wave * 16 + 4 * g) * up) * down;
+                        const floatx4 h0 = mfma_x3(fj0, xs, ld4(W + PL::fc_b + 2 * hw * 16 + 4 * g) * up) * down;
                         const floatx4 h1 =
-                            mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * wave + 1) * 16 + 4 * g) * up) * down;
+                            mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * hw + 1) * 16 + 4 * g) * up) * down;
                         float gv[8];
 #pragma unroll
                         for (int r = 0; r < 4; r += 2) {
@@ -714,11 +729,11 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         }
                         const Split2 gs = split2(gv, xs_scale);
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-                        const floatx4 y0 = mfma_x3(f3.ld2(Frag3::mp + wave), gs, zero) * down;
-                        const floatx4 y1 = mfma_x3(f3.ld2(Frag3::mp + 4 + wave), gs, zero) * down;
+                        const floatx4 y0 = mfma_x3(f3.ld2(Frag3::mp + hw), gs, zero) * down;
+                        const floatx4 y1 = mfma_x3(f3.ld2(Frag3::mp + 4 + hw), gs, zero) * down;
                         if ((lane_id() & 15) == 0) {
-                            *reinterpret_cast<floatx4*>(&S.part_y[wave][4 * g]) = y0;
-                            *reinterpret_cast<floatx4*>(&S.part_y[wave][16 + 4 * g]) = y1;
+                            *reinterpret_cast<floatx4*>(&S.part_y[hw][4 * g]) = y0;
+                            *reinterpret_cast<floatx4*>(&S.part_y[hw][16 + 4 * g]) = y1;
                         }
                     }
                 }
@@ -855,6 +870,19 @@ int set_darkroom_memo(int on) {
     return DPT_OK;
 }
 
+template <bool kWs, int NW>
+static int launch_darkroom_geom(const ModelView& M, const DarkroomParams& p, hipStream_t st) {
+    const size_t dyn = sizeof(float) * (size_t)PTop::make(M.n_layer).total;
+    if (dyn + sizeof(DrSmem<kWs, NW>) > 160 * 1024) {
+        set_error(DPT_EUNSUPPORTED, "n_layer=%d: parameter block does not fit in LDS", M.n_layer);
+        return DPT_EUNSUPPORTED;
+    }
+    const void* kern = reinterpret_cast<const void*>(rollout_darkroom_kernel<kWs, NW>);
+    if (dyn > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    hipLaunchKernelGGL((rollout_darkroom_kernel<kWs, NW>), dim3(p.N), dim3(NW * 64), dyn, st, M, p);
+    return check_hip(hipGetLastError(), "rollout_darkroom_kernel launch");
+}
+
 int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_darkroom_rollout_args& a,
                             hipStream_t st) {
     DarkroomParams p;
@@ -883,27 +911,22 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
         set_error(DPT_EUNSUPPORTED, "fused darkroom rollout needs n_layer >= 2 (got %d)", M.n_layer);
         return DPT_EUNSUPPORTED;
     }
-    const size_t dyn = sizeof(float) * (size_t)PTop::make(M.n_layer).total;
-    const bool ws = a.workspace != nullptr;
-    const void* kern = ws ? reinterpret_cast<const void*>(rollout_darkroom_kernel<true>)
-                          : reinterpret_cast<const void*>(rollout_darkroom_kernel<false>);
-    if (dyn + (ws ? sizeof(DrSmem<true>) : sizeof(DrSmem<false>)) > 160 * 1024) {
-        set_error(DPT_EUNSUPPORTED, "n_layer=%d: parameter block does not fit in LDS", M.n_layer);
-        return DPT_EUNSUPPORTED;
-    }
-    if (dyn > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
     if (p.tab) {
         hipLaunchKernelGGL(state_tables_kernel, dim3(a.dim * a.dim), dim3(64), 0, st, M, a.dim, a.workspace);
         if (int rc = check_hip(hipGetLastError(), "state_tables_kernel launch")) return rc;
     }
-    if (ws) hipLaunchKernelGGL(rollout_darkroom_kernel<true>, dim3(a.N), dim3(kFwdWaves * 64), dyn, st, M, p);
-    else hipLaunchKernelGGL(rollout_darkroom_kernel<false>, dim3(a.N), dim3(kFwdWaves * 64), dyn, st, M, p);
-    return check_hip(hipGetLastError(), "rollout_darkroom_kernel launch");
+    // the smallest geometry that holds the window: 4 waves (two workgroups per CU) up to 128
+    // tokens, else 8 waves (one per CU) up to 256
+    const int64_t window = 1 + (int64_t)a.ctx_episodes * a.horizon;
+    const bool ws = a.workspace != nullptr;
+    if (window <= DrGeom<4>::kT)
+        return ws ? launch_darkroom_geom<true, 4>(M, p, st) : launch_darkroom_geom<false, 4>(M, p, st);
+    return ws ? launch_darkroom_geom<true, kDrMaxWaves>(M, p, st) : launch_darkroom_geom<false, kDrMaxWaves>(M, p, st);
 }
 
-int darkroom_max_window() { return kFwdT; }
+int darkroom_max_window() { return DrGeom<kDrMaxWaves>::kT; }
 
-int64_t darkroom_workspace_numel(int N) { return kDrTab + (int64_t)N * kDrWsPerTask; }
+int64_t darkroom_workspace_numel(int N) { return kDrTab + (int64_t)N * DrGeom<kDrMaxWaves>::kWsPerTask; }
 
 }  // namespace dpt
 

@@ -187,7 +187,7 @@ class DeviceModel:
         int32, logits (Heps*horizon, N, 5) f32 and forwards (N, Heps) int32 (window
         forwards run per task and episode: one per distinct state per episode under
         set_darkroom_memo) if requested.  Raises
-        NotImplementedError outside sd=2 / A=5 / window <= 128 (use the per-step path).
+        NotImplementedError outside sd=2 / A=5 / window <= 256 (use the per-step path).
         """
         dev = device()
         goals_d = _dev(goals, torch.int32, dev).contiguous()

@@ -3,7 +3,7 @@
 ``deploy_online_vec`` (evals/eval_darkroom.py:20-84): with the DPT controller
 over this package's ``Transformer`` and a ``DarkroomEnvVec`` the whole loop is
 one fused kernel launch (dpt_rollout_darkroom) when the window fits (1 + H <=
-128); otherwise it stays on the device step by step — per step one window forward (gfx950 kernel) over the fixed
+256); otherwise it stays on the device step by step — per step one window forward (gfx950 kernel) over the fixed
 in-context episodes with the current state as query, device sampling, the
 integer grid step kernel, and an on-device append into the episode buffers;
 returns are summed on device and copied once at the end.  Other controllers
@@ -67,7 +67,7 @@ def _episode_device(dm, ctrl, vec_env, ctx, horizon):
     return es, ea, ns, er
 
 
-_FUSED_MAX_WINDOW = 128  # dpt_rollout_darkroom: 1 + H tokens per forward
+_FUSED_MAX_WINDOW = 256  # dpt_rollout_darkroom: 1 + H tokens per forward
 
 
 def _fused_ok(vec_env, controller, H):

@@ -315,8 +315,9 @@ int dpt_rollout_policy(const dpt_policy_rollout_args* args_host, void* stream);
  * prediction at the last position.  Action a_t = select(logits, u_t) with
  * u_t = uniforms[(e*horizon+t)*N + i] or Philox(seed, counter + e*horizon + t,
  * first_task + i, DPT_STREAM_SELECT) -- the same draws as dpt_select_action.
- * Requires sd = 2, A = 5, 1 + R*horizon <= 128 and dim <= 255 (else
- * DPT_EUNSUPPORTED: use dpt_forward_window per step).                       */
+ * Requires sd = 2, A = 5, 1 + R*horizon <= 256 and dim <= 255 (else
+ * DPT_EUNSUPPORTED: use dpt_forward_window per step).  Windows of up to 128
+ * tokens run 4 waves per task (two tasks per CU), longer ones 8 waves.       */
 typedef struct dpt_darkroom_rollout_args {
     int32_t N, Heps, horizon, ctx_episodes;
     int32_t dim, sample;

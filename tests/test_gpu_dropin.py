@@ -272,7 +272,7 @@ def test_eval_darkroom_device_loop_matches_reference(fused):
 
 
 def test_eval_darkroom_per_step_memo_bit_identical():
-    """The per-step device loop (window 1 + 2*70 = 141 > 128 tokens, so not fused) forwards only
+    """The per-step device loop (window 1 + 2*130 = 261 > 256 tokens, so not fused) forwards only
     the tasks whose state is new in the episode; returns are identical with the memo off."""
     import dpt_hip
     from ctrls.ctrl_darkroom import DarkroomTransformerController
@@ -280,7 +280,7 @@ def test_eval_darkroom_per_step_memo_bit_identical():
     from evals import eval_darkroom
     _, m = ref_model("darkroom")
     rs = np.random.RandomState(8)
-    envs = [DarkroomEnv(10, rs.randint(0, 10, 2), 70) for _ in range(48)]
+    envs = [DarkroomEnv(10, rs.randint(0, 10, 2), 130) for _ in range(48)]
     outs = []
     try:
         for memo in (False, True):
@@ -288,15 +288,15 @@ def test_eval_darkroom_per_step_memo_bit_identical():
             np.random.seed(5)
             ctrl = DarkroomTransformerController(m, batch_size=48, sample=True)
             vec = DarkroomEnvVec(envs)
-            assert not eval_darkroom._fused_ok(vec, ctrl, 140)
-            outs.append(eval_darkroom.deploy_online_vec(vec, ctrl, 4, 140, 70))
+            assert not eval_darkroom._fused_ok(vec, ctrl, 260)
+            outs.append(eval_darkroom.deploy_online_vec(vec, ctrl, 3, 260, 130))
     finally:
         dpt_hip.set_darkroom_memo(True)
     assert np.array_equal(outs[0], outs[1])
 
 
 def test_eval_darkroom_per_step_shard_invariant():
-    """The per-step device loop (window 1 + 2*70 = 141 > 128 tokens, so not fused) keys its
+    """The per-step device loop (window 1 + 2*130 = 261 > 256 tokens, so not fused) keys its
     selection draws by the GLOBAL task id (DarkroomEnvVec.first_task), like the fused kernel:
     two shards of the tasks, each with the same controller seed, give the unsharded returns."""
     from ctrls.ctrl_darkroom import DarkroomTransformerController
@@ -307,12 +307,12 @@ def test_eval_darkroom_per_step_shard_invariant():
     goals = [rs.randint(0, 10, 2) for _ in range(40)]
 
     def run(lo, hi):
-        envs = [DarkroomEnv(10, g_, 70) for g_ in goals[lo:hi]]
+        envs = [DarkroomEnv(10, g_, 130) for g_ in goals[lo:hi]]
         ctrl = DarkroomTransformerController(m, batch_size=hi - lo, sample=True)
         ctrl._stream.seed = 31337
         vec = DarkroomEnvVec(envs, first_task=lo)
-        assert not eval_darkroom._fused_ok(vec, ctrl, 140)
-        return eval_darkroom.deploy_online_vec(vec, ctrl, 3, 140, 70)
+        assert not eval_darkroom._fused_ok(vec, ctrl, 260)
+        return eval_darkroom.deploy_online_vec(vec, ctrl, 3, 260, 130)
 
     full = run(0, 40)
     assert np.array_equal(np.concatenate([run(0, 17), run(17, 40)]), full)

@@ -307,10 +307,12 @@ def test_rollout_darkroom_fused_matches_reference(tag):
     assert np.array_equal(out["returns"].cpu().numpy(), r["returns"])
 
 
-@pytest.mark.parametrize("Heps,horizon,R", [(3, 30, 2), (2, 127, 1)])
+@pytest.mark.parametrize("Heps,horizon,R", [(3, 30, 2), (2, 127, 1), (3, 64, 2), (2, 255, 1)])
 def test_rollout_darkroom_philox_vs_oracle(Heps, horizon, R):
     """Philox draws (the select stream of dpt_select_action) through the fused kernel equal the
-    oracle fed the same uniforms; the second case is the largest window (1 + R*horizon = 128)."""
+    oracle fed the same uniforms; (2, 127, 1) is the largest window of the 4-wave kernel
+    (1 + R*horizon = 128), (3, 64, 2) the smallest of the 8-wave one (129) and (2, 255, 1) its
+    largest (256)."""
     d = dh()
     _, m, W = model_from_golden("darkroom")
     rs = np.random.RandomState(3)
@@ -344,7 +346,7 @@ def test_rollout_darkroom_large_properties():
     hi = m.rollout_darkroom(goals[1000:], 2, 100, 1, seed=11, first_task=1000, want_actions=True)
     assert np.array_equal(np.concatenate([lo["actions"].cpu().numpy(), hi["actions"].cpu().numpy()]), a1)
     with pytest.raises(NotImplementedError):
-        m.rollout_darkroom(goals[:4], 1, 128, 1)
+        m.rollout_darkroom(goals[:4], 1, 128, 2)  # window 257
     # greedy episode 1 logits == the per-step window kernel on the recorded context
     og = m.rollout_darkroom(goals[:64], 2, 100, 1, sample=False, want_actions=True, want_logits=True)
     acts = og["actions"].cpu().numpy()
@@ -735,3 +737,51 @@ def test_rollout_darkroom_dim12_workspace_without_state_table():
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(w, 4).numpy(), 4, 404, goals[tasks], Heps, horizon, R, u,
                                     True, dim=dim, threads=16, want_logits=True)
     check_darkroom_tasks(outs[1], tasks, ref, Heps, horizon)
+
+
+@pytest.mark.parametrize("Heps,horizon,R", [(4, 100, 2), (3, 85, 3)])
+def test_rollout_darkroom_long_windows(Heps, horizon, R):
+    """Windows of 129..256 tokens run the 8-wave kernel (two 16-token blocks per wave): window 201
+    (the reference's H = 200 with horizon 100) and 256 (the largest).  Sampled tasks agree with the
+    float64 C oracle fed the same Philox draws (logits within 1e-5, actions and returns exactly up
+    to each task's first near-tie draw); the logits memo is bit-identical to one forward per step;
+    the workspace and LDS-only variants agree within the logit bar up to the first differing
+    sampled action."""
+    import dpt_hip
+    from oracle import c_oracle
+    d = dh()
+    g, m, _ = model_from_golden("darkroom")
+    N, seed = 192, 77
+    goals = darkroom_config(N)
+    steps = Heps * horizon
+    outs = {}
+    try:
+        for ws, memo in ((True, True), (True, False), (False, True)):
+            dpt_hip.set_darkroom_workspace(ws)
+            dpt_hip.set_darkroom_memo(memo)
+            o = m.rollout_darkroom(goals, Heps, horizon, R, seed=seed, want_actions=True, want_logits=True,
+                                   want_forwards=True)
+            outs[ws, memo] = {k: o[k].cpu().numpy() for k in ("actions", "logits", "returns", "forwards")}
+    finally:
+        dpt_hip.set_darkroom_workspace(True)
+        dpt_hip.set_darkroom_memo(True)
+    on, off = outs[True, True], outs[True, False]
+    for k in ("actions", "logits", "returns"):
+        assert np.array_equal(on[k], off[k]), k
+    assert (off["forwards"] == horizon).all() and on["forwards"].sum() < off["forwards"].sum()
+    lds = outs[False, True]
+    diff = lds["actions"] != on["actions"]
+    first = np.where(diff.any(1), diff.argmax(1), steps)
+    assert (first < steps).mean() <= 0.02
+    for t in range(N):
+        f = min(first[t] + 1, steps)
+        assert_logits(lds["logits"][:f, t], on["logits"][:f, t])
+    tasks = np.arange(0, N, 3)
+    u = np.stack([philox_np.uniform(seed, k, tasks, d.STREAM_SELECT) for k in range(steps)])
+    w = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w/")}
+    ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(w, 4).numpy(), 4, 404, goals[tasks], Heps, horizon, R, u,
+                                    True, threads=16, want_logits=True)
+    res = {"logits": torch.from_numpy(on["logits"]), "actions": torch.from_numpy(on["actions"]),
+           "returns": torch.from_numpy(on["returns"])}
+    assert len(tasks) >= 64
+    assert check_darkroom_tasks(res, tasks, ref, Heps, horizon) >= len(tasks) // 2
