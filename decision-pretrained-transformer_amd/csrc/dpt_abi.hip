@@ -162,6 +162,12 @@ static int fwd_scales(ModelView& v, int n_layer) {
     v.attn_ew = expo(gw, -24, 12);
     v.attn_ey = expo(ymax, -24, 8);
     v.attn_eq = expo(qmax, -24, 8);
+    // gelu_split folds 2^-3(ew + ex) into a constant: keep it a normal fp32 number
+    if (v.mlp_ew + v.mlp_ex < -40) {
+        set_error(DPT_EUNSUPPORTED, "MLP weights/activations too large for the fp16 split products (bound 2^%d)",
+                  -(v.mlp_ew + v.mlp_ex) + 28);
+        return DPT_EUNSUPPORTED;
+    }
     return DPT_OK;
 }
 

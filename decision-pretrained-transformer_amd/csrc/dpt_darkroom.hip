@@ -54,6 +54,12 @@ __device__ unsigned long long g_dr_last;
 // other workgroup's waves on the same SIMD (only issue order changes: bit-identical;
 // -0.9 % at config 3)
 #define DPT_TAIL_PRIO(p) __builtin_amdgcn_s_setprio(p)
+// The wave that runs the step's serial tail (ln_f, head, selection, env step) and the memo-hit
+// chain (on its lane 0, which keeps the episode's state and return in registers): the last MLP
+// wave, whose blocks are the fewest (blocks_of_wave gives the last waves the middle block or none)
+#ifndef DPT_TAIL_WAVE
+#define DPT_TAIL_WAVE 3
+#endif
 
 namespace dpt {
 
@@ -252,6 +258,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     const int task = blockIdx.x;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr int kTailWave = DPT_TAIL_WAVE, kTailTid = 64 * kTailWave;
+    static_assert(kTailWave < NW && kTailWave < kFF / 32, "the tail wave is an MLP wave of the last layer");
     const int steps_total = p.Heps * p.horizon;
     const float scale = 0.17677669529663687f;  // 1/sqrt(head_dim = 32)
     const int L = M.n_layer;
@@ -291,7 +299,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             S.sy = 0;
             S.nfwd = 0;
         }
-        // thread 0's copy of the state and the episode's return (it runs every selection)
+        // the tail thread's copy of the state and the episode's return (it runs every selection)
         int cur_x = 0, cur_y = 0, cur_ret = 0;
         for (int i = tid; i < kMemoStates; i += blockDim.x) {
             S.memo_q[i][0] = -1.0;
@@ -330,6 +338,11 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 if (j >= nb) break;
                 float m, l, o[8];
                 attend(S.kv, q[j], qb[j], 1, scale, m, l, o, M);
+                // the partial at its true scale (attend's o, l carry 2^(attn_ey + kPExp), 2^kPExp)
+                l *= exp2i(-kPExp);
+                const float down = exp2i(-(M.attn_ey + kPExp));
+#pragma unroll
+                for (int k = 0; k < 8; ++k) o[k] *= down;
                 const int lane = lane_id();
                 if constexpr (kWs) {
                     ws_store(l0_cache<NW>(p, task, 2, qb[j]), o);
@@ -375,7 +388,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 // thread 0 runs consecutive steps whose state was already queried this
                 // episode (a memo hit needs no forward); the other threads wait at one
                 // barrier for the first state that needs one
-                if (tid == 0) {
+                if (tid == kTailTid) {
                     DPT_TAIL_PRIO(3);  // the memo-hit chain is the workgroup's critical path
                     int tt = t;
                     while (tt < p.horizon) {
@@ -536,17 +549,14 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 DR_STAMP(2 * layer);
                 if (last) break;
                 if (nb > 0) {
-                    float o[2][8];
+                    float o[2][8], l[2];
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
                         if (j >= nb) break;
-                        float m, l;
-                        attend(S.kv, q[j], qb[j], 0, scale, m, l, o[j], M);
-                        const float inv = 1.0f / l;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) o[j][k] *= inv;
+                        float m;
+                        attend(S.kv, q[j], qb[j], 0, scale, m, l[j], o[j], M);
                     }
-                    DPT_BLOCKS(nb, attn_proj3<NB>(W, split0.layer(layer), o, x, M));
+                    DPT_BLOCKS(nb, attn_proj3_ol<NB>(W, split0.layer(layer), o, l, x, M));
                 }
                 bar_lds();  // every read of this layer's K/V is done
                 DR_STAMP(2 * layer + 1);
@@ -570,10 +580,13 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 const int hw = wave & (kMlpWaves - 1);
                 const Split2 pj0 = f3.ld2(Frag3::proj), pj1 = f3.ld2(Frag3::proj + 1);
                 const Split2 fj0 = f3.ld2(Frag3::fc + 2 * hw), fj1 = f3.ld2(Frag3::fc + 2 * hw + 1);
-                // (1) the attention as flash partials (m, l, o): with split values key
-                // tiles 2 wave and 2 wave + 1 (one pair, both products on mfma_x3), else
-                // key tiles wave and wave + NW
+                // (1) the attention as flash partials (m, l, o), in attend's convention (exp2
+                // domain; l and o at 2^kPExp and 2^(attn_ey + kPExp), so o / l is the output at
+                // the c_proj split's scale): with split values key tiles 2 wave and 2 wave + 1
+                // (one pair, both products on mfma_x3), else key tiles wave and wave + NW
                 const int nparts = kSplitV ? (qlast >> 1) + 1 : qlast + 1;
+                // raw score product -> exp2-domain score
+                const float sl = scale * 1.4426950408889634f * exp2i(-(M.attn_ey + M.attn_eq));
                 if constexpr (kSplitV) {
                     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
                     const int kb = 2 * wave;
@@ -581,8 +594,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
                         const Split2 qs = split2(qv, exp2i(M.attn_eq));  // the query, broadcast to every column
-                        const float kscale = scale * exp2i(-(M.attn_ey + M.attn_eq));
-                        float sv[8], mt = -INFINITY;
+                        float sv[8];
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
                             const int kt = kb + h;
@@ -594,27 +606,23 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             const Split2 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane]};
                             const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const float sr = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * kscale : -INFINITY;
-                                sv[4 * h + r] = sr;
-                                mt = fmaxf(mt, sr);
-                            }
+                            for (int r = 0; r < 4; ++r) sv[4 * h + r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] : -INFINITY;
                         }
-                        mt = max_cols(mt);
+                        const float mt = max_cols(fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
+                                                        fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])))) *
+                                         sl;
+                        // P x 2^kPExp <= 2^kPExp (mt is the exact max): fp16 two-part as in attend
+                        const float bm = (float)kPExp - mt;
                         float pr[8];
 #pragma unroll
-                        for (int r = 0; r < 8; ++r) pr[r] = __expf(sv[r] - mt);
+                        for (int r = 0; r < 8; ++r) pr[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], sl, bm));
                         float lt = ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
                         lt = sum_cols(lt);
-                        // P <= 1 here (mt is the exact max): fp16 two-part at 2^kPExp as in attend
-                        const Split2 ps = split2(pr, exp2i(kPExp));
+                        const Split2 ps = split2(pr, 1.0f);
                         const int pp = wave;
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-                        const float down = exp2i(-(M.attn_ey + kPExp));
-                        const floatx4 o0 =
-                            mfma_x3(Split2{S.kv.VS[pp][0][0][lane], S.kv.VS[pp][0][1][lane]}, ps, zero) * down;
-                        const floatx4 o1 =
-                            mfma_x3(Split2{S.kv.VS[pp][1][0][lane], S.kv.VS[pp][1][1][lane]}, ps, zero) * down;
+                        const floatx4 o0 = mfma_x3(Split2{S.kv.VS[pp][0][0][lane], S.kv.VS[pp][0][1][lane]}, ps, zero);
+                        const floatx4 o1 = mfma_x3(Split2{S.kv.VS[pp][1][0][lane], S.kv.VS[pp][1][1][lane]}, ps, zero);
                         if (c == 0) {
                             *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
                             *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;
@@ -634,20 +642,19 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         // split key tile x the split query, broadcast to every column
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
                         const Split2 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane]};
-                        const floatx4 sc = mfma_x3(ks, split2(qv, exp2i(M.attn_eq)), floatx4{0.f, 0.f, 0.f, 0.f}) *
-                                           exp2i(-(M.attn_ey + M.attn_eq));
+                        const floatx4 sc = mfma_x3(ks, split2(qv, exp2i(M.attn_eq)), floatx4{0.f, 0.f, 0.f, 0.f});
                         float sv[4], mt = -INFINITY;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            sv[r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * scale : -INFINITY;
+                            sv[r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * sl : -INFINITY;
                             mt = fmaxf(mt, sv[r]);
                         }
                         mt = max_cols(mt);
                         float pr[4];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) pr[r] = __expf(sv[r] - mt);
+                        for (int r = 0; r < 4; ++r) pr[r] = __builtin_amdgcn_exp2f(sv[r] - mt);
                         float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
-                        lt = sum_cols(lt);
+                        lt = sum_cols(lt) * exp2i(kPExp);
                         const floatx4 v0 = ld4(&S.kv.Vt[c][kt * 16 + 4 * g]);
                         const floatx4 v1 = ld4(&S.kv.Vt[16 + c][kt * 16 + 4 * g]);
                         floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
@@ -655,6 +662,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         for (int s4 = 0; s4 < 4; ++s4) o0 = mfma4(v0[s4], pr[s4], o0);
 #pragma unroll
                         for (int s4 = 0; s4 < 4; ++s4) o1 = mfma4(v1[s4], pr[s4], o1);
+                        o0 = o0 * exp2i(M.attn_ey + kPExp);
+                        o1 = o1 * exp2i(M.attn_ey + kPExp);
                         if (c == 0) {
                             *reinterpret_cast<floatx4*>(&S.part_o[kt][4 * g]) = o0;
                             *reinterpret_cast<floatx4*>(&S.part_o[kt][16 + 4 * g]) = o1;
@@ -677,7 +686,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     float lsum = 0.f;
                     floatx4 oa = {0.f, 0.f, 0.f, 0.f}, ob = {0.f, 0.f, 0.f, 0.f};
                     for (int w = 0; w < nparts; ++w) {
-                        const float e = __expf(S.part_m[w] - mx);
+                        const float e = __builtin_amdgcn_exp2f(S.part_m[w] - mx);
                         lsum += S.part_l[w] * e;
                         const floatx4 pa = ld4(&S.part_o[w][4 * g]), pb = ld4(&S.part_o[w][16 + 4 * g]);
 #pragma unroll
@@ -686,21 +695,19 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             ob[r] = fmaf(pb[r], e, ob[r]);
                         }
                     }
-                    const float inv = 1.0f / lsum;
-                    float o[8];
+                    // o / lsum: the attention output at the split scale 2^attn_ey
+                    const float o[8] = {oa[0], oa[1], oa[2], oa[3], ob[0], ob[1], ob[2], ob[3]};
                     const floatx4 xa = ld4(&S.xl[4 * g]), xb = ld4(&S.xl[16 + 4 * g]);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        o[r] = oa[r] * inv;
-                        o[4 + r] = ob[r] * inv;
                         xl[r] = xa[r];
                         xl[4 + r] = xb[r];
                     }
                     {
-                        const float up = exp2i(M.attn_ew + M.attn_ey), down = exp2i(-(M.attn_ew + M.attn_ey));
-                        const Split2 os = split2(o, exp2i(M.attn_ey));
-                        const floatx4 a0 = mfma_x3(pj0, os, ld4(W + PL::proj_b + 4 * g) * up) * down;
-                        const floatx4 a1 = mfma_x3(pj1, os, ld4(W + PL::proj_b + 16 + 4 * g) * up) * down;
+                        const float down = exp2i(-(M.attn_ew + M.attn_ey));
+                        const Split2 os = split2(o, 1.0f / lsum);
+                        const floatx4 a0 = mfma_x3(pj0, os, ld4(W + PL::proj_b + 4 * g)) * down;
+                        const floatx4 a1 = mfma_x3(pj1, os, ld4(W + PL::proj_b + 16 + 4 * g)) * down;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             xl[r] += a0[r];
@@ -711,23 +718,11 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     ln_cols(xl, xn, W + PL::ln2_g, W + PL::ln2_b);
                     {
                         // the MLP's fp16 two-part products at scale 2^(mlp_ew + mlp_ex) (mlp3_n)
-                        const float xs_scale = exp2i(M.mlp_ex), up = exp2i(M.mlp_ew + M.mlp_ex),
-                                    down = exp2i(-(M.mlp_ew + M.mlp_ex));
+                        const float xs_scale = exp2i(M.mlp_ex), down = exp2i(-(M.mlp_ew + M.mlp_ex));
                         const Split2 xs = split2(xn, xs_scale);
-                        const floatx4 h0 = mfma_x3(fj0, xs, ld4(W + PL::fc_b + 2 * hw * 16 + 4 * g) * up) * down;
-                        const floatx4 h1 =
-                            mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * hw + 1) * 16 + 4 * g) * up) * down;
-                        float gv[8];
-#pragma unroll
-                        for (int r = 0; r < 4; r += 2) {
-                            const floatx2 g0 = gelu_fast2(floatx2{h0[r], h0[r + 1]});
-                            const floatx2 g1 = gelu_fast2(floatx2{h1[r], h1[r + 1]});
-                            gv[r] = g0.x;
-                            gv[r + 1] = g0.y;
-                            gv[4 + r] = g1.x;
-                            gv[4 + r + 1] = g1.y;
-                        }
-                        const Split2 gs = split2(gv, xs_scale);
+                        const floatx4 h0 = mfma_x3(fj0, xs, ld4(W + PL::fc_b + 2 * hw * 16 + 4 * g));
+                        const floatx4 h1 = mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * hw + 1) * 16 + 4 * g));
+                        const Split2 gs = gelu_split(h0, h1, GeluSplit(M.mlp_ew, M.mlp_ex));
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
                         const floatx4 y0 = mfma_x3(f3.ld2(Frag3::mp + hw), gs, zero) * down;
                         const floatx4 y1 = mfma_x3(f3.ld2(Frag3::mp + 4 + hw), gs, zero) * down;
@@ -739,12 +734,13 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 }
                 bar_lds();
                 DR_STAMP(2 * L);
-                // (3) wave 0: residual, ln_f, head, selection, env step
-                if (wave == 0) {
+                // (3) the tail wave: residual, ln_f, head, selection, env step
+                if (wave == kTailWave) {
                     // the step's serial tail: issue ahead of the other workgroup's waves on this SIMD
                     DPT_TAIL_PRIO(3);
                     const int lane = lane_id(), g = lane >> 4;
-                    floatx4 ya = ld4(W + PL::mp_b + 4 * g), yb = ld4(W + PL::mp_b + 16 + 4 * g);
+                    const float mdown = exp2i(-(M.mlp_ew + M.mlp_ex));  // mp_b is stored at the MLP product scale (PL)
+                    floatx4 ya = ld4(W + PL::mp_b + 4 * g) * mdown, yb = ld4(W + PL::mp_b + 16 + 4 * g) * mdown;
 #pragma unroll
                     for (int w = 0; w < kFF / 32; ++w) {
                         const floatx4 pa = ld4(&S.part_y[w][4 * g]), pb = ld4(&S.part_y[w][16 + 4 * g]);
@@ -800,7 +796,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         }
 
         // episode bookkeeping: returns, then shift-append the context (eval_darkroom.py:75-82)
-        if (tid == 0) {
+        if (tid == kTailTid) {
             p.returns_out[(size_t)task * p.Heps + ep] = cur_ret;
             if (p.forwards_out) p.forwards_out[(size_t)task * p.Heps + ep] = S.nfwd;
         }

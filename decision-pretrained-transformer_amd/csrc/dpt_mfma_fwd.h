@@ -207,6 +207,42 @@ __device__ inline float gelu_fast(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
+// gelu_new of the c_fc output taken straight from its product accumulator, returned as the
+// fp16 two-part split of mlp.c_proj's B operand.  With y = h 2^(ew+ex) (the accumulator, bias
+// included) every scale is an exact power of two folded into a constant:
+//   gelu(h) 2^ex = y / ((1 + 2^t) 2^ew),  t = h (c1 + c2 h^2) = y (c1' + c2' y^2),
+//   c1' = c1 2^-(ew+ex), c2' = c2 2^-3(ew+ex)
+// and the quotient's multiply rounds straight into the fp16 parts (v_fma_mix: hi = f16(y r),
+// lo = f16(y r - hi), each one rounding).  Six VALU slots and two transcendentals per value
+// instead of the eleven of scale-down, gelu_fast, scale-up and split2.  fwd_scales keeps
+// ew + ex >= -40, so c2' stays a normal fp32 number.
+struct GeluSplit {
+    float c1, c2, s;
+    __device__ GeluSplit(int ew, int ex) {
+        const float k1 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+        c1 = k1 * exp2i(-(ew + ex));
+        c2 = (k1 * 0.044715f) * exp2i(-3 * (ew + ex));
+        s = exp2i(ew);
+    }
+};
+__device__ inline Split2 gelu_split(const floatx4& a, const floatx4& b, const GeluSplit& k) {
+    const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    unsigned hh[4], mm[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const float y0 = v[2 * p], y1 = v[2 * p + 1];
+        const float t0 = fmaf(y0 * y0, k.c2, k.c1) * y0, t1 = fmaf(y1 * y1, k.c2, k.c1) * y1;
+        const float r0 = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(t0), k.s, k.s));
+        const float r1 = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(t1), k.s, k.s));
+        const halfx2 h = {(_Float16)__builtin_fmaf(y0, r0, 0.0f), (_Float16)__builtin_fmaf(y1, r1, 0.0f)};
+        const halfx2 m = {(_Float16)__builtin_fmaf(y0, r0, -(float)h.x), (_Float16)__builtin_fmaf(y1, r1, -(float)h.y)};
+        hh[p] = __builtin_bit_cast(unsigned, h);
+        mm[p] = __builtin_bit_cast(unsigned, m);
+    }
+    return Split2{__builtin_bit_cast(halfx8, uint4{hh[0], hh[1], hh[2], hh[3]}),
+                  __builtin_bit_cast(halfx8, uint4{mm[0], mm[1], mm[2], mm[3]})};
+}
+
 template <int NB>
 __device__ inline void ln_n(const float (&x)[2][8], float (&xn)[2][8], const float* gam, const float* bet) {
 #pragma unroll
@@ -221,42 +257,33 @@ template <int NB>
 __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&x)[2][8],
                               int ew, int ex) {
     const int g = lane_id() >> 4;
-    const float xs_scale = exp2i(ex), up = exp2i(ew + ex), down = exp2i(-(ew + ex));
-    const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g) * up, yb1 = ld4(W + PL::mp_b + 16 + 4 * g) * up;
+    const float xs_scale = exp2i(ex), down = exp2i(-(ew + ex));
+    const GeluSplit gk(ew, ex);
+    const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);  // scaled (PL)
     floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
     Split2 xs[2];
 #pragma unroll
     for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], xs_scale);
-    // c_fc tiles one pair ahead (in flight across the pair's split + c_proj products), the
+    // c_fc tiles one pair ahead (in flight across the pair's gelu + c_proj products), the
     // pair's c_proj tiles at its start (in flight across its c_fc + gelu)
     Split2 wf0 = f3.ld2(Frag3::fc), wf1 = f3.ld2(Frag3::fc + 1);
 #pragma unroll
     for (int p = 0; p < kFF / 32; ++p) {
         const Split2 w0 = f3.ld2(Frag3::mp + p), w1 = f3.ld2(Frag3::mp + 4 + p);
-        float gv[2][8];
-        const floatx4 fb0 = ld4(W + PL::fc_b + 2 * p * 16 + 4 * g) * up;
-        const floatx4 fb1 = ld4(W + PL::fc_b + (2 * p + 1) * 16 + 4 * g) * up;
+        Split2 gs[2];
+        const floatx4 fb0 = ld4(W + PL::fc_b + 2 * p * 16 + 4 * g);
+        const floatx4 fb1 = ld4(W + PL::fc_b + (2 * p + 1) * 16 + 4 * g);
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const floatx4 h0 = mfma_x3(wf0, xs[j], fb0) * down, h1 = mfma_x3(wf1, xs[j], fb1) * down;
-#pragma unroll
-            for (int r = 0; r < 4; r += 2) {
-                const floatx2 g0 = gelu_fast2(floatx2{h0[r], h0[r + 1]}), g1 = gelu_fast2(floatx2{h1[r], h1[r + 1]});
-                gv[j][r] = g0.x;
-                gv[j][r + 1] = g0.y;
-                gv[j][4 + r] = g1.x;
-                gv[j][4 + r + 1] = g1.y;
-            }
-        }
+        for (int j = 0; j < NB; ++j)
+            gs[j] = gelu_split(mfma_x3(wf0, xs[j], fb0), mfma_x3(wf1, xs[j], fb1), gk);
         if (p + 1 < kFF / 32) {
             wf0 = f3.ld2(Frag3::fc + 2 * p + 2);
             wf1 = f3.ld2(Frag3::fc + 2 * p + 3);
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-            const Split2 gs = split2(gv[j], xs_scale);
-            y0[j] = mfma_x3(w0, gs, y0[j]);
-            y1[j] = mfma_x3(w1, gs, y1[j]);
+            y0[j] = mfma_x3(w0, gs[j], y0[j]);
+            y1[j] = mfma_x3(w1, gs[j], y1[j]);
         }
     }
 #pragma unroll
@@ -277,11 +304,11 @@ template <int NB>
 __device__ inline void u_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&xs)[2], float (&q)[2][8],
                                  const ModelView& M) {
     const int g = lane_id() >> 4;
-    const float up = exp2i(M.attn_ew + M.attn_ey), down = exp2i(-(M.attn_ew + M.attn_ey));
+    const float down = exp2i(-(M.attn_ew + M.attn_ey));
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
         const Split2 w = f3.ld2(Frag3::attn + ob);
-        const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g) * up;
+        const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);  // scaled (PL)
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             const floatx4 acc = mfma_x3(w, xs[j], bias) * down;
@@ -302,17 +329,14 @@ __device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float
 // attn_proj on mfma_x3: x^T += Wvp^T o^T + bvp (o, a convex combination of the values y,
 // shares their bound and scale)
 template <int NB>
-__device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8],
-                                  const ModelView& M) {
+__device__ inline void attn_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&os)[2], float (&x)[2][8],
+                                    const ModelView& M) {
     const int g = lane_id() >> 4;
-    const float up = exp2i(M.attn_ew + M.attn_ey), down = exp2i(-(M.attn_ew + M.attn_ey));
-    Split2 os[2];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], exp2i(M.attn_ey));
+    const float down = exp2i(-(M.attn_ew + M.attn_ey));
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
         const Split2 w = f3.ld2(Frag3::proj + ob);
-        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g) * up;
+        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g);  // scaled (PL)
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             const floatx4 acc = mfma_x3(w, os[j], bias) * down;
@@ -320,6 +344,24 @@ __device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const floa
             for (int r = 0; r < 4; ++r) x[j][ob * 4 + r] += acc[r];
         }
     }
+}
+template <int NB>
+__device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8],
+                                  const ModelView& M) {
+    Split2 os[2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], exp2i(M.attn_ey));
+    attn_proj3_s<NB>(W, f3, os, x, M);
+}
+// the same from attend's unnormalised (o, l): o / l is the attention output x 2^attn_ey already,
+// so the split takes 1 / l as its scale (one multiply per value)
+template <int NB>
+__device__ inline void attn_proj3_ol(const float* W, const FragSrc3& f3, const float (&o)[2][8], const float (&l)[2],
+                                     float (&x)[2][8], const ModelView& M) {
+    Split2 os[2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], 1.0f / l[j]);
+    attn_proj3_s<NB>(W, f3, os, x, M);
 }
 
 // Folded attention input of the NB blocks qb[]: keys and values are the
@@ -381,11 +423,12 @@ __device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const fl
     kv_store<NB>(S, qb, xn, xs);
 }
 
-// Causal flash attention of query block qb over keys [key_lo, 16*qb + c]:
+// Causal flash attention of query block qb over keys [key_lo, 16*qb + c] (key_lo <= 16):
 // per token column a softmax reference m (-inf when no key; never more than
-// kSlack below the column's max), l = sum_s 2^(s-m) and the unnormalised o^T =
-// sum_s 2^(s-m) v_s (C-layout), all in the exp2 domain: s and m are the scores
-// times log2(e) (folded into the scale), so each probability is one v_exp_f32.
+// kSlack below the column's max), l = 2^kPExp sum_s 2^(s-m) and the unnormalised o^T =
+// 2^(attn_ey + kPExp) sum_s 2^(s-m) v_s (C-layout), all in the exp2 domain: s and m are the
+// scores times log2(e) (folded into the scale), so each probability is one v_exp_f32.  o / l is
+// the attention output at the scale of the c_proj product's B operand (attn_proj3_ol).
 template <class KV>
 __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
                               float& lsum, float (&o)[8], const ModelView& M) {
@@ -410,13 +453,19 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         // so it holds finite values).  The softmax reference moves as in the per-tile
         // form below, one vote per pair, but with kSlackP = 8: P <= 2^8, so P x 2^kPExp
         // fits fp16, and o accumulates at scale 2^(attn_ey + kPExp).
+        // Per score: the vote compares the raw products with a threshold kept in their units
+        // (thr = (m + kSlackP) / scale, moved with m), and the probability is one fma into
+        // the exponent, 2^(sc scale - m + kPExp) = P x 2^kPExp (bm = kPExp - m), so neither
+        // the scaled score nor the P x 2^kPExp product is formed; masks only on the diagonal
+        // tile and the tile holding key_lo.
         constexpr float kSlackP = 8.f;
+        const float inv_scale = 1.0f / scale;
         m = -INFINITY;
         lsum = 0.f;
+        float thr = -INFINITY, bm = 0.f;  // bm = 0 while no key (not NaN)
         floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
         for (int kb = 0; kb <= qb; kb += 2) {
             float sv[8];
-            float mt = -INFINITY;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int kt = kb + h;
@@ -428,17 +477,17 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
                 const Split2 ks{S.KS[kt][0][lane], S.KS[kt][1][lane]};
                 const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = kt * 16 + 4 * g + r;
-                    float sr = sc[r] * scale;
-                    if ((kt == qb && 4 * g + r > c) || key < key_lo) sr = -INFINITY;
-                    sv[4 * h + r] = sr;
-                    mt = fmaxf(mt, sr);
+                for (int r = 0; r < 4; ++r) sv[4 * h + r] = sc[r];
+                if (kt == qb || kt * 16 < key_lo) {  // wave-uniform
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if ((kt == qb && 4 * g + r > c) || kt * 16 + 4 * g + r < key_lo) sv[4 * h + r] = -INFINITY;
                 }
             }
-            if (__builtin_amdgcn_ballot_w64(mt > m + kSlackP)) {  // wave-uniform
-                mt = max_cols(mt);
-                const float mn = fmaxf(m, mt);
+            const float mt = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
+                                   fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
+            if (__builtin_amdgcn_ballot_w64(mt > thr)) {  // wave-uniform
+                const float mn = fmaxf(m, max_cols(mt * scale));
                 const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
                 lsum *= corr;
 #pragma unroll
@@ -447,23 +496,23 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
                     o1[r] *= corr;
                 }
                 m = mn;
+                thr = (mn + kSlackP) * inv_scale;
+                bm = mn == -INFINITY ? 0.f : (float)kPExp - mn;
             }
-            const float base = m == -INFINITY ? 0.f : m;  // no key yet: keep 0, not NaN
             float pr[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) pr[r] = __builtin_amdgcn_exp2f(sv[r] - base);
+            for (int r = 0; r < 8; ++r) pr[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], scale, bm));
             lsum += ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
-            const Split2 ps = split2(pr, exp2i(kPExp));
+            const Split2 ps = split2(pr, 1.0f);
             const int pp = kb >> 1;
             o0 = mfma_x3(Split2{S.VS[pp][0][0][lane], S.VS[pp][0][1][lane]}, ps, o0);
             o1 = mfma_x3(Split2{S.VS[pp][1][0][lane], S.VS[pp][1][1][lane]}, ps, o1);
         }
         lsum = sum_cols(lsum);
-        const float down = exp2i(-(M.attn_ey + kPExp));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            o[r] = o0[r] * down;
-            o[4 + r] = o1[r] * down;
+            o[r] = o0[r];
+            o[4 + r] = o1[r];
         }
         return;
     }
@@ -516,11 +565,13 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
 #pragma unroll
         for (int s = 0; s < 4; ++s) o1 = mfma4(v1[s], pr[s], o1);
     }
-    lsum = sum_cols(lsum);
+    // the split-value form's scales (exact powers of two)
+    lsum = sum_cols(lsum) * exp2i(kPExp);
+    const float up = exp2i(M.attn_ey + kPExp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        o[r] = o0[r];
-        o[4 + r] = o1[r];
+        o[r] = o0[r] * up;
+        o[4 + r] = o1[r] * up;
     }
 }
 
@@ -536,21 +587,24 @@ __device__ inline int blocks_of_wave(int w, int nqb, int (&qb)[2]) {
 }
 
 // Copy the small per-layer parameters of n_layer blocks into LDS (layout PL;
-// attention biases in the folded form: attn_b[0, E) = g0, proj_b = bvp).
+// attention biases in the folded form: attn_b[0, E) = g0, proj_b = bvp).  The biases enter
+// the split products' accumulators, so they are stored at those products' scales (exact
+// powers of two): g0 and bvp x 2^(attn_ew + attn_ey), fc_b and mp_b x 2^(mlp_ew + mlp_ex).
 __device__ inline void load_layer_params(float* P, const ModelView& M, int tid, int nthreads) {
+    const float sa = exp2i(M.attn_ew + M.attn_ey), sm = exp2i(M.mlp_ew + M.mlp_ex);
     for (int i = tid; i < M.n_layer * PL::size; i += nthreads) {
         const int l = i / PL::size, k = i % PL::size;
         const float* Wg = M.layers + (size_t)l * LayerOff::size;
         float v;
         if (k < PL::ln1_b) v = Wg[LayerOff::ln1_g + k];
         else if (k < PL::attn_b) v = Wg[LayerOff::ln1_b + k - PL::ln1_b];
-        else if (k < PL::attn_b + kE) v = M.l0[(size_t)l * L0Off::size + L0Off::g0 + k - PL::attn_b];  // folded
-        else if (k < PL::proj_b) v = 0.f;                                                            // unused
-        else if (k < PL::ln2_g) v = M.l0[(size_t)l * L0Off::size + L0Off::bvp + k - PL::proj_b];     // folded
+        else if (k < PL::attn_b + kE) v = M.l0[(size_t)l * L0Off::size + L0Off::g0 + k - PL::attn_b] * sa;  // folded
+        else if (k < PL::proj_b) v = 0.f;                                                                 // unused
+        else if (k < PL::ln2_g) v = M.l0[(size_t)l * L0Off::size + L0Off::bvp + k - PL::proj_b] * sa;     // folded
         else if (k < PL::ln2_b) v = Wg[LayerOff::ln2_g + k - PL::ln2_g];
         else if (k < PL::fc_b) v = Wg[LayerOff::ln2_b + k - PL::ln2_b];
-        else if (k < PL::mp_b) v = Wg[LayerOff::fc_b + k - PL::fc_b];
-        else v = Wg[LayerOff::mp_b + k - PL::mp_b];
+        else if (k < PL::mp_b) v = Wg[LayerOff::fc_b + k - PL::fc_b] * sm;
+        else v = Wg[LayerOff::mp_b + k - PL::mp_b] * sm;
         P[i] = v;
     }
 }

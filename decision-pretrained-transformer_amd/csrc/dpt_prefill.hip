@@ -117,17 +117,14 @@ prefill_kernel(ModelView M, PrefillArgs a) {
         }
         bar_lds();
         if (nb > 0) {
-            float o[2][8];
+            float o[2][8], l[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 if (j >= nb) break;
-                float m, l;
-                attend(S, q[j], qb[j], 0, scale, m, l, o[j], M);
-                const float inv = 1.0f / l;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) o[j][k] *= inv;
+                float m;
+                attend(S, q[j], qb[j], 0, scale, m, l[j], o[j], M);
             }
-            DPT_BLOCKS(nb, attn_proj3<NB>(W, fs, o, x, M));
+            DPT_BLOCKS(nb, attn_proj3_ol<NB>(W, fs, o, l, x, M));
         }
         bar_lds();  // every read of this layer's K/V is done
         {
