@@ -66,6 +66,7 @@ int set_decode_tile(int);
 int set_darkroom_memo(int);
 int set_cache_budget(int64_t);
 int set_block0_mfma(int);
+int set_select_fast(int);
 int regret_max_steps();
 int64_t regret_workspace_numel(int N, int H);
 int launch_regret_moments(const double*, const double*, int, int, int, const double*, double*, double*, hipStream_t);
@@ -209,6 +210,10 @@ int dpt_tuning_set(int32_t key, int64_t value) {
     }
     if (key == DPT_TUNE_CACHE_BUDGET) {
         REQUIRE(set_cache_budget(value) == DPT_OK, "cache budget %lld B: >= 0", (long long)value);
+        return DPT_OK;
+    }
+    if (key == DPT_TUNE_SELECT_FAST) {
+        REQUIRE(set_select_fast((int)value) == DPT_OK, "select fast path %lld: 0 or 1", (long long)value);
         return DPT_OK;
     }
     if (key == DPT_TUNE_BLOCK0_MFMA) {

@@ -237,6 +237,60 @@ __device__ inline int select_from_cdf(const double* q, double u) {
     return idx < NA ? idx : NA - 1;
 }
 
+// The same selection with a fp32 fast path.  cdf_fast is the cdf in fp32 (q_k = prefix_k(e) /
+// sum(e), e_k = 2^((x_k - m) log2 e) on v_exp_f32); it is within about 1e-6 (absolute) of
+// cdf_fixed's fp64 values (the fp32 quotients and exponentials differ by a few ulp, and a term's
+// weight e_k / sum(e) shrinks faster than its argument's rounding grows).  Where every
+// |q_k - u| exceeds kCdfMargin = 2^-15 the comparisons q_k <= u therefore agree with cdf_fixed's,
+// and select_fast returns select_from_cdf's index without the fp64 work; otherwise (about 5e-4 of
+// the draws, NaN logits included) it runs cdf_fixed itself.  Bit-identical to select_fixed.
+constexpr float kCdfMargin = 1.0f / 32768.0f;
+template <int NA>
+__device__ inline void cdf_fast(const float (&lg)[NA], float temp, float (&q)[NA]) {
+    float xk[NA], e[NA];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        xk[k] = (temp == 1.0f) ? lg[k] : lg[k] / temp;
+        m = fmaxf(m, xk[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) e[k] = __builtin_amdgcn_exp2f((xk[k] - m) * 1.4426950408889634f);
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) tot += e[k];
+    const float r = __builtin_amdgcn_rcpf(tot);
+    float c = 0.f;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        c += e[k];
+        q[k] = c * r;
+    }
+}
+template <int NA>
+__device__ inline int select_fast(const float* q, const float (&lg)[NA], float temp, double u) {
+    const float uf = (float)u;
+    int idx = 0;
+    bool safe = true;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        idx += (q[k] <= uf) ? 1 : 0;
+        safe = safe && __builtin_fabsf(q[k] - uf) > kCdfMargin;  // false for NaN
+    }
+    if (safe) return idx < NA ? idx : NA - 1;
+    double qe[NA];
+    cdf_fixed<NA>(lg, temp, qe);
+    return select_from_cdf<NA>(qe, u);
+}
+// select_fixed through the fast path (bit-identical)
+template <int NA>
+__device__ inline int select_fixed_fast(const float (&lg)[NA], int sample, float temp, double u) {
+    if (!sample) return select_fixed<NA>(lg, 0, temp, u);
+    float q[NA];
+    cdf_fast<NA>(lg, temp, q);
+    return select_fast<NA>(q, lg, temp, u);
+}
+
 // Every block's attention folded (ModelView::l0, one L0Off block per layer,
 // derived at model creation by derive_l0_kernel): with y = LN1(h), q.k_s =
 // y_s . u + (terms constant over the keys s) for u = Wk q = y G + g0, and

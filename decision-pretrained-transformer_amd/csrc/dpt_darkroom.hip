@@ -113,7 +113,7 @@ struct alignas(16) DrSmem {
     float part_y[kFF / 32][kE];       // last layer: MLP partials per pair of hidden chunks
     // per-episode logits memo, one row per grid state (dim * dim <= kMemoStates)
     float memo_lg[kMemoStates][kDrA];
-    double memo_q[kMemoStates][kDrA];  // and their selection cdf (cdf_fixed), so a hit selects by 5 compares
+    float memo_q[kMemoStates][kDrA];   // and their fp32 selection cdf (cdf_fast): a hit selects by 5 compares
     // (no separate valid flag: an empty row holds memo_q[s][0] = -1 and memo_lg[s][0] = NaN, so a
     // hit is decided by the row's own values, read in one LDS round trip)
     double u_ep[kFwdT];                // this episode's selection uniforms, one per step
@@ -302,7 +302,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         // the tail thread's copy of the state and the episode's return (it runs every selection)
         int cur_x = 0, cur_y = 0, cur_ret = 0;
         for (int i = tid; i < kMemoStates; i += blockDim.x) {
-            S.memo_q[i][0] = -1.0;
+            S.memo_q[i][0] = -1.0f;
             S.memo_lg[i][0] = __builtin_nanf("");
         }
         // the episode's selection uniforms up front, one thread per step (off the serial
@@ -361,12 +361,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         // the policy's logits are a pure function of (window, query state) and the
         // window is fixed for the whole episode: a state queried before in this
         // episode reuses that forward's logits (bit-identical to re-running it)
-        // q: the selection cdf of lg (cdf_fixed) when sampling; select_from_cdf(q, u)
-        // equals select_fixed(lg, u) bit for bit
-        auto finish_step = [&](const float (&lg)[kDrA], const double* q, int t, int sx, int sy) {
+        // q: the fp32 selection cdf of lg (cdf_fast) when sampling; select_fast(q, lg, u) equals
+        // select_fixed(lg, u) bit for bit (the exact fp64 cdf decides within 2^-15 of an edge)
+        auto finish_step = [&](const float (&lg)[kDrA], const float* q, int t, int sx, int sy) {
             const int step = ep * p.horizon + t;
             const double u = p.sample ? S.u_ep[t] : 0.0;
-            const int a = p.sample ? select_from_cdf<kDrA>(q, u) : select_fixed<kDrA>(lg, 0, p.temp, u);
+            const int a = p.sample ? select_fast<kDrA>(q, lg, p.temp, u) : select_fixed<kDrA>(lg, 0, p.temp, u);
             const int ea = p.perms ? perm[a] : a;
             int nx = sx + (ea == 0) - (ea == 1);
             int ny = sy + (ea == 2) - (ea == 3);
@@ -393,15 +393,14 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     int tt = t;
                     while (tt < p.horizon) {
                         const int sidx = cur_x * p.dim + cur_y;
-                        float lg[kDrA];
-                        double qv[kDrA];
+                        float lg[kDrA], qv[kDrA];
 #pragma unroll
                         for (int k = 0; k < kDrA; ++k) {
                             lg[k] = S.memo_lg[sidx][k];
                             qv[k] = S.memo_q[sidx][k];
                         }
                         // a stored row: sampling reads its cdf (q[0] >= 0), greedy its logits
-                        if (p.sample ? !(qv[0] >= 0.0) : __builtin_isnan(lg[0])) break;
+                        if (p.sample ? !(qv[0] >= 0.0f) : __builtin_isnan(lg[0])) break;
                         finish_step(lg, qv, tt, cur_x, cur_y);
                         ++tt;
                     }
@@ -772,8 +771,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
                     DR_STAMP(2 * L + 2);
                     if (lane == 0) {
-                        double q[kDrA] = {0.0, 0.0, 0.0, 0.0, 0.0};
-                        if (p.sample) cdf_fixed<kDrA>(lg, p.temp, q);
+                        float q[kDrA] = {0.f, 0.f, 0.f, 0.f, 0.f};
+                        if (p.sample) cdf_fast<kDrA>(lg, p.temp, q);
                         if (p.memo) {
                             const int sidx = sx * p.dim + sy;
 #pragma unroll

@@ -1221,7 +1221,7 @@ __device__ inline int select_rollout(const float* logits, int A, int sample, dou
         float lg[NA];
 #pragma unroll
         for (int k = 0; k < NA; ++k) lg[k] = logits[k];
-        return select_fixed<NA>(lg, sample, 1.0f, u);
+        return select_fixed_fast<NA>(lg, sample, 1.0f, u);
     };
     if (A == 5) return fixed(std::integral_constant<int, 5>{});
     if (A == 20) return fixed(std::integral_constant<int, 20>{});

@@ -71,12 +71,22 @@ __global__ void darkroom_opt_kernel(const int32_t* __restrict__ state, const int
 
 __global__ void select_kernel(const float* __restrict__ logits, int N, int A, int sample, float temp,
                               const double* __restrict__ uniforms, uint64_t seed, uint64_t counter,
-                              int64_t first_task, int32_t* __restrict__ action) {
+                              int64_t first_task, int fast_path, int32_t* __restrict__ action) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     double u = 0.0;
     if (sample) u = uniforms ? uniforms[i] : philox_uniform(seed, counter, first_task + i, DPT_STREAM_SELECT);
-    action[i] = select_from_logits(logits + (size_t)i * A, A, sample, temp, u);
+    const float* lp = logits + (size_t)i * A;
+    auto fast = [&](auto na) {
+        constexpr int NA = decltype(na)::value;
+        float lg[NA];
+#pragma unroll
+        for (int k = 0; k < NA; ++k) lg[k] = lp[k];
+        return select_fixed_fast<NA>(lg, sample, temp, u);
+    };
+    if (fast_path && A == 5) action[i] = fast(std::integral_constant<int, 5>{});
+    else if (fast_path && A == 20) action[i] = fast(std::integral_constant<int, 20>{});
+    else action[i] = select_from_logits(lp, A, sample, temp, u);
 }
 
 // Materialise the Philox draws the library uses (tests, data-generation replay).
@@ -252,10 +262,18 @@ int launch_darkroom_opt(const int32_t* state, const int32_t* goal, const int32_t
     return check_hip(hipGetLastError(), "darkroom_opt_kernel launch");
 }
 
+static bool g_select_fast = true;  // DPT_TUNE_SELECT_FAST
+
+int set_select_fast(int on) {
+    if (on != 0 && on != 1) return DPT_EINVAL;
+    g_select_fast = on == 1;
+    return DPT_OK;
+}
+
 int launch_select(const float* logits, int N, int A, int sample, float temp, const double* uniforms,
                   uint64_t seed, uint64_t counter, int64_t first_task, int32_t* action, hipStream_t st) {
     hipLaunchKernelGGL(select_kernel, grid_for(N), dim3(kEnvThreads), 0, st, logits, N, A, sample, temp,
-                       uniforms, seed, counter, first_task, action);
+                       uniforms, seed, counter, first_task, g_select_fast ? 1 : 0, action);
     return check_hip(hipGetLastError(), "select_kernel launch");
 }
 

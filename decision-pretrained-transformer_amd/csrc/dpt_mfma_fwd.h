@@ -125,11 +125,15 @@ struct Frag3 {
 struct FragSrc3 {
     __amdgpu_buffer_rsrc_t r;
     int base;  // byte offset of this layer's tiles
-    __device__ halfx8 ld1(int tile, int part) const {
+    // the lane's byte offset inside a tile: a helper that loads several tiles computes it once
+    // (three VALU instructions per load otherwise, from the opaque lane_id)
+    __device__ static int lane_off() { return lane_id() * 16; }
+    __device__ halfx8 ld1(int tile, int part, int vo) const {
         return __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(
-                                              r, lane_id() * 16, base + (tile * Frag3::parts + part) * 1024, 0));
+                                              r, vo, base + (tile * Frag3::parts + part) * 1024, 0));
     }
-    __device__ Split2 ld2(int tile) const { return Split2{ld1(tile, 0), ld1(tile, 1)}; }
+    __device__ Split2 ld2(int tile, int vo) const { return Split2{ld1(tile, 0, vo), ld1(tile, 1, vo)}; }
+    __device__ Split2 ld2(int tile) const { return ld2(tile, lane_off()); }
     __device__ FragSrc3 layer(int l) const { return FragSrc3{r, l * Frag3::bytes}; }
 };
 
@@ -212,9 +216,7 @@ __device__ inline float gelu_fast(float x) {
 // included) every scale is an exact power of two folded into a constant:
 //   gelu(h) 2^ex = y / ((1 + 2^t) 2^ew),  t = h (c1 + c2 h^2) = y (c1' + c2' y^2),
 //   c1' = c1 2^-(ew+ex), c2' = c2 2^-3(ew+ex)
-// and the quotient's multiply rounds straight into the fp16 parts (v_fma_mix: hi = f16(y r),
-// lo = f16(y r - hi), each one rounding).  Six VALU slots and two transcendentals per value
-// instead of the eleven of scale-down, gelu_fast, scale-up and split2.  fwd_scales keeps
+// so the scale-down before gelu and the scale-up of split2 vanish.  fwd_scales keeps
 // ew + ex >= -40, so c2' stays a normal fp32 number.
 struct GeluSplit {
     float c1, c2, s;
@@ -226,16 +228,22 @@ struct GeluSplit {
     }
 };
 __device__ inline Split2 gelu_split(const floatx4& a, const floatx4& b, const GeluSplit& k) {
-    const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    // pairs on the packed f32 ops (v_pk_mul / v_pk_fma: two values per issue, each rounded like
+    // the scalar op); hi from one v_cvt_pk_f16_f32 per pair, lo = f16(g - hi) by v_fma_mix as split2
+    float one = 1.0f;
+    asm volatile("" : "+s"(one));
+    const floatx2 c1 = {k.c1, k.c1}, c2 = {k.c2, k.c2}, sv = {k.s, k.s};
     unsigned hh[4], mm[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-        const float y0 = v[2 * p], y1 = v[2 * p + 1];
-        const float t0 = fmaf(y0 * y0, k.c2, k.c1) * y0, t1 = fmaf(y1 * y1, k.c2, k.c1) * y1;
-        const float r0 = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(t0), k.s, k.s));
-        const float r1 = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(t1), k.s, k.s));
-        const halfx2 h = {(_Float16)__builtin_fmaf(y0, r0, 0.0f), (_Float16)__builtin_fmaf(y1, r1, 0.0f)};
-        const halfx2 m = {(_Float16)__builtin_fmaf(y0, r0, -(float)h.x), (_Float16)__builtin_fmaf(y1, r1, -(float)h.y)};
+        const floatx2 y = p < 2 ? floatx2{a[2 * p], a[2 * p + 1]} : floatx2{b[2 * p - 4], b[2 * p - 3]};
+        const floatx2 t = __builtin_elementwise_fma(y * y, c2, c1) * y;
+        const floatx2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+        const floatx2 d = __builtin_elementwise_fma(e, sv, sv);
+        const floatx2 g = y * floatx2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+        const halfx2 h = __builtin_convertvector(g, halfx2);
+        const halfx2 m = {(_Float16)__builtin_fmaf(g.x, one, -(float)h.x),
+                          (_Float16)__builtin_fmaf(g.y, one, -(float)h.y)};
         hh[p] = __builtin_bit_cast(unsigned, h);
         mm[p] = __builtin_bit_cast(unsigned, m);
     }
@@ -247,6 +255,21 @@ template <int NB>
 __device__ inline void ln_n(const float (&x)[2][8], float (&xn)[2][8], const float* gam, const float* bet) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) ln_cols(x[j], xn[j], gam, bet);
+}
+
+// x += (a | b) x down, down an exact power of two: one packed fma per pair (the product is exact,
+// so each result equals x + a down rounded once, as the separate multiply and add)
+__device__ inline void resid_add(float (&x)[8], const floatx4& a, const floatx4& b, float down) {
+    const floatx2 dd = {down, down};
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+        const floatx2 u = __builtin_elementwise_fma(floatx2{a[r], a[r + 1]}, dd, floatx2{x[r], x[r + 1]});
+        const floatx2 v = __builtin_elementwise_fma(floatx2{b[r], b[r + 1]}, dd, floatx2{x[4 + r], x[5 + r]});
+        x[r] = u.x;
+        x[r + 1] = u.y;
+        x[4 + r] = v.x;
+        x[5 + r] = v.y;
+    }
 }
 
 // x^T += MLP(xn^T) on fp16 two-part products (mfma_x3): c_fc per 16-unit chunk, mlp.c_proj
@@ -266,10 +289,11 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
     for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], xs_scale);
     // c_fc tiles one pair ahead (in flight across the pair's gelu + c_proj products), the
     // pair's c_proj tiles at its start (in flight across its c_fc + gelu)
-    Split2 wf0 = f3.ld2(Frag3::fc), wf1 = f3.ld2(Frag3::fc + 1);
+    const int vo = FragSrc3::lane_off();
+    Split2 wf0 = f3.ld2(Frag3::fc, vo), wf1 = f3.ld2(Frag3::fc + 1, vo);
 #pragma unroll
     for (int p = 0; p < kFF / 32; ++p) {
-        const Split2 w0 = f3.ld2(Frag3::mp + p), w1 = f3.ld2(Frag3::mp + 4 + p);
+        const Split2 w0 = f3.ld2(Frag3::mp + p, vo), w1 = f3.ld2(Frag3::mp + 4 + p, vo);
         Split2 gs[2];
         const floatx4 fb0 = ld4(W + PL::fc_b + 2 * p * 16 + 4 * g);
         const floatx4 fb1 = ld4(W + PL::fc_b + (2 * p + 1) * 16 + 4 * g);
@@ -277,8 +301,8 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
         for (int j = 0; j < NB; ++j)
             gs[j] = gelu_split(mfma_x3(wf0, xs[j], fb0), mfma_x3(wf1, xs[j], fb1), gk);
         if (p + 1 < kFF / 32) {
-            wf0 = f3.ld2(Frag3::fc + 2 * p + 2);
-            wf1 = f3.ld2(Frag3::fc + 2 * p + 3);
+            wf0 = f3.ld2(Frag3::fc + 2 * p + 2, vo);
+            wf1 = f3.ld2(Frag3::fc + 2 * p + 3, vo);
         }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -287,14 +311,7 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
         }
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-        const floatx4 d0 = y0[j] * down, d1 = y1[j] * down;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            x[j][r] += d0[r];
-            x[j][4 + r] += d1[r];
-        }
-    }
+    for (int j = 0; j < NB; ++j) resid_add(x[j], y0[j], y1[j], down);
 }
 
 // u = xn G + g0 of the NB blocks (the folded c_attn: only its q part) on fp16 two-part
@@ -303,11 +320,11 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
 template <int NB>
 __device__ inline void u_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&xs)[2], float (&q)[2][8],
                                  const ModelView& M) {
-    const int g = lane_id() >> 4;
+    const int g = lane_id() >> 4, vo = FragSrc3::lane_off();
     const float down = exp2i(-(M.attn_ew + M.attn_ey));
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
-        const Split2 w = f3.ld2(Frag3::attn + ob);
+        const Split2 w = f3.ld2(Frag3::attn + ob, vo);
         const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);  // scaled (PL)
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -331,19 +348,12 @@ __device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float
 template <int NB>
 __device__ inline void attn_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&os)[2], float (&x)[2][8],
                                     const ModelView& M) {
-    const int g = lane_id() >> 4;
+    const int g = lane_id() >> 4, vo = FragSrc3::lane_off();
     const float down = exp2i(-(M.attn_ew + M.attn_ey));
+    const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
+    const floatx4 b0 = ld4(W + PL::proj_b + 4 * g), b1 = ld4(W + PL::proj_b + 16 + 4 * g);  // scaled (PL)
 #pragma unroll
-    for (int ob = 0; ob < 2; ++ob) {
-        const Split2 w = f3.ld2(Frag3::proj + ob);
-        const floatx4 bias = ld4(W + PL::proj_b + ob * 16 + 4 * g);  // scaled (PL)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const floatx4 acc = mfma_x3(w, os[j], bias) * down;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) x[j][ob * 4 + r] += acc[r];
-        }
-    }
+    for (int j = 0; j < NB; ++j) resid_add(x[j], mfma_x3(w0, os[j], b0), mfma_x3(w1, os[j], b1), down);
 }
 template <int NB>
 __device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8],
@@ -464,12 +474,14 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         lsum = 0.f;
         float thr = -INFINITY, bm = 0.f;  // bm = 0 while no key (not NaN)
         floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-        for (int kb = 0; kb <= qb; kb += 2) {
+        // one pair of key tiles; MASKED only for the pair holding the diagonal tile (and the
+        // pair holding key_lo): the others need neither the causal nor the key_lo test
+        auto pair = [&](const int kb, auto masked) {
             float sv[8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int kt = kb + h;
-                if (kt > qb) {  // wave-uniform
+                if (decltype(masked)::value && kt > qb) {  // wave-uniform
 #pragma unroll
                     for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
                     continue;
@@ -478,7 +490,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
                 const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
                 for (int r = 0; r < 4; ++r) sv[4 * h + r] = sc[r];
-                if (kt == qb || kt * 16 < key_lo) {  // wave-uniform
+                if constexpr (decltype(masked)::value) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         if ((kt == qb && 4 * g + r > c) || kt * 16 + 4 * g + r < key_lo) sv[4 * h + r] = -INFINITY;
@@ -501,13 +513,28 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
             }
             float pr[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) pr[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], scale, bm));
-            lsum += ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
+            for (int r = 0; r < 8; r += 2) {
+                const floatx2 a2 = __builtin_elementwise_fma(floatx2{sv[r], sv[r + 1]}, floatx2{scale, scale},
+                                                             floatx2{bm, bm});
+                pr[r] = __builtin_amdgcn_exp2f(a2.x);
+                pr[r + 1] = __builtin_amdgcn_exp2f(a2.y);
+            }
+            const floatx2 l2 = (floatx2{pr[0], pr[1]} + floatx2{pr[2], pr[3]}) +
+                               (floatx2{pr[4], pr[5]} + floatx2{pr[6], pr[7]});
+            lsum += l2.x + l2.y;
             const Split2 ps = split2(pr, 1.0f);
             const int pp = kb >> 1;
             o0 = mfma_x3(Split2{S.VS[pp][0][0][lane], S.VS[pp][0][1][lane]}, ps, o0);
             o1 = mfma_x3(Split2{S.VS[pp][1][0][lane], S.VS[pp][1][1][lane]}, ps, o1);
+        };
+        const int kb_last = qb & ~1;  // the pair holding the diagonal tile
+        int kb = 0;
+        if (key_lo > 0 && kb_last > 0) {
+            pair(0, std::true_type{});
+            kb = 2;
         }
+        for (; kb < kb_last; kb += 2) pair(kb, std::false_type{});
+        pair(kb_last, std::true_type{});
         lsum = sum_cols(lsum);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

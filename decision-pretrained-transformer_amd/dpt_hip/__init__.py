@@ -399,6 +399,12 @@ def set_block0_mfma(on):
     _lib.call("dpt_tuning_set", _lib.TUNE_BLOCK0_MFMA, int(bool(on)))
 
 
+def set_select_fast(on):
+    """select_action for 5 and 20 arms: the fp32 cdf with the exact fp64 cdf within 2^-15 of an edge
+    (default), or the fp64 cdf for every sample.  Bit-identical either way."""
+    _lib.call("dpt_tuning_set", _lib.TUNE_SELECT_FAST, int(bool(on)))
+
+
 _darkroom_memo = True
 _darkroom_ws = True
 

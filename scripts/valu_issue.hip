@@ -1,0 +1,121 @@
+// Microbenchmark (diagnostic, not product code): issue cost per instruction on gfx950 of the
+// VALU forms the DarkRoom forward uses -- scalar f32, packed f32, transcendental, fp16
+// conversions and v_fma_mix -- alone and interleaved with v_mfma_f32_16x16x32_f16, at one and
+// two waves per SIMD.  Each wave runs an unrolled block of independent instructions in a loop;
+// the cycle count is s_memtime around the loop (max over waves), reported per instruction.
+// Build: hipcc --offload-arch=gfx950 -O3 scripts/valu_issue.hip -o scripts/valu_issue
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+#define R8(X) X X X X X X X X
+constexpr int kIters = 2048;
+
+// 8 independent instructions of the form given, on registers v[0..7] (and v[8..15] as inputs)
+#define BODY_MUL asm volatile(R8("v_mul_f32 %0, %0, %1\n") : "+v"(a0) : "v"(b0));
+template <int K>
+__global__ void __launch_bounds__(512) kern(unsigned long long* out, float seed) {
+    float a[16], b[16];
+    for (int i = 0; i < 16; ++i) {
+        a[i] = seed * (threadIdx.x + i);
+        b[i] = seed + i;
+    }
+    floatx4 acc[4] = {};
+    halfx8 ha, hb;
+    for (int i = 0; i < 8; ++i) {
+        ha[i] = (_Float16)(seed * i);
+        hb[i] = (_Float16)(seed + i);
+    }
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < kIters; ++it) {
+#define V(i) "v"(a[i])
+        if constexpr (K == 0) {  // 16 v_mul_f32
+            asm volatile(
+                "v_mul_f32 %0, %0, %16\n v_mul_f32 %1, %1, %16\n v_mul_f32 %2, %2, %16\n v_mul_f32 %3, %3, %16\n"
+                "v_mul_f32 %4, %4, %16\n v_mul_f32 %5, %5, %16\n v_mul_f32 %6, %6, %16\n v_mul_f32 %7, %7, %16\n"
+                "v_mul_f32 %8, %8, %16\n v_mul_f32 %9, %9, %16\n v_mul_f32 %10, %10, %16\n v_mul_f32 %11, %11, %16\n"
+                "v_mul_f32 %12, %12, %16\n v_mul_f32 %13, %13, %16\n v_mul_f32 %14, %14, %16\n v_mul_f32 %15, %15, %16\n"
+                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]),
+                  "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
+                : "v"(b[0]));
+        }
+        if constexpr (K == 1 || K == 5) {  // 8 v_pk_mul_f32 (16 values)
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            f2* p = reinterpret_cast<f2*>(a);
+            f2 q = {b[0], b[1]};
+            asm volatile(
+                "v_pk_mul_f32 %0, %0, %8\n v_pk_mul_f32 %1, %1, %8\n v_pk_mul_f32 %2, %2, %8\n v_pk_mul_f32 %3, %3, %8\n"
+                "v_pk_mul_f32 %4, %4, %8\n v_pk_mul_f32 %5, %5, %8\n v_pk_mul_f32 %6, %6, %8\n v_pk_mul_f32 %7, %7, %8\n"
+                : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3]), "+v"(p[4]), "+v"(p[5]), "+v"(p[6]), "+v"(p[7])
+                : "v"(q));
+        }
+        if constexpr (K == 2 || K == 6) {  // 8 v_exp_f32
+            asm volatile(
+                "v_exp_f32 %0, %0\n v_exp_f32 %1, %1\n v_exp_f32 %2, %2\n v_exp_f32 %3, %3\n"
+                "v_exp_f32 %4, %4\n v_exp_f32 %5, %5\n v_exp_f32 %6, %6\n v_exp_f32 %7, %7\n"
+                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]));
+        }
+        if constexpr (K == 3 || K == 7) {  // 8 v_fma_mixlo_f16
+            asm volatile(
+                "v_fma_mixlo_f16 %0, %8, %9, 0\n v_fma_mixlo_f16 %1, %8, %9, 0\n v_fma_mixlo_f16 %2, %8, %9, 0\n"
+                "v_fma_mixlo_f16 %3, %8, %9, 0\n v_fma_mixlo_f16 %4, %8, %9, 0\n v_fma_mixlo_f16 %5, %8, %9, 0\n"
+                "v_fma_mixlo_f16 %6, %8, %9, 0\n v_fma_mixlo_f16 %7, %8, %9, 0\n"
+                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
+                : "v"(b[0]), "v"(b[1]));
+        }
+        if constexpr (K == 8 || K == 9) {  // 8 v_cvt_pk_f16_f32
+            asm volatile(
+                "v_cvt_pk_f16_f32 %0, %8, %9\n v_cvt_pk_f16_f32 %1, %8, %9\n v_cvt_pk_f16_f32 %2, %8, %9\n"
+                "v_cvt_pk_f16_f32 %3, %8, %9\n v_cvt_pk_f16_f32 %4, %8, %9\n v_cvt_pk_f16_f32 %5, %8, %9\n"
+                "v_cvt_pk_f16_f32 %6, %8, %9\n v_cvt_pk_f16_f32 %7, %8, %9\n"
+                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
+                : "v"(b[0]), "v"(b[1]));
+        }
+        if constexpr (K == 10) {  // 8 v_mul_f32 (to pair with MFMAs)
+            asm volatile(
+                "v_mul_f32 %0, %0, %8\n v_mul_f32 %1, %1, %8\n v_mul_f32 %2, %2, %8\n v_mul_f32 %3, %3, %8\n"
+                "v_mul_f32 %4, %4, %8\n v_mul_f32 %5, %5, %8\n v_mul_f32 %6, %6, %8\n v_mul_f32 %7, %7, %8\n"
+                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
+                : "v"(b[0]));
+        }
+        if constexpr (K >= 4) {  // + 4 independent v_mfma_f32_16x16x32_f16
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[j], 0, 0, 0);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    float s = 0.f;
+    for (int i = 0; i < 16; ++i) s += a[i];
+    for (int j = 0; j < 4; ++j) s += acc[j][0];
+    if (s == 12345.f) out[1] = 1;  // keep the work
+    if ((threadIdx.x & 63) == 0) atomicMax(out, t1 - t0);
+}
+
+int main() {
+    unsigned long long* d;
+    (void)hipMalloc(&d, 16);
+    const char* names[] = {"16 v_mul_f32", "8 v_pk_mul_f32", "8 v_exp_f32", "8 v_fma_mixlo_f16",
+                           "4 mfma16x16x32f16 alone", "4 mfma + 8 v_pk_mul_f32", "4 mfma + 8 v_exp_f32",
+                           "4 mfma + 8 v_fma_mixlo_f16", "8 v_cvt_pk_f16_f32", "4 mfma + 8 v_cvt_pk_f16_f32",
+                           "4 mfma + 8 v_mul_f32"};
+    void (*ks[])(unsigned long long*, float) = {kern<0>, kern<1>, kern<2>, kern<3>, kern<4>, kern<5>,
+                                                kern<6>, kern<7>, kern<8>, kern<9>, kern<10>};
+    for (int waves_per_simd = 1; waves_per_simd <= 2; ++waves_per_simd) {
+        for (int k = 0; k < 11; ++k) {
+            unsigned long long h = 0;
+            (void)hipMemset(d, 0, 16);
+            // one workgroup per CU-sized slot: 4 or 8 waves (1 or 2 per SIMD)
+            hipLaunchKernelGGL(ks[k], dim3(256), dim3(256 * waves_per_simd), 0, 0, d, 1.0001f);
+            (void)hipMemset(d, 0, 16);
+            hipLaunchKernelGGL(ks[k], dim3(256), dim3(256 * waves_per_simd), 0, 0, d, 1.0001f);
+            (void)hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+            printf("{\"waves_per_simd\": %d, \"block\": \"%s\", \"cycles_per_iter\": %.2f}\n", waves_per_simd,
+                   names[k], (double)h / kIters);
+        }
+    }
+    return 0;
+}

@@ -117,6 +117,38 @@ def test_select_action_matches_reference():
     assert np.array_equal(got[ok], ref[ok])
 
 
+def test_select_fast_path_equals_fp64_cdf():
+    """select_fast (fp32 cdf, exact fp64 cdf within 2^-15 of an edge; the rollouts' selection)
+    against the fp64-only path on adversarial draws: uniforms placed 1e-9 .. 1e-3 either side of
+    every cdf edge, logit spreads up to 60, temperature 1 and 0.5, NaN rows.  Bit-identical."""
+    d = dh()
+    rs = np.random.RandomState(11)
+    for A in (5, 20):
+        for spread in (0.1, 3.0, 20.0, 60.0):
+            lg = (rs.randn(4096, A) * spread).astype(np.float32)
+            lg[::97] = lg[::97, :1]  # ties
+            for temp in (1.0, 0.5):
+                cdf = np.cumsum(O.softmax_f32(lg, temp).astype(np.float64), -1)
+                cdf /= cdf[:, -1:]
+                k = rs.randint(0, A - 1, 4096)
+                delta = rs.choice([1e-9, 1e-7, 1e-6, 1e-5, 3e-5, 1e-4, 1e-3], 4096) * rs.choice([-1, 1], 4096)
+                u = np.clip(cdf[np.arange(4096), k] + delta, 0.0, np.nextafter(1.0, 0.0))
+                u[::5] = rs.uniform(0, 1, u[::5].shape)
+                lgn = lg.copy()
+                lgn[::211, 1] = np.nan
+                for logits in (lgn, lg):
+                    d.set_select_fast(False)
+                    ref = d.select_action(logits, True, temp=temp, uniforms=u).cpu().numpy()
+                    d.set_select_fast(True)
+                    got = d.select_action(logits, True, temp=temp, uniforms=u).cpu().numpy()
+                    assert np.array_equal(got, ref), (A, spread, temp, np.nonzero(got != ref)[0][:10])
+                # and the reference's own selection away from the edges (numpy's expf is not
+                # correctly rounded, so nearer than 1e-5 only the device paths are compared)
+                ok = O.boundary_margin(O.softmax_f32(lg, temp), u) > 1e-5
+                assert np.array_equal(got[ok], O.select_actions(lg, u, True, temp=temp)[ok])
+    d.set_select_fast(True)
+
+
 @pytest.mark.parametrize("name", ["bandit5", "darkroom", "linear20"])
 def test_forward_window_logits(name):
     g, m, W = model_from_golden(name)
