@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(512) kern(unsigned long long* out, float seed)
                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
                 : "v"(b[0]));
         }
-        if constexpr (K >= 4) {  // + 4 independent v_mfma_f32_16x16x32_f16
+        if constexpr (K >= 4 && K != 8) {  // + 4 independent v_mfma_f32_16x16x32_f16
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[j], 0, 0, 0);
         }
