@@ -219,9 +219,10 @@ def main():
         cfg = {"tasks_per_gpu": N, "horizon": H, "episodes": Heps}
         # rollout_darkroom_kernel: every matrix product as fp16 two-part splits on
         # v_mfma_f32_16x16x32_f16 (h*h + h*m + m*h, fp32 accumulation: about 2^-21 relative per
-        # product); LayerNorm, softmax, gelu, embedding, head in fp32; cdf in fp64
+        # product); LayerNorm, softmax, gelu, embedding, head in fp32; selection cdf in fp32
+        # (the exact fp64 cdf within 2^-15 of an edge, select_fast)
         dtype = ("f16x2-split MFMA products (fp32 accumulate, ~2^-21/product) + f32 VALU / "
-                 "f64 selection cdf; int32 grid")
+                 "f32 selection cdf (f64 within 2^-15 of an edge); int32 grid")
 
     for w in range(args.warmup):
         one(w)
