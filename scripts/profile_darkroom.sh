@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 TAG=${1:-r1}
 OUT=gpurun_out/prof_dr_$TAG
 mkdir -p $OUT
-BENCH="bench.py --workload darkroom"
+BENCH="bench.py --workload darkroom --no-cpu-baseline"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run -- \
     python3 $BENCH --steps 2 --warmup 1 > $OUT/bench_trace.log 2>&1 || exit $?
 pass() {
