@@ -249,11 +249,19 @@ template <int NA>
 __device__ inline void cdf_fast(const float (&lg)[NA], float temp, float (&q)[NA]) {
     float xk[NA], e[NA];
     float m = -INFINITY;
+    // temp is uniform: a real branch, so the IEEE divisions (a dozen instructions each, on the
+    // tail's serial chain) run only when temp != 1 (the empty asm keeps the compiler from
+    // computing both sides and selecting)
+    if (temp == 1.0f) {
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
-        xk[k] = (temp == 1.0f) ? lg[k] : lg[k] / temp;
-        m = fmaxf(m, xk[k]);
+        for (int k = 0; k < NA; ++k) xk[k] = lg[k];
+    } else {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < NA; ++k) xk[k] = lg[k] / temp;
     }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) m = fmaxf(m, xk[k]);
 #pragma unroll
     for (int k = 0; k < NA; ++k) e[k] = __builtin_amdgcn_exp2f((xk[k] - m) * 1.4426950408889634f);
     float tot = 0.f;
