@@ -9,8 +9,7 @@
 // pairwise summation), so the per-arm reward lists are kept in a workspace laid
 // out [arm][k][task] (lane-contiguous: coalesced) and summed with numpy's
 // pairwise order each step: means, bounds and therefore action indices are
-// bit-identical to the reference for the same draws (LinUCB excepted: its 2x2
-// inverse is LAPACK's in the reference, closed-form here).
+// bit-identical to the reference for the same draws (LinUCB: see linucb_choose).
 #include "dpt_common.h"
 
 namespace dpt {
@@ -66,6 +65,176 @@ __device__ double pw_sum(const double* x, size_t stride, int n) {
 
 constexpr int kMaxD = 8;  // LinUCB feature dimension (lin_d) supported
 
+// ----------------------------------------------------------------------------- LinUCB
+// LinUCBPolicy.act_numpy_vec (ctrls/ctrl_bandit.py:503-526) rebuilds its estimate from the
+// whole context every step with numpy:
+//   X = arms[argmax(actions)]; cov = I + X^T X; cov_inv = np.linalg.inv(cov)
+//   theta = (cov_inv @ X^T) @ r; value_k = theta @ arm_k + c * sqrt(arm_k @ cov_inv @ arm_k)
+// numpy hands each product to its BLAS (OpenBLAS, scipy-openblas 0.3.29 in the image the
+// fixtures were recorded in) and each of those kernels has its own, fixed rounding order.  The
+// lane restates those orders (established against numpy on the recording host:
+// tests/golden/gen_golden.py linucb fixtures), so at lin_d = 2 every value -- and so every arm
+// index -- is bit-identical to the reference's:
+//   X^T X  dsyrk: per entry one fma chain over the context, K-blocked like the level-3 driver
+//          (blocks of GEMM_Q = 384, a remainder between Q and 2Q split in halves), C += block;
+//   inv    dgesv(cov, I): getf2 (partial pivot by first max |.|, l = a10 * (1/a00), u11 =
+//          a11 - l u01 unfused) then getrs (unit-lower forward step, upper back step with the
+//          reciprocal diagonal, the off-diagonal term fused);
+//   cov_inv @ X^T  dgemm with K = d: per entry an fma chain from 0;
+//   (.) @ r  dgemv_t: 2048-row blocks of the first n - n%4 rows, two interleaved unfused
+//          accumulators per block summed into y, then the n%4 tail rows contracted into y;
+//   theta @ arm, arm @ cov_inv, (.) @ arm  ddot / dgemv_n with d rows: fma chains from 0.
+// For lin_d > 2 the inverse is a plain partial-pivot LU and the d-column kernels are not
+// restated (OpenBLAS switches to its 4-column microkernels), so indices there are equal up to
+// near-ties of the arm values.
+constexpr int kSyrkQ = 384;
+__host__ __device__ inline int syrk_block(int ls, int n) {
+    const int ml = n - ls;
+    if (ml >= 2 * kSyrkQ) return kSyrkQ;
+    if (ml > kSyrkQ) return (ml + 1) / 2;
+    return ml;
+}
+
+// dgemv_t row reduction y = sum_k m(k) r(k) over k < n in OpenBLAS's order (see above)
+template <class Mk, class Rk>
+__host__ __device__ inline double gemv_t_sum(Mk m, Rk r, int n) {
+    const int m3 = n & 3, m1 = n - m3;
+    double y = 0.0;
+    for (int s0 = 0; s0 < m1; s0 += 2048) {
+        const int nb = min(2048, m1 - s0);
+        double l0 = 0.0, l1 = 0.0;
+        for (int k = s0; k < s0 + nb; k += 2) {
+            l0 = l0 + m(k) * r(k);
+            l1 = l1 + m(k + 1) * r(k + 1);
+        }
+        y = y + (l0 + l1);
+    }
+    if (m3 == 1) {
+        y = fma(m(m1), r(m1), y);
+    } else if (m3 == 2) {
+        y = y + fma(m(m1), r(m1), m(m1 + 1) * r(m1 + 1));
+    } else if (m3 == 3) {
+        y = y + fma(m(m1 + 2), r(m1 + 2), fma(m(m1), r(m1), m(m1 + 1) * r(m1 + 1)));
+    }
+    return y;
+}
+
+// One LinUCB decision from the n-transition context (arm indices act(k), rewards rew(k), time
+// order).  arms (A, d) row-major.
+template <class Act, class Rew>
+__host__ __device__ int linucb_choose(Act act, Rew rew, int n, const double* arms, int A, int d, double c) {
+    // cov = I + X^T X (upper triangle, mirrored like numpy's syrk result)
+    double cov[kMaxD * kMaxD];
+    for (int p = 0; p < d; ++p)
+        for (int q = p; q < d; ++q) cov[p * kMaxD + q] = 0.0;
+    for (int ls = 0; ls < n;) {
+        const int ml = syrk_block(ls, n);
+        double acc[kMaxD * kMaxD];
+        for (int p = 0; p < d; ++p)
+            for (int q = p; q < d; ++q) acc[p * kMaxD + q] = 0.0;
+        for (int k = ls; k < ls + ml; ++k) {
+            const double* x = arms + (size_t)act(k) * d;
+            for (int p = 0; p < d; ++p)
+                for (int q = p; q < d; ++q) acc[p * kMaxD + q] = fma(x[p], x[q], acc[p * kMaxD + q]);
+        }
+        for (int p = 0; p < d; ++p)
+            for (int q = p; q < d; ++q) cov[p * kMaxD + q] = cov[p * kMaxD + q] + acc[p * kMaxD + q];
+        ls += ml;
+    }
+    for (int p = 0; p < d; ++p) {
+        cov[p * kMaxD + p] = 1.0 + cov[p * kMaxD + p];
+        for (int q = p + 1; q < d; ++q) {
+            cov[p * kMaxD + q] = 0.0 + cov[p * kMaxD + q];
+            cov[q * kMaxD + p] = cov[p * kMaxD + q];
+        }
+    }
+    double ci[kMaxD * kMaxD];
+    if (d == 2) {
+        const bool sw = fabs(cov[kMaxD]) > fabs(cov[0]);  // idamax: the first max
+        const double a00 = sw ? cov[kMaxD] : cov[0], a01 = sw ? cov[kMaxD + 1] : cov[1];
+        const double a10 = sw ? cov[0] : cov[kMaxD], a11 = sw ? cov[1] : cov[kMaxD + 1];
+        const double l = a10 * (1.0 / a00);
+        const double u11 = a11 - l * a01;
+        const double r00 = 1.0 / a00, r11 = 1.0 / u11;
+        for (int col = 0; col < 2; ++col) {
+            const double b0 = (sw ? 1 : 0) == col ? 1.0 : 0.0, b1 = (sw ? 0 : 1) == col ? 1.0 : 0.0;
+            const double y1 = b1 - l * b0;
+            const double x1 = y1 * r11;
+            const double x0 = fma(-a01, x1, b0) * r00;
+            ci[col] = x0;
+            ci[kMaxD + col] = x1;
+        }
+    } else {
+        // LU with partial pivoting (reciprocal pivots, LAPACK style), then the d unit columns
+        double lu[kMaxD * kMaxD];
+        int piv[kMaxD];
+        for (int k = 0; k < d * kMaxD; ++k) lu[k] = cov[k];
+        for (int j = 0; j < d; ++j) {
+            int pr = j;
+            for (int p = j + 1; p < d; ++p)
+                if (fabs(lu[p * kMaxD + j]) > fabs(lu[pr * kMaxD + j])) pr = p;
+            piv[j] = pr;
+            if (pr != j)
+                for (int q = 0; q < d; ++q) {
+                    const double t = lu[j * kMaxD + q];
+                    lu[j * kMaxD + q] = lu[pr * kMaxD + q];
+                    lu[pr * kMaxD + q] = t;
+                }
+            const double rp = 1.0 / lu[j * kMaxD + j];
+            for (int p = j + 1; p < d; ++p) {
+                const double lf = lu[p * kMaxD + j] * rp;
+                lu[p * kMaxD + j] = lf;
+                for (int q = j + 1; q < d; ++q) lu[p * kMaxD + q] = lu[p * kMaxD + q] - lf * lu[j * kMaxD + q];
+            }
+        }
+        for (int col = 0; col < d; ++col) {
+            double b[kMaxD];
+            for (int p = 0; p < d; ++p) b[p] = p == col ? 1.0 : 0.0;
+            for (int j = 0; j < d; ++j) {
+                const double t = b[j];
+                b[j] = b[piv[j]];
+                b[piv[j]] = t;
+            }
+            for (int p = 1; p < d; ++p)
+                for (int q = 0; q < p; ++q) b[p] = fma(-lu[p * kMaxD + q], b[q], b[p]);
+            for (int p = d - 1; p >= 0; --p) {
+                double t = b[p];
+                for (int q = p + 1; q < d; ++q) t = fma(-lu[p * kMaxD + q], b[q], t);
+                b[p] = t * (1.0 / lu[p * kMaxD + p]);
+            }
+            for (int p = 0; p < d; ++p) ci[p * kMaxD + col] = b[p];
+        }
+    }
+    // theta = (cov_inv @ X^T) @ r
+    double theta[kMaxD];
+    for (int p = 0; p < d; ++p) {
+        const double* cp = ci + p * kMaxD;
+        auto mk = [&](int k) {
+            const double* x = arms + (size_t)act(k) * d;
+            double acc = cp[0] * x[0];
+            for (int j = 1; j < d; ++j) acc = fma(cp[j], x[j], acc);
+            return acc;
+        };
+        theta[p] = gemv_t_sum(mk, rew, n);
+    }
+    int best_k = 0;
+    double best = -INFINITY;
+    for (int k = 0; k < A; ++k) {
+        const double* x = arms + (size_t)k * d;
+        double tv = theta[0] * x[0];
+        for (int p = 1; p < d; ++p) tv = fma(theta[p], x[p], tv);
+        double qv = 0.0;
+        for (int j = 0; j < d; ++j) {
+            double w = ci[j] * x[0];
+            for (int p = 1; p < d; ++p) w = fma(ci[p * kMaxD + j], x[p], w);
+            qv = j == 0 ? w * x[0] : fma(w, x[j], qv);
+        }
+        const double v = tv + c * sqrt(qv);
+        if (v > best) { best = v; best_k = k; }
+    }
+    return best_k;
+}
+
 struct PolicyParams {
     int N, H, A, policy, online, type, sample, d, C, step0;
     const int32_t* ctx_actions;
@@ -91,25 +260,26 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
     const double* mrow = P.means + (size_t)i * A;
     int cnt[kMaxA];
     for (int k = 0; k < A; ++k) cnt[k] = 0;
-    // LinUCB running design: X^T X (d x d, d <= kMaxD, row-major) and X^T r
-    double xtx[kMaxD * kMaxD], xtr[kMaxD];
-    for (int k = 0; k < kMaxD * kMaxD; ++k) xtx[k] = 0.0;
-    for (int k = 0; k < kMaxD; ++k) xtr[k] = 0.0;
     int opt = 0;
     for (int k = 1; k < A; ++k)
         if (mrow[k] > mrow[opt]) opt = k;
     const int L = P.C + P.H;                   // list capacity per arm
     const size_t lstride = (size_t)L * P.N;    // arm stride of the lists
+    // LinUCB keeps the context itself in the workspace (it re-reads it every step):
+    // rewards [k][task] fp64, then arm indices [k][task] int32, lane-contiguous
+    const bool lin = P.policy == DPT_POLICY_LINUCB;
+    double* lin_r = P.lists;
+    int32_t* lin_a = reinterpret_cast<int32_t*>(P.lists + lstride);
+    int n_ctx = 0;
     auto append = [&](int a, double r) {
-        if (P.lists) P.lists[a * lstride + (size_t)cnt[a] * P.N + i] = r;
-        ++cnt[a];
-        if (P.policy == DPT_POLICY_LINUCB) {
-            const double* x = P.arms + (size_t)a * P.d;
-            for (int p = 0; p < P.d; ++p) {
-                xtr[p] += x[p] * r;
-                for (int q = 0; q < P.d; ++q) xtx[p * kMaxD + q] += x[p] * x[q];
-            }
+        if (lin) {
+            lin_r[(size_t)n_ctx * P.N + i] = r;
+            lin_a[(size_t)n_ctx * P.N + i] = a;
+        } else if (P.lists) {
+            P.lists[a * lstride + (size_t)cnt[a] * P.N + i] = r;
         }
+        ++cnt[a];
+        ++n_ctx;
     };
     for (int c = 0; c < P.C; ++c)  // prefix context (set_batch_numpy_vec), time order
         append(P.ctx_actions[(size_t)i * P.C + c], P.ctx_rewards[(size_t)i * P.C + c]);
@@ -122,64 +292,9 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
                 const double u = P.policy_noise ? P.policy_noise[(size_t)i]
                                                 : philox_uniform(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_POLICY);
                 a = min((int)(u * A), A - 1);
-            } else if (P.d <= 2) {  // closed-form 2 x 2 inverse
-                const double c00 = 1.0 + xtx[0], c01 = xtx[1], c11 = 1.0 + xtx[kMaxD + 1];
-                const double det = c00 * c11 - c01 * c01;
-                const double i00 = c11 / det, i01 = -c01 / det, i11 = c00 / det;
-                const double t0 = i00 * xtr[0] + i01 * xtr[1], t1 = i01 * xtr[0] + i11 * xtr[1];
-                double best = -INFINITY;
-                for (int k = 0; k < A; ++k) {
-                    const double x0 = P.arms[k * P.d], x1 = P.d > 1 ? P.arms[k * P.d + 1] : 0.0;
-                    const double q = x0 * (i00 * x0 + i01 * x1) + x1 * (i01 * x0 + i11 * x1);
-                    const double v = (t0 * x0 + t1 * x1) + P.c * sqrt(q);
-                    if (v > best) { best = v; a = k; }
-                }
             } else {
-                // cov_inv = inv(I + X^T X) by Gauss-Jordan (cov is symmetric positive definite, so no
-                // pivoting), theta = cov_inv X^T r, value = theta . x + c sqrt(x cov_inv x)
-                // (ctrls/ctrl_bandit.py:505-522; LAPACK's inverse rounds differently: equal up to
-                // near-ties of the arm values)
-                const int d = P.d;
-                double m[kMaxD * kMaxD], inv[kMaxD * kMaxD];
-                for (int p = 0; p < d; ++p)
-                    for (int q = 0; q < d; ++q) {
-                        m[p * kMaxD + q] = xtx[p * kMaxD + q] + (p == q ? 1.0 : 0.0);
-                        inv[p * kMaxD + q] = p == q ? 1.0 : 0.0;
-                    }
-                for (int c = 0; c < d; ++c) {
-                    const double piv = 1.0 / m[c * kMaxD + c];
-                    for (int q = 0; q < d; ++q) {
-                        m[c * kMaxD + q] *= piv;
-                        inv[c * kMaxD + q] *= piv;
-                    }
-                    for (int p = 0; p < d; ++p) {
-                        if (p == c) continue;
-                        const double f = m[p * kMaxD + c];
-                        for (int q = 0; q < d; ++q) {
-                            m[p * kMaxD + q] -= f * m[c * kMaxD + q];
-                            inv[p * kMaxD + q] -= f * inv[c * kMaxD + q];
-                        }
-                    }
-                }
-                double theta[kMaxD];
-                for (int p = 0; p < d; ++p) {
-                    double t = 0.0;
-                    for (int q = 0; q < d; ++q) t += inv[p * kMaxD + q] * xtr[q];
-                    theta[p] = t;
-                }
-                double best = -INFINITY;
-                for (int k = 0; k < A; ++k) {
-                    const double* x = P.arms + (size_t)k * d;
-                    double tv = 0.0, qv = 0.0;
-                    for (int p = 0; p < d; ++p) {
-                        tv += theta[p] * x[p];
-                        double s = 0.0;
-                        for (int q = 0; q < d; ++q) s += inv[p * kMaxD + q] * x[q];
-                        qv += x[p] * s;
-                    }
-                    const double v = tv + P.c * sqrt(qv);
-                    if (v > best) { best = v; a = k; }
-                }
+                a = linucb_choose([&](int k) { return lin_a[(size_t)k * P.N + i]; },
+                                  [&](int k) { return lin_r[(size_t)k * P.N + i]; }, n_ctx, P.arms, A, P.d, P.c);
             }
         } else {
             // per-arm sums over the context (numpy pairwise order, fp64)
@@ -220,7 +335,10 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
                         double best = -INFINITY;
                         int am = 0;
                         for (int k = 0; k < A; ++k) {
-                            const double g = philox_normal(P.seed, ((uint64_t)P.step0 + h) * 128 + s, task, DPT_STREAM_POLICY + k);
+                            const double g = P.policy_noise
+                                                 ? P.policy_noise[(((size_t)h * 100 + s) * P.N + i) * A + k]
+                                                 : philox_normal(P.seed, ((uint64_t)P.step0 + h) * 128 + s, task,
+                                                                 DPT_STREAM_POLICY + k);
                             const double v = post_m[k] + post_s[k] * g;
                             if (v > best) { best = v; am = k; }
                         }

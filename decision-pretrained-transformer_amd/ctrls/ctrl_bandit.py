@@ -138,7 +138,8 @@ class _KernelPolicy(Controller):
     posterior normals, LinUCB's first arm) from the controller's stream: step k of the
     stream is Philox counter k of one seed, so the per-step and fused loops act on the same
     draws.  ``policy_noise``, optional: callable(counter) -> that step's draws ((N, A)
-    posterior normals, or (N,) uniforms for LinUCB's first arm), injected instead.
+    posterior normals, (100, N, A) for Thompson's sample=False vote, or (N,) uniforms for
+    LinUCB's first arm), injected instead.
     """
 
     policy = None

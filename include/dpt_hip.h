@@ -272,8 +272,10 @@ int dpt_rollout_bandit(const dpt_model* model, const dpt_bandit_rollout_args* ar
  *   DPT_POLICY_LINUCB   LinUCBPolicy(c)      :447-528 (arms (A, lin_d), lin_d <= 8)
  * Per-arm statistics are recomputed each step from the per-arm reward lists in
  * numpy's fp64 pairwise-summation order, as the reference does, so action
- * indices match it bit for bit given the same draws.  policy_noise: Thompson
- * (H,N,A) posterior normals; LinUCB (N) uniforms for the empty-context arm.  */
+ * indices match it bit for bit given the same draws (LinUCB: numpy's BLAS/LAPACK
+ * rounding order restated at lin_d = 2; equal up to near-ties above).  policy_noise:
+ * Thompson (H,N,A) posterior normals (sample = 1) or (H,100,N,A) for the 100-draw vote
+ * (sample = 0); LinUCB (N) uniforms for the empty-context arm.  */
 #define DPT_POLICY_OPT 0
 #define DPT_POLICY_EMP 1
 #define DPT_POLICY_UCB 2

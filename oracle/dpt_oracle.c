@@ -3,8 +3,11 @@
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
  * this library (oracle/build/libdpt_oracle.so).  It mirrors
- * oracle/dpt_oracle.py (pinned to the reference's golden vectors) in fp32 and
- * is the CPU timing baseline ("port"): the reference algorithm
+ * oracle/dpt_oracle.py and is pinned to the reference's recorded rollouts itself
+ * (tests/test_oracle_golden.py::test_c_bandit_oracle_matches_reference,
+ * ::test_c_darkroom_oracle_matches_reference).  The fp32 bandit rollout is the CPU
+ * timing baseline ("port"), the float64 one (dpt_oracle_bandit_rollout_f64) the
+ * full-size checker of the GPU tests: the reference algorithm
  * (evals/eval_bandit.py:56-103 + ctrls/ctrl_bandit.py:422-444 + models/net.py:41-60)
  * recomputes the whole window at every step; recompute=0 switches to the
  * exact incremental (KV-cache) form of the same arithmetic.
@@ -107,20 +110,49 @@ static void token_forward(const view_t* v, const float* tok, int p, float* kc, f
     linear(xn, E, v->head_w, v->head_b, v->A, logits);
 }
 
-static int select_action(const float* lg, int A, int sample, double u) {
+/* numpy's float32 sum along a contiguous axis (pairwise_sum, numpy/_core/src/umath/
+ * loops_utils.h.src): sequential below 8 elements, else 8 running partials, a fixed tree and
+ * the remainder (A <= 64 < 128, so no recursive halving) */
+static float np_sum_f32(const float* x, int n) {
+    if (n < 8) {
+        float res = 0.f;
+        for (int i = 0; i < n; ++i) res += x[i];
+        return res;
+    }
+    float r[8];
+    for (int j = 0; j < 8; ++j) r[j] = x[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; ++j) r[j] += x[i + j];
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += x[i];
+    return res;
+}
+
+/* ctrls/ctrl_bandit.py:435-443: greedy = first argmax of the fp32 logits; sampling =
+ * scipy.special.softmax in float32 (max-shift, exp, numpy sum, divide) then numpy
+ * RandomState.choice(A, p): cdf = cumsum(float64(p)) / last, idx = #(cdf <= u).
+ * *margin (if non-NULL) = distance of u to the nearest interior cdf edge. */
+static int select_action(const float* lg, int A, int sample, double u, double* margin) {
     int best = 0;
+    if (margin) *margin = INFINITY;
     if (!sample) {
         for (int k = 1; k < A; ++k)
             if (lg[k] > lg[best]) best = k;
         return best;
     }
-    float m = -INFINITY, e[64], s = 0.f;
+    float m = -INFINITY, e[64];
     for (int k = 0; k < A; ++k) m = lg[k] > m ? lg[k] : m;
-    for (int k = 0; k < A; ++k) { e[k] = expf(lg[k] - m); s += e[k]; }
+    for (int k = 0; k < A; ++k) e[k] = expf(lg[k] - m);
+    const float s = np_sum_f32(e, A);
     double c = 0.0, cdf[64];
     for (int k = 0; k < A; ++k) { c += (double)(e[k] / s); cdf[k] = c; }
     int idx = 0;
-    for (int k = 0; k < A; ++k) idx += (cdf[k] / c <= u);
+    for (int k = 0; k < A; ++k) {
+        const double q = cdf[k] / c;
+        idx += (q <= u);
+        if (margin && k < A - 1 && fabs(q - u) < *margin) *margin = fabs(q - u);
+    }
     return idx < A ? idx : A - 1;
 }
 
@@ -150,7 +182,7 @@ int dpt_oracle_bandit_rollout(const float* blob, int L, int A, int npos, const d
             }
             if (logits_out)
                 for (int k = 0; k < A; ++k) logits_out[((size_t)h * N + i) * A + k] = lg[k];
-            int a = select_action(lg, A, sample, sample ? u[(size_t)h * N + i] : 0.0);
+            int a = select_action(lg, A, sample, sample ? u[(size_t)h * N + i] : 0.0, NULL);
             double mean = means[(size_t)i * A + a];
             volatile double noise = 0.0 + var * g[(size_t)h * N + i];
             double r = mean + noise;
@@ -168,6 +200,110 @@ int dpt_oracle_bandit_rollout(const float* blob, int L, int A, int npos, const d
         free(toks);
     }
     return rc;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * The same bandit rollout with the forward in float64 (the full-size checker of the GPU
+ * tests, like oracle/dpt_oracle.py's default dtype): every position's embedding, LayerNorms,
+ * projections, attention and MLP in double from the fp32 weights, the logits rounded to
+ * float32 as models/net.py hands them to the controller (`.cpu().detach().numpy()` of a
+ * float32 tensor), then the reference's float32 softmax and float64 choice (select_action).
+ * Position p's keys/values depend only on tokens <= p, so the incremental decode below is
+ * the same arithmetic as re-forwarding the window each step (recompute=1 does that; tested).
+ * Outputs as dpt_oracle_bandit_rollout, plus margin (H,N): distance of u to the nearest
+ * interior cdf edge (the caller's near-tie flag).
+ * ------------------------------------------------------------------------------------------ */
+
+static void layer_norm_d(const double* x, const float* g, const float* b, double* y);
+static void linear_d(const double* x, int in, const float* W, const float* b, int out, double* y);
+
+static void token_forward_d(const view_t* v, const float* tok, int p, double* kc, double* vc, int Tcap,
+                            double* sc, double* logits) {
+    double x[E], xn[E], qkv[3 * E], o[E], t[E], h[FF], tk[64];
+    for (int k = 0; k < v->F; ++k) tk[k] = tok[k];
+    linear_d(tk, v->F, v->emb_w, v->emb_b, E, x);
+    for (int j = 0; j < E; ++j) x[j] += v->wpe[(size_t)p * E + j];
+    for (int l = 0; l < v->L; ++l) {
+        const float* W = v->layers + (size_t)l * LSIZE;
+        double* K = kc + (size_t)l * Tcap * E;
+        double* V = vc + (size_t)l * Tcap * E;
+        layer_norm_d(x, W + 0, W + 32, xn);
+        linear_d(xn, E, W + 64, W + 3136, 3 * E, qkv);
+        memcpy(K + (size_t)p * E, qkv + E, E * sizeof(double));
+        memcpy(V + (size_t)p * E, qkv + 2 * E, E * sizeof(double));
+        double m = -INFINITY, s = 0.0;
+        for (int j = 0; j <= p; ++j) {
+            double d = 0.0;
+            for (int k = 0; k < E; ++k) d += qkv[k] * K[(size_t)j * E + k];
+            sc[j] = d / sqrt((double)E);
+            if (sc[j] > m) m = sc[j];
+        }
+        for (int j = 0; j <= p; ++j) {
+            sc[j] = exp(sc[j] - m);
+            s += sc[j];
+        }
+        for (int k = 0; k < E; ++k) o[k] = 0.0;
+        for (int j = 0; j <= p; ++j) {
+            const double pj = sc[j] / s;
+            for (int k = 0; k < E; ++k) o[k] += pj * V[(size_t)j * E + k];
+        }
+        linear_d(o, E, W + 3232, W + 4256, E, t);
+        for (int j = 0; j < E; ++j) x[j] += t[j];
+        layer_norm_d(x, W + 4288, W + 4320, xn);
+        linear_d(xn, E, W + 4352, W + 8448, FF, h);
+        for (int j = 0; j < FF; ++j)
+            h[j] = 0.5 * h[j] * (1.0 + tanh(0.7978845608028654 * (h[j] + 0.044715 * h[j] * h[j] * h[j])));
+        linear_d(h, FF, W + 8576, W + 12672, E, t);
+        for (int j = 0; j < E; ++j) x[j] += t[j];
+    }
+    layer_norm_d(x, v->lnf_g, v->lnf_b, xn);
+    linear_d(xn, E, v->head_w, v->head_b, v->A, logits);
+}
+
+int dpt_oracle_bandit_rollout_f64(const float* blob, int L, int A, int npos, const double* means, int N, int H,
+                                  double var, const double* u, const double* g, int sample, int recompute,
+                                  int nthreads, int32_t* actions, double* rewards, double* arm_value,
+                                  float* logits_out, double* margin_out) {
+    if (A > 64 || H > npos || H < 1) return -1;
+    view_t v = make_view(blob, L, 1, A, npos);
+    const int F = v.F;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int i = 0; i < N; ++i) {
+        double* kc = (double*)malloc(sizeof(double) * (size_t)L * (H + 1) * E);
+        double* vc = (double*)malloc(sizeof(double) * (size_t)L * (H + 1) * E);
+        double* sc = (double*)malloc(sizeof(double) * (size_t)(H + 1));
+        float* toks = (float*)calloc((size_t)(H + 1) * F, sizeof(float));
+        double lgd[64];
+        float lg[64];
+        toks[0] = 1.f; /* query token [1, 0...] */
+        for (int h = 0; h < H; ++h) {
+            for (int p = recompute ? 0 : h; p <= h; ++p) token_forward_d(&v, toks + (size_t)p * F, p, kc, vc, H + 1, sc, lgd);
+            for (int k = 0; k < A; ++k) lg[k] = (float)lgd[k];
+            if (logits_out)
+                for (int k = 0; k < A; ++k) logits_out[((size_t)h * N + i) * A + k] = lg[k];
+            double mg;
+            int a = select_action(lg, A, sample, sample ? u[(size_t)h * N + i] : 0.0, &mg);
+            if (margin_out) margin_out[(size_t)h * N + i] = mg;
+            double mean = means[(size_t)i * A + a];
+            volatile double noise = 0.0 + var * g[(size_t)h * N + i];
+            double r = mean + noise;
+            actions[(size_t)i * H + h] = a;
+            rewards[(size_t)i * H + h] = r;
+            arm_value[(size_t)i * H + h] = mean;
+            float* t = toks + (size_t)(h + 1) * F;
+            t[0] = 1.f;
+            t[1 + a] = 1.f;
+            t[1 + A] = 1.f;
+            t[2 + A] = (float)r;
+        }
+        free(kc);
+        free(vc);
+        free(sc);
+        free(toks);
+    }
+    return 0;
 }
 
 /* ------------------------------------------------------------------------------------------

@@ -553,6 +553,66 @@ def linucb_d4():
     print("LinUCB d=4")
 
 
+def linucb_long():
+    """LinUCB (ctrls/ctrl_bandit.py:447-528) with lin_d = 2 on the C4 arm table (20 arms,
+    collect_data.py:230-231) over 800 steps, so the context crosses the BLAS blocking sizes
+    (384 / 768 rows of the X^T X product): through eval_linear_bandit.deploy_online_vec with
+    every draw recorded."""
+    import numpy as np
+    from envs import bandit_env
+    from ctrls import ctrl_bandit as cb
+    from evals import eval_linear_bandit
+    N, H, A, d, var = 24, 800, 20, 2, 0.3
+    arms = np.random.RandomState(1234).normal(size=(A, d)) / np.sqrt(d)
+    thetas = np.random.RandomState(23).normal(0, 1, (N, d)) / np.sqrt(d)
+    envs = [bandit_env.LinearBanditEnv(t, arms, H, var=var) for t in thetas]
+    vec = bandit_env.BanditEnvVec(envs)
+    np.random.seed(29)
+    with DrawRecorder(np) as rec:
+        cm, meta = eval_linear_bandit.deploy_online_vec(vec, cb.LinUCBPolicy(envs[0], const=1.0, batch_size=N), H,
+                                                        include_meta=True)
+    np.savez_compressed(os.path.join(OUT, "linucb_long.npz"), means=np.stack([e.means for e in envs]), arms=arms,
+                        theta=thetas, cum_means=cm, actions=meta["context_actions"].argmax(-1).astype(np.int8),
+                        g=np.array(rec.g).reshape(H, N), first_action=np.asarray(rec.plain[0]))
+    print("LinUCB long")
+
+
+def linear_offline():
+    """evals/eval_linear_bandit.py:202-286 (offline: Opt, the DPT greedy leg, Thompson with the
+    100-draw vote and prior 0/1, LinUCB with const 0 'linreg') on fixed contexts of 20-arm linear
+    bandits, at every context length 1..Hc as offline_graph (:289-339) sweeps them.  The vote's
+    posterior normals are recorded per call; returns are the dict offline() hands back."""
+    import numpy as np
+    import torch
+    from envs import bandit_env
+    from evals import eval_linear_bandit
+    model = fixture_transformer("linear20")
+    N, Hc, A, d, var = 10, 12, 20, 2, 0.3
+    rs = np.random.RandomState(61)
+    arms = np.random.RandomState(1234).normal(size=(A, d)) / np.sqrt(d)
+    thetas = rs.normal(0, 1, (N, d)) / np.sqrt(d)
+    trajs = []
+    for t in thetas:
+        env = bandit_env.LinearBanditEnv(t, arms, Hc, var=var)
+        a = rs.randint(0, A, Hc)
+        trajs.append({"theta": t, "arms": arms, "means": env.means, "context_states": np.ones((Hc, 1)),
+                      "context_actions": np.eye(A)[a], "context_next_states": np.ones((Hc, 1)),
+                      "context_rewards": env.means[a] + 0.3 * rs.normal(size=Hc)})
+    out = {"theta": thetas, "arms": arms, "var": np.float64(var)}
+    for k in ("context_actions", "context_rewards"):
+        out[k] = np.stack([t[k] for t in trajs])
+    for h in range(1, Hc + 1):
+        np.random.seed(300 + h)
+        with DrawRecorder(np) as rec, torch.no_grad():
+            b = eval_linear_bandit.offline(trajs, model, n_eval=N, horizon=h, var=var)
+        assert sorted(b) == ["linreg", "lnr", "opt", "thmp"] and len(rec.garr) == 100
+        out[f"h{h}/vote_g"] = np.stack(rec.garr)  # (100, N, A)
+        for k, v in b.items():
+            out[f"h{h}/{k}"] = np.asarray(v)
+    np.savez_compressed(os.path.join(OUT, "linear_offline.npz"), **out)
+    print("linear offline")
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit("reference checkout not present; fixtures are committed")

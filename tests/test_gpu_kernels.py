@@ -512,8 +512,9 @@ def first_tie(margin, bar=1e-5):
 def test_rollout_full_config_sampled_tasks(A, H, var, N):
     """BASELINE configs 2 (5 arms, H=500) and 4 (20 arms, H=1000; one GPU's 4096-task shard) at full
     size, and config 2 with a partial last tile (4093 tasks): the fused rollout agrees, on >= 64
-    sampled tasks (every slot of the first two tiles, the last tile, random ones), with the C
-    oracle fed the same Philox draws -- logits within 1e-5 at every step and actions / arm values
+    sampled tasks (every slot of the first two tiles, the last tile, random ones), with the
+    float64 C oracle (pinned to the reference's rollouts by test_c_bandit_oracle_matches_reference)
+    fed the same Philox draws -- logits within 1e-5 at every step and actions / arm values
     exactly, each task up to its first near-tie draw (a uniform within 1e-5 of a cdf edge)."""
     import bench
     import dpt_hip
@@ -536,10 +537,10 @@ def test_rollout_full_config_sampled_tasks(A, H, var, N):
     u = np.stack([philox_np.uniform(seed, h, tasks, dpt_hip.STREAM_SELECT) for h in range(H)])
     g = np.stack([philox_np.normal(seed, h, tasks, dpt_hip.STREAM_REWARD) for h in range(H)])
     blob = dpt_hip.pack_weights(sd, L).numpy()
-    ref = c_oracle.bandit_rollout(blob, L, A, 4 * (1 + H), means[tasks], H, var, u, g, True, False, 16,
-                                  want_logits=True)
+    ref = c_oracle.bandit_rollout_f64(blob, L, A, 4 * (1 + H), means[tasks], H, var, u, g, True, False, 16,
+                                      want_logits=True)
     lg = out["logits"].cpu().numpy()[:, tasks]
-    margin = O.boundary_margin(O.softmax_f32(ref["logits"], 1.0), u)  # (H, n)
+    margin = ref["margin"]  # (H, n)
     full = 0
     for j, t in enumerate(tasks):
         n = first_tie(margin[:, j])  # steps 0..n-1 agree exactly; a near-tie may flip step n's action

@@ -231,6 +231,57 @@ def test_c_darkroom_oracle_matches_reference(tag):
     assert np.array_equal(outs[0]["actions"], outs[1]["actions"])
 
 
+def _bandit_cases():
+    """(fixture, weights, means, H, var, u, g, sample, ref actions, ref cum_means, ref rewards, ref logits)
+    of every recorded reference bandit rollout (evals/eval_bandit.py:56-103 with the DPT controller)."""
+    for tag in ("sample", "greedy", "var0"):
+        yield f"rollout_bandit_{tag}", "bandit5"
+    yield "rollout_linear_sample", "linear20"
+    yield "c1_bandit", "bandit5"
+
+
+@pytest.mark.parametrize("fix,wname", list(_bandit_cases()))
+@pytest.mark.parametrize("mode", ["f32", "f64"])
+def test_c_bandit_oracle_matches_reference(fix, wname, mode):
+    """The C restatement of the bandit online rollout (oracle/dpt_oracle.c: the fp32 CPU baseline
+    and the float64 full-size checker of the GPU tests) against the reference's recorded rollouts
+    with its draws injected: actions, rewards and cum_means exactly, logits within 1e-5.  The
+    float64 form is also checked in its re-forward-every-step (reference) shape."""
+    import torch
+    from oracle import c_oracle
+    import dpt_hip
+    g = golden(f"{fix}.npz")
+    fw, _ = weights(wname)
+    Hw, _, A, L, _ = (int(x) for x in fw["cfg"])
+    sd = {k[2:]: torch.from_numpy(v) for k, v in fw.items() if k.startswith("w/")}
+    blob = dpt_hip.pack_weights(sd, L).numpy()
+    npos = 4 * (1 + Hw)
+    if fix == "c1_bandit":
+        means, u, gg = g["eval/means"], g["eval/u"], g["eval/g"]
+        H, sample = int(g["cfg"][1]), True
+        ref_a, ref_cm, ref_r, ref_lg = g["eval/actions"], g["eval/cum_means"], g["eval/rewards"], None
+    else:
+        means, u, gg = g["means"], g["u"], g["g"]
+        _, H, _, sample = (int(x) for x in g["cfg"])
+        ref_a, ref_cm, ref_r, ref_lg = g["ctx_actions"].argmax(-1), g["cum_means"], g["ctx_rewards"], g["logits"]
+    var = float(g["var"])
+    runs = []
+    if mode == "f32":
+        runs.append(c_oracle.bandit_rollout(blob, L, A, npos, means, H, var, u, gg, bool(sample), False, 2,
+                                            want_logits=True))
+    else:
+        for rec in (False, True):
+            runs.append(c_oracle.bandit_rollout_f64(blob, L, A, npos, means, H, var, u, gg, bool(sample), rec, 2,
+                                                    want_logits=True))
+        assert np.array_equal(runs[0]["logits"], runs[1]["logits"])  # decode == re-forward, bit for bit
+    for o in runs:
+        if ref_lg is not None:
+            assert np.abs(o["logits"] - ref_lg).max() <= 1e-5
+        assert np.array_equal(o["actions"], ref_a)
+        assert np.array_equal(o["rewards"], ref_r)
+        assert np.array_equal(o["cum_means"], ref_cm)
+
+
 @pytest.mark.parametrize("name", ["darkroom", "bandit5"])
 def test_torch_oracle_gradients_match_reference(name):
     """oracle/dpt_oracle_torch.py (float64 autograd of the restated forward, the checker of the
@@ -253,9 +304,11 @@ def test_torch_oracle_gradients_match_reference(name):
         assert np.abs(got - ref).max() <= 1e-10 * max(1e-30, np.abs(ref).max()), k
 
 
-def test_linucb_d4_matches_reference():
-    """LinUCB with lin_d = 4 (np.linalg.inv in the oracle, as in the reference)."""
-    g = golden("linucb_d4.npz")
+@pytest.mark.parametrize("fix", ["linucb_d4", "linucb_long"])
+def test_linucb_matches_reference(fix):
+    """LinUCB with lin_d = 4, and lin_d = 2 over 800 steps (np.linalg.inv in the oracle, as in
+    the reference)."""
+    g = golden(f"{fix}.npz")
     H = g["g"].shape[0]
     out = O.bandit_policy_rollout("linucb", g["means"], H, 0.3, g["g"], c=1.0, arms=g["arms"],
                                   first_u_idx=g["first_action"])
