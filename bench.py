@@ -99,13 +99,31 @@ def cpu_info():
     return "unknown"
 
 
-def cpu_baseline(sd, means, H, var, n_layer, A, n_rec=128, n_kv=2048):
-    """The C oracle (oracle/dpt_oracle.c) on this host's cores: reference algorithm
-    (whole window re-forwarded each step) on a bounded task sample, and the same
-    arithmetic with an exact K/V cache."""
+def host_cpus():
+    """The host cores this process may run on: the affinity mask, capped by a cgroup CPU quota
+    (cgroup v2 cpu.max) when one is set; with nproc, the quota and the CPU model for the line."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    threads = max(1, min(aff, int(quota)) if quota else aff)
+    return threads, {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                     "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cpu_model": cpu_info()}
+
+
+def cpu_baseline(sd, means, H, var, n_layer, A, n_rec=None, n_kv=2048):
+    """The C oracle (oracle/dpt_oracle.c, fp32 as the reference's torch forward) on every host core
+    this process may use: the reference algorithm (whole window re-forwarded each step) on a
+    bounded sample of the workload, BASELINE config 1 (64 tasks, H=100, 5 arms) in full, and the
+    same arithmetic with an exact K/V cache."""
     from oracle import c_oracle
     import dpt_hip
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, hw = host_cpus()
+    n_rec = n_rec or 2 * max(16, threads)  # two tasks per thread: ~10 s of work per thread at H=500
     blob = dpt_hip.pack_weights(sd, n_layer).numpy()
     npos = 4 * (1 + H)
     rs = np.random.RandomState(7)
@@ -113,16 +131,48 @@ def cpu_baseline(sd, means, H, var, n_layer, A, n_rec=128, n_kv=2048):
     t0 = time.perf_counter()
     c_oracle.bandit_rollout(blob, n_layer, A, npos, means[:n_rec], H, var, u, g, True, True, threads)
     t_rec = time.perf_counter() - t0
+    # config 1 in full: 64 tasks x H=100 (its own means, RandomState(1); the model's first wpe rows)
+    H1, N1 = 100, 64
+    m1 = np.random.RandomState(1).uniform(0, 1, (N1, A))
+    u1, g1 = rs.uniform(size=(H1, N1)), rs.normal(size=(H1, N1))
+    t0 = time.perf_counter()
+    c_oracle.bandit_rollout(blob, n_layer, A, npos, m1, H1, var, u1, g1, True, True, threads)
+    t_c1 = time.perf_counter() - t0
     u, g = rs.uniform(size=(H, n_kv)), rs.normal(size=(H, n_kv))
     t0 = time.perf_counter()
     c_oracle.bandit_rollout(blob, n_layer, A, npos, means[:n_kv], H, var, u, g, True, False, threads)
     t_kv = time.perf_counter() - t0
     return ({"value": n_rec * H / t_rec, "unit": "env-steps/s", "cores": threads, "kind": "port",
              "sample": f"{n_rec} tasks x H={H} full online rollout, reference algorithm (whole window "
-                       f"re-forwarded every step, evals/eval_bandit.py:56-103), fp32 C + OpenMP, {cpu_info()}",
-             "seconds": t_rec},
+                       f"re-forwarded every step, evals/eval_bandit.py:56-103), fp32 C + OpenMP",
+             "seconds": t_rec, "host": hw,
+             "config1_full": {"value": N1 * H1 / t_c1, "unit": "env-steps/s", "seconds": t_c1,
+                              "sample": f"BASELINE config 1 in full: {N1} tasks x H={H1}, 5 arms, var {var}, "
+                                        "reference algorithm"}},
             {"value": n_kv * H / t_kv, "unit": "env-steps/s", "cores": threads, "kind": "port-kvcache",
              "sample": f"{n_kv} tasks x H={H}, same C oracle with an exact K/V cache", "seconds": t_kv})
+
+
+def cpu_baseline_darkroom(sd, goals, H, n_layer, n_tasks=None, n_eps=8):
+    """DarkRoom online eval on the host cores: the float64 C restatement (oracle/dpt_oracle.c,
+    pinned to the reference's rollouts) with the reference's algorithm -- one full window forward
+    per env step, no memo (evals/eval_darkroom.py:53-66) -- on the first n_eps episodes of
+    n_tasks tasks (episode 0 has an empty window, the others the full 1 + H tokens)."""
+    from oracle import c_oracle
+    import dpt_hip
+    threads, hw = host_cpus()
+    n_tasks = n_tasks or 2 * max(8, threads)
+    blob = dpt_hip.pack_weights(sd, n_layer).numpy()
+    u = np.random.RandomState(7).uniform(size=(n_eps * H, n_tasks))
+    t0 = time.perf_counter()
+    c_oracle.darkroom_rollout(blob, n_layer, 4 * (1 + H), goals[:n_tasks], n_eps, H, 1, u, True, memo=False,
+                              threads=threads)
+    t = time.perf_counter() - t0
+    return {"value": n_tasks * n_eps * H / t, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "seconds": t, "host": hw,
+            "sample": f"{n_tasks} tasks x {n_eps} episodes x {H} steps of the online eval (episode 0 empty "
+                      f"window, then 1+{H} tokens), reference algorithm: a full window forward every step, "
+                      "float64 C + OpenMP"}
 
 
 def main():
@@ -326,6 +376,8 @@ def main():
         base, kv = cpu_baseline(sd, means_all, H, args.var, L, A)
         line["cpu_baseline"] = base
         line["cpu_baseline_kvcache"] = kv
+    if rank == 0 and world == 1 and wl == "darkroom" and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_darkroom(sd, goals_all, H, L)
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:

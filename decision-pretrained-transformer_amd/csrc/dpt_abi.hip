@@ -501,8 +501,9 @@ static int train_dims(const dpt_train_desc* d, TrDims& o) {
                 d->window <= d->n_positions,
             "train desc: n_layer=%d n_embd=%d sd=%d A=%d n_positions=%d batch=%d window=%d", d->n_layer, d->n_embd,
             d->state_dim, d->action_dim, d->n_positions, d->batch, d->window);
+    REQUIRE((d->reserved & ~DPT_TRAIN_FORWARD_ONLY) == 0, "train desc: unknown flags 0x%x", d->reserved);
     o = TrDims{d->n_layer, d->n_embd, 2 * d->state_dim + d->action_dim + 1, d->action_dim, d->batch, d->window,
-               d->n_positions};
+               d->n_positions, (d->reserved & DPT_TRAIN_FORWARD_ONLY) ? 1 : 0};
     return train_dims_check(o);
 }
 
@@ -535,6 +536,7 @@ int dpt_train_backward(const dpt_train_desc* d, const float* blob, const float* 
     TrDims t;
     if (int rc = train_dims(d, t)) return rc;
     REQUIRE(blob && tokens && ws && dpreds && dblob, "null pointer");
+    REQUIRE(!t.fwd_only, "train backward: the description is forward-only (DPT_TRAIN_FORWARD_ONLY)");
     return train_backward(t, blob, tokens, ws, dpreds, dblob, S(stream));
 }
 

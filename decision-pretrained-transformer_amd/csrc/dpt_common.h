@@ -309,6 +309,7 @@ __device__ inline int select_fixed_fast(const float (&lg)[NA], int sample, float
 // token features, actions, sequences, tokens per sequence, wpe rows.
 struct TrDims {
     int L, E, F, A, B, T, npos;
+    int fwd_only;  // DPT_TRAIN_FORWARD_ONLY: inference workspace (nothing saved for a backward)
     __host__ __device__ int R() const { return B * T; }
     __host__ __device__ int64_t layer_size() const { return 12ll * E * E + 13ll * E; }
 };

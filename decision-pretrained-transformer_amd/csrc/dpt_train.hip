@@ -69,13 +69,16 @@ struct TrWs {
     __host__ __device__ static int64_t nchunks(const TrDims& d) { return (d.R() + kTrRowsPerChunk - 1) / kTrRowsPerChunk; }
     __host__ __device__ static TrWs make(const TrDims& d) {
         TrWs w;
-        const int64_t R = d.R(), E = d.E, L = d.L, TT = (int64_t)d.B * d.T * d.T;
+        const int64_t R = d.R(), E = d.E, TT = (int64_t)d.B * d.T * d.T;
+        // forward-only: one slot per per-layer array (x ping-pongs over two), no probabilities,
+        // no backward scratch
+        const int64_t L = d.fwd_only ? 1 : d.L;
         int64_t p = 0;
-        w.x = p; p += (L + 1) * R * E;
+        w.x = p; p += (d.fwd_only ? 2 : L + 1) * R * E;
         w.y1 = p; p += L * R * E;
         w.st1 = p; p += L * R * 2;
         w.qkv = p; p += L * R * 3 * E;
-        w.P = p; p += L * TT;
+        w.P = p; p += d.fwd_only ? 0 : L * TT;
         w.o = p; p += L * R * E;
         w.x2 = p; p += L * R * E;
         w.y2 = p; p += L * R * E;
@@ -83,6 +86,10 @@ struct TrWs {
         w.hpre = p; p += L * R * 4 * E;
         w.yf = p; p += R * E;
         w.stf = p; p += R * 2;
+        if (d.fwd_only) {
+            w.dx = w.dx2 = w.dqkv = w.dout = w.dh = w.dy = w.dS = w.part = w.total = p;
+            return w;
+        }
         w.dx = p; p += R * E;
         w.dx2 = p; p += R * E;
         w.dqkv = p; p += R * 3 * E;
@@ -197,11 +204,11 @@ __global__ void tr_attn_fwd(const float* __restrict__ qkv, TrDims d, float* __re
         l += p;
     }
     const float inv = 1.0f / wave_sum(l);
-    float* prow = P + ((int64_t)b * T + t) * T;
+    float* prow = P ? P + ((int64_t)b * T + t) * T : nullptr;  // saved for the backward unless forward-only
     for (int j = lane; j <= t; j += 64) {
         const float p = pr[j] * inv;
         pr[j] = p;
-        prow[j] = p;
+        if (prow) prow[j] = p;
     }
     wave_lds_sync();
     for (int e = lane; e < E; e += 64) {
@@ -429,19 +436,22 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
     }
     if (attn_lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)tr_attn_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)attn_lds);
     hipLaunchKernelGGL(tr_embed, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, tok, blob, d, B, ws + W.x);
+    // slot of layer l's arrays: l, or 0 (x: l & 1) in the forward-only workspace
+    auto xs = [&](int l) -> int64_t { return d.fwd_only ? (l & 1) : l; };
     for (int l = 0; l < d.L; ++l) {
         const TrLayer P = TrLayer::make(B.layers + l * d.layer_size(), E);
-        const float* x = ws + W.x + l * RE;
-        float* y1 = ws + W.y1 + l * RE;
-        float* st1 = ws + W.st1 + (int64_t)l * R * 2;
-        float* qkv = ws + W.qkv + l * RE * 3;
-        float* Pm = ws + W.P + l * TT;
-        float* o = ws + W.o + l * RE;
-        float* x2 = ws + W.x2 + l * RE;
-        float* y2 = ws + W.y2 + l * RE;
-        float* st2 = ws + W.st2 + (int64_t)l * R * 2;
-        float* hpre = ws + W.hpre + l * RE * 4;
-        float* xn = ws + W.x + (l + 1) * RE;
+        const int64_t sl = d.fwd_only ? 0 : l;
+        const float* x = ws + W.x + xs(l) * RE;
+        float* y1 = ws + W.y1 + sl * RE;
+        float* st1 = ws + W.st1 + sl * R * 2;
+        float* qkv = ws + W.qkv + sl * RE * 3;
+        float* Pm = d.fwd_only ? nullptr : ws + W.P + sl * TT;
+        float* o = ws + W.o + sl * RE;
+        float* x2 = ws + W.x2 + sl * RE;
+        float* y2 = ws + W.y2 + sl * RE;
+        float* st2 = ws + W.st2 + sl * R * 2;
+        float* hpre = ws + W.hpre + sl * RE * 4;
+        float* xn = ws + W.x + xs(l + 1) * RE;
         hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x,
                            blob + P.ln1_g, blob + P.ln1_b, R, E, y1, st1);
         hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 3)), dim3(kTrThreads), 0, st, y1, blob + P.attn_w,
@@ -459,7 +469,7 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
         if (int rc = launched("train forward layer")) return rc;
     }
     hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st,
-                       ws + W.x + d.L * RE, blob + B.lnf_g, blob + B.lnf_b, R, E, ws + W.yf, ws + W.stf);
+                       ws + W.x + xs(d.L) * RE, blob + B.lnf_g, blob + B.lnf_b, R, E, ws + W.yf, ws + W.stf);
     hipLaunchKernelGGL(tr_linear, dim3(blocks_for((int64_t)R * d.A)), dim3(kTrThreads), 0, st, ws + W.yf,
                        blob + B.head_w, blob + B.head_b, nullptr, R, E, d.A, 0, preds);
     return launched("train forward head");

@@ -67,8 +67,11 @@ def unpack_grads(dblob, params):
     return out
 
 
-def desc(n_layer, n_embd, state_dim, action_dim, n_positions, batch, window):
-    return _lib.TrainDesc(n_layer, n_embd, state_dim, action_dim, n_positions, batch, window, 0)
+FORWARD_ONLY = 1  # DPT_TRAIN_FORWARD_ONLY: inference workspace, no backward
+
+
+def desc(n_layer, n_embd, state_dim, action_dim, n_positions, batch, window, flags=0):
+    return _lib.TrainDesc(n_layer, n_embd, state_dim, action_dim, n_positions, batch, window, flags)
 
 
 def _numel(fn, d):
@@ -105,20 +108,28 @@ class TransformerFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, tokens, dims, *params):
-        d = desc(*dims)
+        # dims[7] (optional) = FORWARD_ONLY when the caller runs without autograd (no_grad, or
+        # no parameter requires grad): the forward-only workspace (one layer's activations, no
+        # attention probabilities, no backward scratch) -- and nothing saved for a backward
+        flags = dims[7] if len(dims) > 7 else 0
+        need = any(ctx.needs_input_grad[2:]) and not flags & FORWARD_ONLY
+        d = desc(*dims[:7], flags=0 if need else FORWARD_ONLY)
         dev = device()
         blob = pack_params(params, dev)
         if blob.numel() != _numel("dpt_train_blob_numel", d):
             raise ValueError("parameter shapes do not match the model description")
         tok = tokens.to(device=dev, dtype=torch.float32).contiguous()
         preds, ws = forward(d, blob, tok)
-        if any(ctx.needs_input_grad[2:]):
+        if need:
             ctx.d, ctx.blob, ctx.tok, ctx.ws = d, blob, tok, ws
             ctx.params_meta = [(p.shape, p.dtype, p.device) for p in params]
         return preds
 
     @staticmethod
     def backward(ctx, dpreds):
+        if getattr(ctx, "ws", None) is None:
+            raise RuntimeError("dpt_hip.train: the saved activations were released by the first backward; "
+                               "a second backward through the same graph (retain_graph=True) is not supported")
         dblob = backward(ctx.d, ctx.blob, ctx.tok, ctx.ws, dpreds)
         shapes = [torch.empty(s, dtype=dt, device="meta") for s, dt, _ in ctx.params_meta]
         grads = [g.to(dv) for g, (_, _, dv) in zip(unpack_grads(dblob, shapes), ctx.params_meta)]

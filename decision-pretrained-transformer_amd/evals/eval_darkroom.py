@@ -186,11 +186,14 @@ def offline(eval_trajs, model, n_eval, H, dim, permuted=False, uniforms=None):
         if sample and uniforms is not None:
             ctrl.uniforms = lambda k: uniforms[k]
         ctrl.set_batch(dict(batch))
-        dm = model.device_model()
-        c = (batch["context_states"], batch["context_actions"], batch["context_next_states"],
-             batch["context_rewards"][..., 0])
-        _, _, _, er = _episode_device(dm, ctrl, vec_env, c, H)
-        res[name] = er.sum(-1).cpu().numpy()
+        if _device_ok(vec_env, ctrl):
+            c = (batch["context_states"], batch["context_actions"], batch["context_next_states"],
+                 batch["context_rewards"][..., 0])
+            _, _, _, er = _episode_device(model.device_model(), ctrl, vec_env, c, H)
+            res[name] = er.sum(-1).cpu().numpy()
+        else:  # other widths / model classes: the controller's own per-step forward
+            _, _, _, rs = vec_env.deploy_eval(ctrl)
+            res[name] = np.sum(rs, axis=-1)
     means = {k: np.mean(v) for k, v in res.items()}
     colors = plt.cm.viridis(np.linspace(0, 1, len(means)))
     plt.bar(means.keys(), means.values(), color=colors)

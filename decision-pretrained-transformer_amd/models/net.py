@@ -154,8 +154,9 @@ class Transformer(nn.Module):
         whole model).  Used when autograd needs the graph and for widths other than 32."""
         from dpt_hip import train as tr
         tok = self._tokens(x)
+        grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         dims = (self.n_layer, self.n_embd, self.state_dim, self.action_dim, self.n_positions, tok.shape[0],
-                tok.shape[1])
+                tok.shape[1], 0 if grad else tr.FORWARD_ONLY)
         preds = tr.TransformerFunction.apply(tok, dims, *tr.param_list(self))
         return preds[:, -1, :] if self.test else preds[:, 1:, :]
 
@@ -168,7 +169,15 @@ class Transformer(nn.Module):
         kernels (dpt_hip.train.TransformerFunction): ``loss.backward()`` fills every
         parameter's ``.grad`` and the reference's AdamW step works unchanged.  Inference
         (eval.py:152 ``model.eval()``; train.py:265-278's test loss under ``torch.no_grad()``)
-        takes the fused kernels at width 32 and the generic kernels at other widths."""
+        takes the fused kernels at width 32 and the generic kernels at other widths.
+
+        Dropout: the reference's GPT2Config applies embd/attn/resid dropout with p = ``dropout``
+        (models/net.py:30-32) in training mode; the HIP kernels have no dropout, so a
+        training-mode forward with ``dropout > 0`` raises instead of silently skipping it
+        (``dropout = 0``, the common_args.py default, and eval mode are exact)."""
+        if self.training and self.dropout > 0:
+            raise NotImplementedError(f"dropout={self.dropout} in training mode: the HIP training kernels "
+                                      "implement dropout 0 only (set --dropout 0 or call model.eval())")
         if (self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())) \
                 or self.n_embd != dpt_hip.E:
             return self._forward_generic(x)

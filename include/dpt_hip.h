@@ -381,8 +381,12 @@ int dpt_regret_moments(const double* arm_value, const double* opt, int32_t N, in
 typedef struct dpt_train_desc {
     int32_t n_layer, n_embd, state_dim, action_dim, n_positions;
     int32_t batch, window;        /* sequences and tokens per sequence (1 + context length) */
-    int32_t reserved;
+    int32_t reserved;             /* flags: DPT_TRAIN_FORWARD_ONLY or 0 */
 } dpt_train_desc;
+/* Inference through the training forward (no backward will follow): the workspace holds one
+ * layer's activations and no attention probabilities or backward scratch
+ * (dpt_train_workspace_numel sizes it by the flag); dpt_train_backward rejects the desc. */
+#define DPT_TRAIN_FORWARD_ONLY 1
 int dpt_train_blob_numel(const dpt_train_desc* desc_host, int64_t* numel_out_host);
 int dpt_train_workspace_numel(const dpt_train_desc* desc_host, int64_t* numel_out_host);
 int dpt_train_forward(const dpt_train_desc* desc_host, const float* blob, const float* tokens, float* workspace,

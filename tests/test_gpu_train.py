@@ -197,3 +197,69 @@ def test_other_widths_forward_and_rollout(E):
     cm = eval_bandit.deploy_online_vec(vec, ctrl, H, uniforms=u, noise=gg)
     ref = O.bandit_online_rollout(W, means, H, 0.3, u, gg)
     assert np.array_equal(cm, ref["cum_means"])
+
+
+@pytest.mark.parametrize("E", [16, 64])
+def test_other_widths_darkroom_offline(E):
+    """evals/eval_darkroom.py offline (:124-189) with a model of width != 32: the DPT legs run the
+    controller's per-step forward (the generic kernels) and match the float64 oracle's episode fed
+    the same uniforms (sampled) and greedily."""
+    import matplotlib
+    matplotlib.use("Agg")
+    from models.net import Transformer
+    from oracle import dpt_oracle as O
+    from evals import eval_darkroom
+    torch.manual_seed(E + 1)
+    m = Transformer(dict(horizon=10, state_dim=2, action_dim=5, n_layer=2, n_embd=E, n_head=1, dropout=0.0,
+                         test=True)).cuda().eval()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.3 * torch.randn_like(p))
+    W = O.split_weights({k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}, 2)
+    rs = np.random.RandomState(E)
+    n, H = 4, 10
+    goals = rs.randint(0, 10, (n, 2))
+    trajs = [{"goal": goals[i], "context_states": rs.randint(0, 10, (H, 2)),
+              "context_actions": np.eye(5)[rs.randint(0, 5, H)], "context_next_states": rs.randint(0, 10, (H, 2)),
+              "context_rewards": rs.randint(0, 2, H)} for i in range(n)]
+    u = rs.uniform(size=(H, n))
+    res = eval_darkroom.offline(trajs, m, n_eval=n, H=H, dim=10, uniforms=u)
+    ctx = tuple(np.stack([t[k] for t in trajs]).astype(np.float64) for k in
+                ("context_states", "context_actions", "context_next_states"))
+    ctx = ctx + (np.stack([t["context_rewards"] for t in trajs])[..., None].astype(np.float64),)
+    assert np.array_equal(res["Opt"], O.darkroom_opt_returns(goals, H))
+    assert np.array_equal(res["Learner"], O.darkroom_offline_episode(W, goals, ctx, H, u, sample=True).sum(-1))
+    assert np.array_equal(res["Learner (greedy)"],
+                          O.darkroom_offline_episode(W, goals, ctx, H, None, sample=False).sum(-1))
+
+
+def test_forward_only_workspace_and_second_backward():
+    """Without autograd the generic forward runs on the forward-only workspace (DPT_TRAIN_FORWARD_ONLY:
+    one layer's activations, no attention probabilities): same preds bit for bit as the training
+    forward, a far smaller workspace, and dpt_train_backward refuses that desc.  A second backward
+    through one graph (retain_graph=True) raises an explicit error."""
+    import dpt_hip
+    from dpt_hip import train as tr
+    g = golden("train_grads.npz")
+    _, m = model_from_fixture("bandit5")
+    batch, _ = batch_from(g, "bandit5")
+    m.train()
+    full = m._forward_generic(batch)
+    with torch.no_grad():
+        fwd_only = m._forward_generic(batch)
+    assert torch.equal(full.detach(), fwd_only)
+    tok = m._tokens(batch)
+    dims = (m.n_layer, m.n_embd, m.state_dim, m.action_dim, m.n_positions, tok.shape[0], tok.shape[1])
+    n_full = tr._numel("dpt_train_workspace_numel", tr.desc(*dims))
+    n_inf = tr._numel("dpt_train_workspace_numel", tr.desc(*dims, flags=tr.FORWARD_ONLY))
+    assert n_inf * 3 < n_full, (n_inf, n_full)
+    d = tr.desc(*dims, flags=tr.FORWARD_ONLY)
+    blob = tr.pack_params(tr.param_list(m), dpt_hip.device())
+    preds, ws = tr.forward(d, blob, tok)
+    assert torch.equal(preds[:, 1:], full.detach())
+    with pytest.raises(ValueError, match="forward-only"):
+        tr.backward(d, blob, tok, ws, torch.ones_like(preds))
+    loss = full.square().sum()
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="retain_graph"):
+        loss.backward()

@@ -84,3 +84,21 @@ def test_train_blob_order_matches_pack_weights():
     assert len(ps) == len(sd) and sum(p.numel() for p in ps) == sum(v.numel() for v in sd.values())
     back = tr.unpack_grads(tr.pack_params(ps), ps)
     assert all(torch.equal(a, b) for a, b in zip(back, ps))
+
+
+def test_training_mode_dropout_is_rejected():
+    """GPT2Config applies dropout in training mode (models/net.py:30-32); the HIP kernels have none,
+    so a training-mode forward with dropout > 0 raises (with or without grad) instead of training
+    or evaluating without it.  Eval mode ignores dropout, as the reference does."""
+    import pytest
+    import torch
+    from models.net import Transformer
+    m = Transformer(dict(horizon=4, state_dim=1, action_dim=5, n_layer=2, n_embd=32, n_head=1, dropout=0.1,
+                         test=False))
+    with pytest.raises(NotImplementedError, match="dropout"):
+        m(_tiny_batch())
+    with torch.no_grad(), pytest.raises(NotImplementedError, match="dropout"):
+        m(_tiny_batch())
+    m.eval()
+    with pytest.raises(RuntimeError, match="ROCm GPU"):  # eval mode goes on to the (absent) GPU
+        m(_tiny_batch())
