@@ -180,6 +180,9 @@ class TrainDesc(ctypes.Structure):
                 ("n_positions", _i32), ("batch", _i32), ("window", _i32), ("reserved", _i32)]
 
 
+TRAIN_FORWARD_ONLY = 1  # dpt_train_desc.reserved flag (DPT_TRAIN_FORWARD_ONLY)
+
+
 SIGNATURES["dpt_train_blob_numel"] = (_i32, [ctypes.POINTER(TrainDesc), ctypes.POINTER(_i64)])
 SIGNATURES["dpt_train_workspace_numel"] = (_i32, [ctypes.POINTER(TrainDesc), ctypes.POINTER(_i64)])
 SIGNATURES["dpt_train_forward"] = (_i32, [ctypes.POINTER(TrainDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p,

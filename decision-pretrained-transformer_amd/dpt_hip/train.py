@@ -67,7 +67,7 @@ def unpack_grads(dblob, params):
     return out
 
 
-FORWARD_ONLY = 1  # DPT_TRAIN_FORWARD_ONLY: inference workspace, no backward
+FORWARD_ONLY = _lib.TRAIN_FORWARD_ONLY  # inference workspace, no backward
 
 
 def desc(n_layer, n_embd, state_dim, action_dim, n_positions, batch, window, flags=0):
