@@ -99,8 +99,12 @@ int dpt_device_count(int* count_out_host);
 
 /* ------------------------------------------------------------------ model
  * Replaces models/net.py:9-60 `Transformer` (+ transformers.GPT2Model with
- * n_head forced to 1, net.py:29).  Only n_embd == 32 (the reference default,
- * common_args.py:31) is built; n_layer is free.
+ * n_head forced to 1, net.py:29).  The dpt_model handle and every entry point
+ * that takes it (dpt_forward_window, dpt_decode_step, dpt_rollout_bandit,
+ * dpt_rollout_darkroom) are built for n_embd == 32 (the reference default,
+ * common_args.py:31); n_layer is free.  Any other width runs through the
+ * width-generic dpt_train_forward / dpt_train_backward below (same blob layout),
+ * which Transformer.forward uses for inference at such widths as well.
  *
  * Packed fp32 weight blob, in this order (all matrices stored [in][out]):
  *   emb_w [F][E]  emb_b [E]                 F = 2*state_dim + action_dim + 1
@@ -117,7 +121,7 @@ typedef struct dpt_model dpt_model;
 
 typedef struct dpt_model_desc {
     int32_t n_layer;
-    int32_t n_embd;      /* must be 32 */
+    int32_t n_embd;      /* must be 32 for this handle (other widths: dpt_train_*) */
     int32_t state_dim;
     int32_t action_dim;  /* 1..32 */
     int32_t n_positions; /* rows of wpe */

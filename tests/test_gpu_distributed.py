@@ -124,3 +124,52 @@ def test_bench_under_torchrun_two_ranks():
     assert line["config"]["tasks_per_gpu"] == 512 and line["config"]["horizon"] == 100
     assert line["config"]["env_steps_per_step"] == 2 * 512 * 100
     assert line["value"] > 0 and line["roofline"]["kernel_ms"] > 0
+
+
+def _worker_nccl(port, n_bandit, H, q):
+    sys.path[:0] = [PKG, ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    import dpt_hip
+    from dpt_hip.distributed import gather_rows, regret_stats_allreduce
+    sd, means = _bandit_case(n_bandit, H)
+    m = dpt_hip.DeviceModel(sd, 4, 1, 5, 4 * (1 + H))
+    local = torch.from_numpy(means).cuda()
+    out = m.rollout_bandit(local, H, 0.3, True, seed=555)
+    stats = regret_stats_allreduce(local.max(dim=1, keepdim=True).values, out["arm_value"], n_bandit)
+    curves = gather_rows(out["arm_value"], n_bandit)
+    t = torch.tensor([1.5, 2.5], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py's max-over-ranks timing reduction
+    dist.barrier()
+    q.put({"stats": {k: v.cpu().numpy() for k, v in stats.items()}, "curves": curves.cpu().numpy(),
+           "t": t.cpu().numpy()})
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_rccl_backend_paths_single_rank():
+    """The RCCL ("nccl" backend) branches the 8-GPU run takes, exercised with one rank on this box's
+    GPU: init_process_group("nccl", device_id=...), the device-tensor all_reduce of
+    regret_stats_allreduce, all_gather_into_tensor in gather_rows, bench.py's MAX reduction.
+    Results equal the process-local computation."""
+    import dpt_hip
+    from dpt_hip.distributed import regret_stats_allreduce
+    n_bandit, H = 777, 120
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_nccl, args=(_free_port(), n_bandit, H, q))
+    p.start()
+    got = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    sd, means = _bandit_case(n_bandit, H)
+    m = dpt_hip.DeviceModel(sd, 4, 1, 5, 4 * (1 + H))
+    md_means = torch.from_numpy(means).cuda()
+    out = m.rollout_bandit(md_means, H, 0.3, True, seed=555)
+    assert np.array_equal(got["curves"], out["arm_value"].cpu().numpy())
+    single = regret_stats_allreduce(md_means.max(dim=1, keepdim=True).values, out["arm_value"], n_bandit)
+    for k, v in single.items():
+        assert np.array_equal(got["stats"][k], v.cpu().numpy()), k
+    assert np.array_equal(got["t"], [1.5, 2.5])
