@@ -123,7 +123,7 @@ def cpu_baseline(sd, means, H, var, n_layer, A, n_rec=None, n_kv=2048):
     from oracle import c_oracle
     import dpt_hip
     threads, hw = host_cpus()
-    n_rec = n_rec or 2 * max(16, threads)  # two tasks per thread: ~10 s of work per thread at H=500
+    n_rec = n_rec or 4 * max(16, threads)  # four tasks per thread (~6 s at H=500 on the GPU box's EPYC)
     blob = dpt_hip.pack_weights(sd, n_layer).numpy()
     npos = 4 * (1 + H)
     rs = np.random.RandomState(7)
@@ -161,7 +161,7 @@ def cpu_baseline_darkroom(sd, goals, H, n_layer, n_tasks=None, n_eps=8):
     from oracle import c_oracle
     import dpt_hip
     threads, hw = host_cpus()
-    n_tasks = n_tasks or 2 * max(8, threads)
+    n_tasks = n_tasks or 4 * max(8, threads)
     blob = dpt_hip.pack_weights(sd, n_layer).numpy()
     u = np.random.RandomState(7).uniform(size=(n_eps * H, n_tasks))
     t0 = time.perf_counter()
