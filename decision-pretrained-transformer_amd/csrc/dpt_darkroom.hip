@@ -276,8 +276,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         P[pt.head_w + (i % kDrA) * kE + i / kDrA] = M.head_w[i];
     for (int i = tid; i < kDrA; i += blockDim.x) P[pt.head_b + i] = M.head_b[i];
     if constexpr (kSplitV) {  // finite values in tiles no episode has written yet (attend)
-        uint4* vs = reinterpret_cast<uint4*>(&S.kv.VS[0][0][0][0]);
-        for (int i = tid; i < (int)(sizeof(S.kv.VS) / 16); i += blockDim.x) vs[i] = uint4{0u, 0u, 0u, 0u};
+        uint4* vs = reinterpret_cast<uint4*>(&S.kv.VT[0][0][0]);
+        for (int i = tid; i < (int)(sizeof(S.kv.VT) / 16); i += blockDim.x) vs[i] = uint4{0u, 0u, 0u, 0u};
     }
     for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
 
@@ -637,8 +637,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         const Split2 ps = split2(pr, 1.0f);
                         const int pp = wave;
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-                        const floatx4 o0 = mfma_x3(Split2{S.kv.VS[pp][0][0][lane], S.kv.VS[pp][0][1][lane]}, ps, zero);
-                        const floatx4 o1 = mfma_x3(Split2{S.kv.VS[pp][1][0][lane], S.kv.VS[pp][1][1][lane]}, ps, zero);
+                        const int vlo = vt_lane_off(lane);
+                        const floatx4 o0 = mfma_x3(vt_split(S.kv, pp, 0, vlo), ps, zero);
+                        const floatx4 o1 = mfma_x3(vt_split(S.kv, pp, 1, vlo), ps, zero);
                         if (c == 0) {
                             *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
                             *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;

@@ -30,18 +30,21 @@ typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 // operand tiles of the score product (KS[block][part h|m][lane], y x 2^attn_ey, written
 // once by the lane that computed the key: 2 KB per 16 keys, no split per read).  Values
 // stay fp32 feature-major (Vt).
-// With SPLITV (requires SPLITK) the values are kept as the fp16 two-part A operand of
-// O^T += V^T P^T over a pair of key tiles (y x 2^attn_ey, the keys' split):
-// VS[pair][feature half][part h|m][lane (g, c)], element j = V[key 16 (2 pair + (j >> 2))
-// + 4g + (j & 3)][feature 16 half + c] (the lane group's k order of P^T's C-layout over
-// the two tiles), 4 KB per 32 keys.
+// With SPLITV (requires SPLITK) the values are kept as the fp16 two-part split of y x 2^attn_ey
+// (the keys' split), token-major: VT[part h|m][key][kVTRow] (features 0..31, rows padded to 72 B).
+// The writer lane holds two runs of 4 consecutive features of its token (C-layout) and
+// stores each as one 8-B write; the A operand of O^T += V^T P^T over a pair of key tiles
+// (element j of lane (g, c) = V[key 16 (2 pair + (j >> 2)) + 4g + (j & 3)][feature 16 half + c],
+// the lane group's k order of P^T's C-layout over the two tiles) is read back transposed by
+// two ds_read_b64_tr_b16 per part (vt_split).
+constexpr int kVTRow = kE + 4;  // halves per VT row: 72 B (8-B aligned rows for the transposed read)
 template <int TMAX, bool SPLITK = false, bool SPLITV = false>
 struct KVBuf {
     static_assert(SPLITK || !SPLITV, "split values need split keys");
     static constexpr bool kSplitK = SPLITK, kSplitV = SPLITV;
     float K[SPLITK ? 1 : TMAX][kKStride];
     halfx8 KS[SPLITK ? TMAX / 16 : 1][SPLITK ? 2 : 1][SPLITK ? 64 : 1];  // (16 B when unused)
-    halfx8 VS[SPLITV ? TMAX / 32 : 1][SPLITV ? 2 : 1][SPLITV ? 2 : 1][SPLITV ? 64 : 1];
+    _Float16 VT[SPLITV ? 2 : 1][SPLITV ? TMAX : 1][SPLITV ? kVTRow : 8];
     float Vt[SPLITV ? 1 : kE][TMAX + 4];
 };
 constexpr bool kSplitKeys = true;  // scores on mfma_x3 (and, with SPLITV, P V too)
@@ -105,6 +108,30 @@ __device__ inline floatx4 mfma_x3(const Split2& a, const Split2& b, floatx4 acc)
 }
 // 2^e as a float (|e| < 127)
 __device__ inline float exp2i(int e) { return __int_as_float((e + 127) << 23); }
+
+// The split A operand of O^T += V^T P^T for key-tile pair pp and feature half `half` from the
+// token-major VT image: per part two ds_read_b64_tr_b16 (T10: the 16-lane group g reads keys
+// 16 (2 pp + t) + 4g + q, q < 4, at features 16 half + 0..15; lane c receives feature c, key q
+// in element q).  `lo` = vt_lane_off() of the calling lane; EXEC must be all ones.
+typedef short i16x4 __attribute__((__vector_size__(4 * sizeof(short))));
+__device__ inline int vt_lane_off(int lane) {
+    // lane 4q + p of group g supplies row 4g + q, columns 4p..4p+3
+    return ((4 * (lane >> 4) + ((lane & 15) >> 2)) * kVTRow + 4 * (lane & 3)) * 2;  // bytes
+}
+template <class KV>
+__device__ inline Split2 vt_split(const KV& S, int pp, int half, int lo) {
+    typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+    const char* base = reinterpret_cast<const char*>(&S.VT[0][0][0]) + lo + (32 * pp * kVTRow + 16 * half) * 2;
+    constexpr int kPart = (int)sizeof(S.VT[0]), kTile = 16 * kVTRow * 2;
+    auto rd = [&](int off) {
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + off));
+    };
+    const i16x4 h0 = rd(0), h1 = rd(kTile), m0 = rd(kPart), m1 = rd(kPart + kTile);
+    typedef short i16x8 __attribute__((ext_vector_type(8)));
+    const i16x8 h = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    const i16x8 m = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+    return Split2{__builtin_bit_cast(halfx8, h), __builtin_bit_cast(halfx8, m)};
+}
 // scale of the attention probabilities in P V (P <= 2^8, so P x 2^kPExp < 2^14)
 constexpr int kPExp = 2;
 
@@ -389,16 +416,16 @@ __device__ inline void kv_store(KV& S, const int (&qb)[2], const float (&xn)[2][
             S.KS[qb[j]][0][lane] = xs[j].h;
             S.KS[qb[j]][1][lane] = xs[j].m;
             if constexpr (KV::kSplitV) {
-                // the same split parts, scattered into V^T's pair-tile order: value k of
-                // lane (g, c) is feature 16 (k >> 2) + 4g + (k & 3) of token 16 b + c
-                const int b = qb[j], c = lane & 15;
-                _Float16* vs = reinterpret_cast<_Float16*>(&S.VS[b >> 1][0][0][0]);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int off = ((k >> 2) * 2 * 64 + (c >> 2) * 16 + 4 * g + (k & 3)) * 8 + (b & 1) * 4 + (c & 3);
-                    vs[off] = xs[j].h[k];
-                    vs[off + 64 * 8] = xs[j].m[k];
-                }
+                // the same split parts, token-major: value k of lane (g, c) is feature
+                // 16 (k >> 2) + 4g + (k & 3) of token 16 b + c, so each half of the lane's 8
+                // values is 4 consecutive features: one 8-B store per part and half
+                const uint4 hu = __builtin_bit_cast(uint4, xs[j].h), mu = __builtin_bit_cast(uint4, xs[j].m);
+                _Float16* row = &S.VT[0][tok][4 * g];
+                *reinterpret_cast<uint2*>(row) = uint2{hu.x, hu.y};
+                *reinterpret_cast<uint2*>(row + 16) = uint2{hu.z, hu.w};
+                _Float16* rowm = &S.VT[1][tok][4 * g];
+                *reinterpret_cast<uint2*>(rowm) = uint2{mu.x, mu.y};
+                *reinterpret_cast<uint2*>(rowm + 16) = uint2{mu.z, mu.w};
             }
         }
 #pragma unroll
@@ -470,6 +497,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         // tile and the tile holding key_lo.
         constexpr float kSlackP = 8.f;
         const float inv_scale = 1.0f / scale;
+        const int vlo = vt_lane_off(lane);
         m = -INFINITY;
         lsum = 0.f;
         float thr = -INFINITY, bm = 0.f;  // bm = 0 while no key (not NaN)
@@ -524,8 +552,8 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
             lsum += l2.x + l2.y;
             const Split2 ps = split2(pr, 1.0f);
             const int pp = kb >> 1;
-            o0 = mfma_x3(Split2{S.VS[pp][0][0][lane], S.VS[pp][0][1][lane]}, ps, o0);
-            o1 = mfma_x3(Split2{S.VS[pp][1][0][lane], S.VS[pp][1][1][lane]}, ps, o1);
+            o0 = mfma_x3(vt_split(S, pp, 0, vlo), ps, o0);
+            o1 = mfma_x3(vt_split(S, pp, 1, vlo), ps, o1);
         };
         const int kb_last = qb & ~1;  // the pair holding the diagonal tile
         int kb = 0;

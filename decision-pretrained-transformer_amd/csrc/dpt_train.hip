@@ -19,7 +19,7 @@
 namespace dpt {
 
 constexpr int kTrThreads = 256;
-constexpr int kTrRowsPerChunk = 256;  // rows per partial of the weight-gradient reductions
+constexpr int kTrRowsPerChunk = 64;   // rows per partial of the weight-gradient reductions
 
 
 // offsets of one layer in the packed blob (dpt_hip.h: [ln1 g b][c_attn W b][c_proj W b][ln2 g b][c_fc W b][mlp.c_proj W b])
@@ -67,38 +67,41 @@ struct TrWs {
     int64_t x, y1, st1, qkv, P, o, x2, y2, st2, hpre, yf, stf;  // x: [L+1][R][E]; per-layer arrays [L][...]
     int64_t dx, dx2, dqkv, dout, dh, dy, dS, part, total;
     __host__ __device__ static int64_t nchunks(const TrDims& d) { return (d.R() + kTrRowsPerChunk - 1) / kTrRowsPerChunk; }
+    __host__ __device__ static int tpad(int T) { return (T + 3) & ~3; }
     __host__ __device__ static TrWs make(const TrDims& d) {
         TrWs w;
-        const int64_t R = d.R(), E = d.E, TT = (int64_t)d.B * d.T * d.T;
+        // every array starts 16-B aligned (the matrix-core kernels read rows as float4); the
+        // attention probabilities / score gradients have rows padded to a multiple of 4 (tpad)
+        const int64_t R = d.R(), E = d.E, TT = (int64_t)d.B * d.T * tpad(d.T);
         // forward-only: one slot per per-layer array (x ping-pongs over two), no probabilities,
         // no backward scratch
         const int64_t L = d.fwd_only ? 1 : d.L;
         int64_t p = 0;
-        w.x = p; p += (d.fwd_only ? 2 : L + 1) * R * E;
-        w.y1 = p; p += L * R * E;
-        w.st1 = p; p += L * R * 2;
-        w.qkv = p; p += L * R * 3 * E;
-        w.P = p; p += d.fwd_only ? 0 : L * TT;
-        w.o = p; p += L * R * E;
-        w.x2 = p; p += L * R * E;
-        w.y2 = p; p += L * R * E;
-        w.st2 = p; p += L * R * 2;
-        w.hpre = p; p += L * R * 4 * E;
-        w.yf = p; p += R * E;
-        w.stf = p; p += R * 2;
+        w.x = p; p += (d.fwd_only ? 2 : L + 1) * R * E; p = (p + 3) & ~3ll;
+        w.y1 = p; p += L * R * E; p = (p + 3) & ~3ll;
+        w.st1 = p; p += L * R * 2; p = (p + 3) & ~3ll;
+        w.qkv = p; p += L * R * 3 * E; p = (p + 3) & ~3ll;
+        w.P = p; p += d.fwd_only ? 0 : L * TT; p = (p + 3) & ~3ll;
+        w.o = p; p += L * R * E; p = (p + 3) & ~3ll;
+        w.x2 = p; p += L * R * E; p = (p + 3) & ~3ll;
+        w.y2 = p; p += L * R * E; p = (p + 3) & ~3ll;
+        w.st2 = p; p += L * R * 2; p = (p + 3) & ~3ll;
+        w.hpre = p; p += L * R * 4 * E; p = (p + 3) & ~3ll;
+        w.yf = p; p += R * E; p = (p + 3) & ~3ll;
+        w.stf = p; p += R * 2; p = (p + 3) & ~3ll;
         if (d.fwd_only) {
             w.dx = w.dx2 = w.dqkv = w.dout = w.dh = w.dy = w.dS = w.part = w.total = p;
             return w;
         }
-        w.dx = p; p += R * E;
-        w.dx2 = p; p += R * E;
-        w.dqkv = p; p += R * 3 * E;
-        w.dout = p; p += R * E;
-        w.dh = p; p += R * 4 * E;
-        w.dy = p; p += R * E;
-        w.dS = p; p += TT;
+        w.dx = p; p += R * E; p = (p + 3) & ~3ll;
+        w.dx2 = p; p += R * E; p = (p + 3) & ~3ll;
+        w.dqkv = p; p += R * 3 * E; p = (p + 3) & ~3ll;
+        w.dout = p; p += R * E; p = (p + 3) & ~3ll;
+        w.dh = p; p += R * 4 * E; p = (p + 3) & ~3ll;
+        w.dy = p; p += R * E; p = (p + 3) & ~3ll;
+        w.dS = p; p += TT; p = (p + 3) & ~3ll;
         const int64_t wmax = std::max<int64_t>(4 * E * E + 4 * E, (int64_t)(d.F + 1) * E);
-        w.part = p; p += nchunks(d) * std::max<int64_t>(wmax, (int64_t)(E + 1) * d.A);
+        w.part = p; p += nchunks(d) * std::max<int64_t>(wmax, (int64_t)(E + 1) * d.A); p = (p + 3) & ~3ll;
         w.total = p;
         return w;
     }
@@ -384,6 +387,349 @@ __global__ void tr_wpe_grad(const float* __restrict__ dx, TrDims d, float* __res
     dwpe[i] = acc;
 }
 
+// ------------------------------------------------------------------------------ matrix-core forms
+// The row products and weight gradients of widths E in {16, 32, 64} (every dimension a multiple of
+// 16) on v_mfma_f32_16x16x4_f32 (fp32 products and accumulation, like the row kernels above; a
+// different but fixed summation order, so results stay deterministic).
+
+// Y[r][n] = epi( sum_k act(X[r][k]) B[k][n] ), B = W ([K][N]) or, TRANS, W^T (W stored [N][K]).
+// One wave = 16 rows x all N columns, 4 waves = 64 rows per workgroup; B is staged in LDS once
+// per workgroup.  The k order inside a lane is permuted -- lane (row i, kq) holds
+// k = kq (K/4) + s at step s, a contiguous run of its row -- and B is read at the same k.
+// EPI: bit 0 + bias[n], bit 1 + res[r][n], bit 2 x gelu'(aux[r][n]); ACT: gelu_new on X.
+constexpr int kMmBias = 1, kMmRes = 2, kMmGeluGrad = 4;
+// LDS row stride of B (floats): the four 16-lane groups of a B read hit rows KS apart, so pad
+// N until two groups of one 32-lane half land 16 banks apart (2-way at worst when impossible)
+__host__ __device__ constexpr int mm_ldb(int K, int N) {
+    for (int p = 0; p < 32; ++p)
+        if (((K / 4) * (N + p)) % 32 == 16) return N + p;
+    return N + 1;
+}
+template <int K, int N, bool TRANS, bool ACT, int EPI>
+__global__ __launch_bounds__(256) void tr_mm_rows(const float* __restrict__ X, const float* __restrict__ W,
+                                                  const float* __restrict__ bias, const float* __restrict__ res,
+                                                  const float* __restrict__ aux, int R, float* __restrict__ Y) {
+    static_assert(K % 16 == 0 && N % 16 == 0, "K, N multiples of 16");
+    constexpr int KS = K / 4;  // k-steps
+    constexpr int LDB = mm_ldb(K, N);
+    extern __shared__ float Bs[];  // [K][LDB]
+    for (int i = threadIdx.x; i < K * N; i += 256) {
+        const int k = i / N, n = i % N;
+        Bs[k * LDB + n] = TRANS ? W[(int64_t)n * K + k] : W[i];
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, kq = lane >> 4;
+    const int row0 = (blockIdx.x * 4 + wave) * 16;
+    const int row = min(row0 + i16, R - 1);  // rows past R compute garbage that is never stored
+    float a[KS];
+    const floatx4* xr = reinterpret_cast<const floatx4*>(X + (int64_t)row * K + kq * KS);
+#pragma unroll
+    for (int s4 = 0; s4 < KS / 4; ++s4) {
+        const floatx4 v = xr[s4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[4 * s4 + q] = ACT ? tr_gelu(v[q]) : v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < N / 16; ++c) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], Bs[(kq * KS + s) * LDB + 16 * c + i16], acc, 0, 0, 0);
+        const int n = 16 * c + i16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int rr = row0 + 4 * kq + r;
+            if (rr >= R) continue;
+            const int64_t o = (int64_t)rr * N + n;
+            float v = acc[r];
+            if (EPI & kMmBias) v += bias[n];
+            if (EPI & kMmRes) v += res[o];
+            if (EPI & kMmGeluGrad) v *= tr_gelu_grad(aux[o]);
+            Y[o] = v;
+        }
+    }
+}
+
+// Weight-gradient partials of one chunk of kTrRowsPerChunk rows: part[c][i][o] = sum_r act(X[r][i])
+// dY[r][o] (i < IN) and part[c][IN][o] = sum_r dY[r][o], summed over the chunks in order by
+// tr_wgrad_reduce.  The chunk's rows are staged in LDS (zeros past R); each wave takes output
+// tiles (IN / 16) x (OUT / 16) round robin, 16 MFMA k-steps of 4 rows each.
+template <int IN, int OUT, bool ACT>
+__global__ __launch_bounds__(256) void tr_wgrad_mfma(const float* __restrict__ X, const float* __restrict__ dY,
+                                                     int R, float* __restrict__ part) {
+    static_assert(IN % 16 == 0 && OUT % 16 == 0, "IN, OUT multiples of 16");
+    constexpr int C = kTrRowsPerChunk;
+    extern __shared__ float sm[];
+    float* Xs = sm;            // [C][IN + 1]: padded rows (conflict-free column reads)
+    float* Ds = sm + C * (IN + 1);  // [C][OUT]
+    const int r0 = blockIdx.x * C;
+    for (int i = threadIdx.x; i < C * IN; i += 256) {
+        const int r = i / IN, k = i % IN;
+        const float v = r0 + r < R ? X[(int64_t)(r0 + r) * IN + k] : 0.f;
+        Xs[r * (IN + 1) + k] = ACT ? tr_gelu(v) : v;
+    }
+    for (int i = threadIdx.x; i < C * OUT; i += 256) {
+        const int r = i / OUT;
+        Ds[i] = r0 + r < R ? dY[(int64_t)r0 * OUT + i] : 0.f;
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, kq = lane >> 4;
+    float* pc = part + (int64_t)blockIdx.x * (IN + 1) * OUT;
+    for (int t = wave; t < (IN / 16) * (OUT / 16); t += 4) {
+        const int ti = t / (OUT / 16), to = t % (OUT / 16);
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < C / 4; ++s) {
+            const int r = 4 * s + kq;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Xs[r * (IN + 1) + 16 * ti + i16], Ds[r * OUT + 16 * to + i16], acc,
+                                                       0, 0, 0);
+        }
+        // C layout: lane (o = i16, kq) holds rows i = 16 ti + 4 kq + r
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pc[(16 * ti + 4 * kq + r) * OUT + 16 * to + i16] = acc[r];
+    }
+    // the bias row: sum over the chunk's rows in order, one thread per output column
+    for (int o = threadIdx.x; o < OUT; o += 256) {
+        float acc = 0.f;
+        for (int r = 0; r < C; ++r) acc += Ds[r * OUT + o];
+        pc[IN * OUT + o] = acc;
+    }
+}
+
+// ---- causal attention on the matrix cores (one head of width E; qkv rows [q | k | v], row stride 3E).
+// A wave owns 16 queries (or, dkv, 16 keys); products are 16 x 16 tiles of v_mfma_f32_16x16x4_f32 with
+// the tokens of the wave on the lane index: S^T = K Q^T gives lane (query n, g) the keys 4g + r of a
+// 16-key tile, which is exactly the B operand of O^T += V^T P^T over that tile (k-step r takes keys
+// 4g' + r of lane group g').  Feature k order of the Q / K products permuted per lane (run g E/4 .. ).
+__device__ inline float grp_max(float v) {
+    v = fmaxf(v, __shfl_xor(v, 16));
+    return fmaxf(v, __shfl_xor(v, 32));
+}
+__device__ inline float grp_sum(float v) {
+    v += __shfl_xor(v, 16);
+    return v + __shfl_xor(v, 32);
+}
+// lane (token n, g): row tok of the [rows][3E] qkv block at column off, features g E/4 .. g E/4 + E/4 - 1
+template <int E>
+__device__ inline void frag_row(const float* __restrict__ base, int tok, int off, float (&f)[E / 4]) {
+    const floatx4* r = reinterpret_cast<const floatx4*>(base + (int64_t)tok * 3 * E + off + (threadIdx.x & 63) / 16 * (E / 4));
+#pragma unroll
+    for (int j = 0; j < E / 16; ++j) {
+        const floatx4 v = r[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) f[4 * j + q] = v[q];
+    }
+}
+// 4 consecutive entries of a T-wide row starting at column c (c % 4 == 0): columns >= T are not
+// touched (stores) or read as 0 (loads)
+__device__ inline void row4_store(float* row, int c, int T, floatx4 v) {
+    if (c + 3 < T) {
+        *reinterpret_cast<floatx4*>(row + c) = v;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (c + r < T) row[c + r] = v[r];
+    }
+}
+__device__ inline floatx4 row4_load(const float* row, int c, int T) {
+    if (c + 3 < T) return *reinterpret_cast<const floatx4*>(row + c);
+    floatx4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = c + r < T ? row[c + r] : 0.f;
+    return v;
+}
+template <int E>
+__device__ inline floatx4 tile_dot(const float (&a)[E / 4], const float (&b)[E / 4]) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < E / 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+    return acc;
+}
+
+// forward: P (saved unless null; rows of keys <= query, zeros past the diagonal inside the diagonal
+// tile) and O = softmax(Q K^T / sqrt(E)) V.  Two passes over the key tiles: the row max and sum,
+// then the probabilities and O.  grid (B, ceil(T / 64)), 256 threads.
+template <int E>
+__global__ __launch_bounds__(256) void tr_attn_fwd_mfma(const float* __restrict__ qkv, TrDims d, float* __restrict__ P,
+                                                        float* __restrict__ O) {
+    const int T = d.T, TP = (T + 3) & ~3, b = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = lane & 15, g = lane >> 4;  // P / dS rows are TP floats (TrWs::tpad)
+    const int q0 = blockIdx.y * 64 + wave * 16;
+    if (q0 >= T) return;
+    const float* base = qkv + (int64_t)b * T * 3 * E;
+    const int qn = q0 + n, qc = min(qn, T - 1);
+    float qf[E / 4];
+    frag_row<E>(base, qc, 0, qf);
+    const float scale = 1.0f / sqrtf((float)E);
+    const int nkt = (min(q0 + 15, T - 1)) / 16 + 1;  // key tiles up to the diagonal
+    auto scores = [&](int kt, float (&sv)[4]) {
+        float kf[E / 4];
+        frag_row<E>(base, min(16 * kt + n, T - 1), E, kf);
+        const floatx4 acc = tile_dot<E>(kf, qf);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int key = 16 * kt + 4 * g + r;
+            sv[r] = (key <= qn && key < T) ? acc[r] * scale : -INFINITY;
+        }
+    };
+    float m = -INFINITY, l = 0.f;
+    for (int kt = 0; kt < nkt; ++kt) {
+        float sv[4];
+        scores(kt, sv);
+        const float mt = grp_max(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])));
+        const float mn = fmaxf(m, mt);
+        l = (m == -INFINITY ? 0.f : l * expf(m - mn));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) l += expf(sv[r] - mn);
+        m = mn;
+    }
+    const float inv = 1.0f / grp_sum(l);
+    floatx4 o[E / 16];
+#pragma unroll
+    for (int ft = 0; ft < E / 16; ++ft) o[ft] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nkt; ++kt) {
+        float sv[4];
+        scores(kt, sv);
+        floatx4 pv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pv[r] = expf(sv[r] - m) * inv;
+        if (P && qn < T) row4_store(P + ((int64_t)b * T + qn) * TP, 16 * kt + 4 * g, T, pv);
+#pragma unroll
+        for (int ft = 0; ft < E / 16; ++ft)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float v = base[(int64_t)min(16 * kt + 4 * g + r, T - 1) * 3 * E + 2 * E + 16 * ft + n];
+                o[ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, pv[r], o[ft], 0, 0, 0);
+            }
+    }
+    if (qn < T)
+#pragma unroll
+        for (int ft = 0; ft < E / 16; ++ft) *reinterpret_cast<floatx4*>(O + ((int64_t)b * T + qn) * E + 16 * ft + 4 * g) = o[ft];
+}
+
+// backward, per 16 queries: D = dO . O, dP = dO V^T, dS = P (dP - D) (stored for the dK pass), dQ =
+// dS K / sqrt(E) into dqkv[:, 0:E].  grid (B, ceil(T / 64)).
+template <int E>
+__global__ __launch_bounds__(256) void tr_attn_bwd_dq_mfma(const float* __restrict__ qkv, const float* __restrict__ P,
+                                                           const float* __restrict__ O, const float* __restrict__ dO,
+                                                           TrDims d, float* __restrict__ dS,
+                                                           float* __restrict__ dqkv) {
+    const int T = d.T, TP = (T + 3) & ~3, b = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = lane & 15, g = lane >> 4;  // P / dS rows are TP floats (TrWs::tpad)
+    const int q0 = blockIdx.y * 64 + wave * 16;
+    if (q0 >= T) return;
+    const float* base = qkv + (int64_t)b * T * 3 * E;
+    const int qn = q0 + n, qc = min(qn, T - 1);
+    const int64_t orow = ((int64_t)b * T + qc) * E + g * (E / 4);
+    float df[E / 4], dd = 0.f;
+#pragma unroll
+    for (int s = 0; s < E / 4; ++s) {
+        df[s] = dO[orow + s];
+        dd = fmaf(df[s], O[orow + s], dd);
+    }
+    dd = grp_sum(dd);
+    const float scale = 1.0f / sqrtf((float)E);
+    const int nkt = (min(q0 + 15, T - 1)) / 16 + 1;
+    floatx4 dq[E / 16];
+#pragma unroll
+    for (int ft = 0; ft < E / 16; ++ft) dq[ft] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nkt; ++kt) {
+        float vf[E / 4];
+        frag_row<E>(base, min(16 * kt + n, T - 1), 2 * E, vf);
+        const floatx4 dp = tile_dot<E>(vf, df);  // lane (query n, g): dP[query][keys 16 kt + 4g + r]
+        const floatx4 pv = row4_load(P + ((int64_t)b * T + qc) * TP, 16 * kt + 4 * g, T);  // 0 past T
+        floatx4 ds;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ds[r] = pv[r] * (dp[r] - dd);
+        if (qn < T) row4_store(dS + ((int64_t)b * T + qn) * TP, 16 * kt + 4 * g, T, ds);
+#pragma unroll
+        for (int ft = 0; ft < E / 16; ++ft)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float kv = base[(int64_t)min(16 * kt + 4 * g + r, T - 1) * 3 * E + E + 16 * ft + n];
+                dq[ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(kv, ds[r], dq[ft], 0, 0, 0);
+            }
+    }
+    if (qn < T)
+#pragma unroll
+        for (int ft = 0; ft < E / 16; ++ft)
+            *reinterpret_cast<floatx4*>(dqkv + ((int64_t)b * T + qn) * 3 * E + 16 * ft + 4 * g) = dq[ft] * scale;
+}
+
+// backward, per 16 keys: dK = dS^T Q / sqrt(E), dV = P^T dO into dqkv[:, E:3E], over the query tiles
+// from the key tile's own (causal) to the last.  grid (B, ceil(T / 64)).
+template <int E>
+__global__ __launch_bounds__(256) void tr_attn_bwd_dkv_mfma(const float* __restrict__ qkv, const float* __restrict__ P,
+                                                            const float* __restrict__ dS, const float* __restrict__ dO,
+                                                            TrDims d, float* __restrict__ dqkv) {
+    const int T = d.T, TP = (T + 3) & ~3, b = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = lane & 15, g = lane >> 4;  // P / dS rows are TP floats (TrWs::tpad)
+    const int k0 = blockIdx.y * 64 + wave * 16;
+    if (k0 >= T) return;
+    const float* base = qkv + (int64_t)b * T * 3 * E;
+    const int kn = k0 + n;
+    floatx4 dk[E / 16], dv[E / 16];
+#pragma unroll
+    for (int ft = 0; ft < E / 16; ++ft) dk[ft] = dv[ft] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int nqt = (T - 1) / 16 + 1;
+    for (int qt = k0 / 16; qt < nqt; ++qt) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int q = 16 * qt + 4 * s + g;  // k-step s: queries 16 qt + 4 s + g'
+            const bool live = q < T && kn < T;
+            const int64_t prow = ((int64_t)b * T + min(q, T - 1)) * TP + min(kn, T - 1);
+            const float dsv = live ? dS[prow] : 0.f, pvv = live ? P[prow] : 0.f;
+#pragma unroll
+            for (int ft = 0; ft < E / 16; ++ft) {
+                const int64_t qrow = (int64_t)min(q, T - 1);
+                const float qv = base[qrow * 3 * E + 16 * ft + n];
+                const float gv = dO[((int64_t)b * T + qrow) * E + 16 * ft + n];
+                dk[ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(qv, dsv, dk[ft], 0, 0, 0);
+                dv[ft] = __builtin_amdgcn_mfma_f32_16x16x4f32(gv, pvv, dv[ft], 0, 0, 0);
+            }
+        }
+    }
+    const float scale = 1.0f / sqrtf((float)E);
+    if (kn < T)
+#pragma unroll
+        for (int ft = 0; ft < E / 16; ++ft) {
+            float* row = dqkv + ((int64_t)b * T + kn) * 3 * E;
+            *reinterpret_cast<floatx4*>(row + E + 16 * ft + 4 * g) = dk[ft] * scale;
+            *reinterpret_cast<floatx4*>(row + 2 * E + 16 * ft + 4 * g) = dv[ft];
+        }
+}
+
+// LayerNorm parameter partials of one chunk: part[c][0][e] = sum_r dy n, part[c][1][e] = sum_r dy
+// with 256 / E row lanes per column, combined in a fixed order through LDS.
+__global__ __launch_bounds__(256) void tr_ln_param_part2(const float* __restrict__ x, const float* __restrict__ st,
+                                                         const float* __restrict__ dy, int R, int E,
+                                                         float* __restrict__ part) {
+    __shared__ float sg[256], sb[256];
+    const int c = blockIdx.x, t = threadIdx.x, lanes = 256 / E;
+    const int e = t % E, rl = t / E;
+    const int r0 = c * kTrRowsPerChunk, r1 = min(R, r0 + kTrRowsPerChunk);
+    float g = 0.f, b = 0.f;
+    if (rl < lanes)
+        for (int r = r0 + rl; r < r1; r += lanes) {
+            const float n = (x[(int64_t)r * E + e] - st[2 * r]) * st[2 * r + 1];
+            const float v = dy[(int64_t)r * E + e];
+            g = fmaf(v, n, g);
+            b += v;
+        }
+    sg[t] = g;
+    sb[t] = b;
+    __syncthreads();
+    if (t < E) {
+        float G = 0.f, Bb = 0.f;
+        for (int k = 0; k < lanes; ++k) {
+            G += sg[k * E + t];
+            Bb += sb[k * E + t];
+        }
+        part[(int64_t)c * 2 * E + t] = G;
+        part[(int64_t)c * 2 * E + E + t] = Bb;
+    }
+}
+
 // ------------------------------------------------------------------------------ host side
 
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + kTrThreads - 1) / kTrThreads); }
@@ -416,10 +762,105 @@ static int wgrad(const float* X, const float* dY, int R, int IN, int OUT, int ge
 static int ln_param_grad(const float* x, const float* stt, const float* dy, int R, int E, float* part, float* dg,
                          float* db, hipStream_t st) {
     const int nch = (R + kTrRowsPerChunk - 1) / kTrRowsPerChunk;
-    hipLaunchKernelGGL(tr_ln_param_part, dim3(nch, blocks_for(E)), dim3(kTrThreads), 0, st, x, stt, dy, R, E, part);
+    if (E <= 256)  // 256 / E row lanes per column (fixed-order LDS combine)
+        hipLaunchKernelGGL(tr_ln_param_part2, dim3(nch), dim3(256), 0, st, x, stt, dy, R, E, part);
+    else
+        hipLaunchKernelGGL(tr_ln_param_part, dim3(nch, blocks_for(E)), dim3(kTrThreads), 0, st, x, stt, dy, R, E, part);
     // the (2, E) partials reduce like a bias-only weight gradient: IN = 1, OUT = E, [sum dy n | sum dy]
     hipLaunchKernelGGL(tr_wgrad_reduce, dim3(blocks_for(2 * E)), dim3(kTrThreads), 0, st, part, nch, 1, E, dg, db);
     return launched("tr_ln_param");
+}
+
+// ---- matrix-core dispatch (widths 16, 32, 64; other widths keep the row kernels)
+static bool mm_fast(int E) { return E == 16 || E == 32 || E == 64; }
+enum MmKind { kMmQkv, kMmProj, kMmFc, kMmMp, kMmBdMp, kMmBdFc, kMmBdProj, kMmBdQkv };
+
+template <class Kern>
+static void allow_lds(Kern k, size_t bytes) {
+    if (bytes > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+template <int K, int N, bool TRANS, bool ACT, int EPI>
+static void launch_mm(const float* X, const float* W, const float* bias, const float* res, const float* aux, int R,
+                      float* Y, hipStream_t st) {
+    const size_t lds = sizeof(float) * K * mm_ldb(K, N);
+    allow_lds(tr_mm_rows<K, N, TRANS, ACT, EPI>, lds);
+    hipLaunchKernelGGL((tr_mm_rows<K, N, TRANS, ACT, EPI>), dim3((R + 63) / 64), dim3(256), lds, st, X, W, bias, res,
+                       aux, R, Y);
+}
+// the layer's row products: forward (qkv, c_proj + residual, c_fc, gelu -> mlp.c_proj + residual)
+// and the backward data products (dh = dx W_mp^T x gelu'(hpre), dy2 = dh W_fc^T, dout = dx2 W_proj^T,
+// dy1 = dqkv W_attn^T); W in the blob's [in][out] layout
+template <int E>
+static void mm_kind(int kind, const float* X, const float* W, const float* bias, const float* res, const float* aux,
+                    int R, float* Y, hipStream_t st) {
+    switch (kind) {
+        case kMmQkv: launch_mm<E, 3 * E, false, false, kMmBias>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmProj: launch_mm<E, E, false, false, kMmBias | kMmRes>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmFc: launch_mm<E, 4 * E, false, false, kMmBias>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmMp: launch_mm<4 * E, E, false, true, kMmBias | kMmRes>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmBdMp: launch_mm<E, 4 * E, true, false, kMmGeluGrad>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmBdFc: launch_mm<4 * E, E, true, false, 0>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmBdProj: launch_mm<E, E, true, false, 0>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmBdQkv: launch_mm<3 * E, E, true, false, 0>(X, W, bias, res, aux, R, Y, st); break;
+    }
+}
+static void mm(int E, int kind, const float* X, const float* W, const float* bias, const float* res, const float* aux,
+               int R, float* Y, hipStream_t st) {
+    if (E == 16) mm_kind<16>(kind, X, W, bias, res, aux, R, Y, st);
+    else if (E == 32) mm_kind<32>(kind, X, W, bias, res, aux, R, Y, st);
+    else mm_kind<64>(kind, X, W, bias, res, aux, R, Y, st);
+}
+
+template <int IN, int OUT, bool ACT>
+static void launch_wg(const float* X, const float* dY, int R, float* part, hipStream_t st) {
+    const size_t lds = sizeof(float) * kTrRowsPerChunk * (IN + 1 + OUT);
+    allow_lds(tr_wgrad_mfma<IN, OUT, ACT>, lds);
+    hipLaunchKernelGGL((tr_wgrad_mfma<IN, OUT, ACT>), dim3((R + kTrRowsPerChunk - 1) / kTrRowsPerChunk), dim3(256), lds,
+                       st, X, dY, R, part);
+}
+// weight gradients of the layer's products: in = gelu(hpre) / y2 / o / y1, dY = dx / dh / dx2 / dqkv
+template <int E>
+static void wg_kind(int kind, const float* X, const float* dY, int R, float* part, hipStream_t st) {
+    switch (kind) {
+        case kMmMp: launch_wg<4 * E, E, true>(X, dY, R, part, st); break;
+        case kMmFc: launch_wg<E, 4 * E, false>(X, dY, R, part, st); break;
+        case kMmProj: launch_wg<E, E, false>(X, dY, R, part, st); break;
+        case kMmQkv: launch_wg<E, 3 * E, false>(X, dY, R, part, st); break;
+    }
+}
+static int wgrad_fast(int E, int kind, const float* X, const float* dY, int R, int IN, int OUT, float* part, float* dW,
+                      float* db, hipStream_t st) {
+    if (E == 16) wg_kind<16>(kind, X, dY, R, part, st);
+    else if (E == 32) wg_kind<32>(kind, X, dY, R, part, st);
+    else wg_kind<64>(kind, X, dY, R, part, st);
+    const int nch = (R + kTrRowsPerChunk - 1) / kTrRowsPerChunk;
+    hipLaunchKernelGGL(tr_wgrad_reduce, dim3(blocks_for((int64_t)(IN + 1) * OUT)), dim3(kTrThreads), 0, st, part, nch,
+                       IN, OUT, dW, db);
+    return launched("tr_wgrad_mfma");
+}
+
+template <int E>
+static void attn_fwd_e(const float* qkv, const TrDims& d, float* P, float* O, hipStream_t st) {
+    hipLaunchKernelGGL(tr_attn_fwd_mfma<E>, dim3(d.B, (d.T + 63) / 64), dim3(256), 0, st, qkv, d, P, O);
+}
+static void attn_fwd_fast(int E, const float* qkv, const TrDims& d, float* P, float* O, hipStream_t st) {
+    if (E == 16) attn_fwd_e<16>(qkv, d, P, O, st);
+    else if (E == 32) attn_fwd_e<32>(qkv, d, P, O, st);
+    else attn_fwd_e<64>(qkv, d, P, O, st);
+}
+template <int E>
+static void attn_bwd_e(const float* qkv, const float* P, const float* O, const float* dO, const TrDims& d, float* dS,
+                       float* dqkv, hipStream_t st) {
+    const dim3 grid(d.B, (d.T + 63) / 64);
+    hipLaunchKernelGGL(tr_attn_bwd_dq_mfma<E>, grid, dim3(256), 0, st, qkv, P, O, dO, d, dS, dqkv);
+    hipLaunchKernelGGL(tr_attn_bwd_dkv_mfma<E>, grid, dim3(256), 0, st, qkv, P, dS, dO, d, dqkv);
+}
+static void attn_bwd_fast(int E, const float* qkv, const float* P, const float* O, const float* dO, const TrDims& d,
+                          float* dS, float* dqkv, hipStream_t st) {
+    if (E == 16) attn_bwd_e<16>(qkv, P, O, dO, d, dS, dqkv, st);
+    else if (E == 32) attn_bwd_e<32>(qkv, P, O, dO, d, dS, dqkv, st);
+    else attn_bwd_e<64>(qkv, P, O, dO, d, dS, dqkv, st);
 }
 
 int train_forward(const TrDims& d, const float* blob, const float* tok, float* ws, float* preds, hipStream_t st) {
@@ -427,10 +868,10 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
     const TrBlob B = TrBlob::make(d);
     const TrWs W = TrWs::make(d);
     const int R = d.R(), E = d.E;
-    const int64_t RE = (int64_t)R * E, TT = (int64_t)d.B * d.T * d.T;
+    const int64_t RE = (int64_t)R * E, TT = (int64_t)d.B * d.T * TrWs::tpad(d.T);
     const int rows_per_block = kTrThreads / 64;
     const size_t attn_lds = sizeof(float) * rows_per_block * (size_t)(d.T + E);
-    if (attn_lds > 160 * 1024) {
+    if (!mm_fast(E) && attn_lds > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "train forward: window T=%d too long for the attention kernel", d.T);
         return DPT_EUNSUPPORTED;
     }
@@ -454,18 +895,33 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
         float* xn = ws + W.x + xs(l + 1) * RE;
         hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x,
                            blob + P.ln1_g, blob + P.ln1_b, R, E, y1, st1);
-        hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 3)), dim3(kTrThreads), 0, st, y1, blob + P.attn_w,
-                           blob + P.attn_b, nullptr, R, E, 3 * E, 0, qkv);
-        hipLaunchKernelGGL(tr_attn_fwd, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), attn_lds, st,
-                           qkv, d, Pm, o);
-        hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, o, blob + P.proj_w, blob + P.proj_b,
-                           x, R, E, E, 0, x2);
+        const bool fast = mm_fast(E);
+        if (fast)
+            mm(E, kMmQkv, y1, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, R, qkv, st);
+        else
+            hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 3)), dim3(kTrThreads), 0, st, y1, blob + P.attn_w,
+                               blob + P.attn_b, nullptr, R, E, 3 * E, 0, qkv);
+        if (fast)
+            attn_fwd_fast(E, qkv, d, Pm, o, st);
+        else
+            hipLaunchKernelGGL(tr_attn_fwd, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), attn_lds,
+                               st, qkv, d, Pm, o);
+        if (fast)
+            mm(E, kMmProj, o, blob + P.proj_w, blob + P.proj_b, x, nullptr, R, x2, st);
+        else
+            hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, o, blob + P.proj_w,
+                               blob + P.proj_b, x, R, E, E, 0, x2);
         hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x2,
                            blob + P.ln2_g, blob + P.ln2_b, R, E, y2, st2);
-        hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, y2, blob + P.fc_w,
-                           blob + P.fc_b, nullptr, R, E, 4 * E, 0, hpre);
-        hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, hpre, blob + P.mp_w, blob + P.mp_b,
-                           x2, R, 4 * E, E, 1, xn);
+        if (fast) {
+            mm(E, kMmFc, y2, blob + P.fc_w, blob + P.fc_b, nullptr, nullptr, R, hpre, st);
+            mm(E, kMmMp, hpre, blob + P.mp_w, blob + P.mp_b, x2, nullptr, R, xn, st);
+        } else {
+            hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, y2, blob + P.fc_w,
+                               blob + P.fc_b, nullptr, R, E, 4 * E, 0, hpre);
+            hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, hpre, blob + P.mp_w,
+                               blob + P.mp_b, x2, R, 4 * E, E, 1, xn);
+        }
         if (int rc = launched("train forward layer")) return rc;
     }
     hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st,
@@ -481,7 +937,7 @@ int train_backward(const TrDims& d, const float* blob, const float* tok, float* 
     const TrBlob B = TrBlob::make(d);
     const TrWs W = TrWs::make(d);
     const int R = d.R(), E = d.E;
-    const int64_t RE = (int64_t)R * E, TT = (int64_t)d.B * d.T * d.T;
+    const int64_t RE = (int64_t)R * E, TT = (int64_t)d.B * d.T * TrWs::tpad(d.T);
     const int rows_per_block = kTrThreads / 64;
     const unsigned row_blocks = (R + rows_per_block - 1) / rows_per_block;
     float* part = ws + W.part;
@@ -516,26 +972,50 @@ int train_backward(const TrDims& d, const float* blob, const float* tok, float* 
         float* dqkv = ws + W.dqkv;
         float* dout = ws + W.dout;
         float* dS = ws + W.dS;
+        const bool fast = mm_fast(E);
         // MLP: x_{l+1} = x2 + gelu(hpre) W_mp + b_mp, hpre = y2 W_fc + b_fc
-        if (int rc = wgrad(hpre, dx, R, 4 * E, E, 1, part, dblob + G.mp_w, dblob + G.mp_b, st)) return rc;
-        hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, dx, blob + P.mp_w, R,
-                           4 * E, E, hpre, nullptr, dh);
-        if (int rc = wgrad(y2, dh, R, E, 4 * E, 0, part, dblob + G.fc_w, dblob + G.fc_b, st)) return rc;
-        hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dh, blob + P.fc_w, R, E,
-                           4 * E, nullptr, nullptr, dy);
+        if (fast) {
+            if (int rc = wgrad_fast(E, kMmMp, hpre, dx, R, 4 * E, E, part, dblob + G.mp_w, dblob + G.mp_b, st)) return rc;
+            mm(E, kMmBdMp, dx, blob + P.mp_w, nullptr, nullptr, hpre, R, dh, st);
+            if (int rc = wgrad_fast(E, kMmFc, y2, dh, R, E, 4 * E, part, dblob + G.fc_w, dblob + G.fc_b, st)) return rc;
+            mm(E, kMmBdFc, dh, blob + P.fc_w, nullptr, nullptr, nullptr, R, dy, st);
+        } else {
+            if (int rc = wgrad(hpre, dx, R, 4 * E, E, 1, part, dblob + G.mp_w, dblob + G.mp_b, st)) return rc;
+            hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, dx, blob + P.mp_w,
+                               R, 4 * E, E, hpre, nullptr, dh);
+            if (int rc = wgrad(y2, dh, R, E, 4 * E, 0, part, dblob + G.fc_w, dblob + G.fc_b, st)) return rc;
+            hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dh, blob + P.fc_w, R,
+                               E, 4 * E, nullptr, nullptr, dy);
+        }
         if (int rc = ln_param_grad(x2, st2, dy, R, E, part, dblob + G.ln2_g, dblob + G.ln2_b, st)) return rc;
         hipLaunchKernelGGL(tr_layernorm_bwd, dim3(row_blocks), dim3(kTrThreads), 0, st, x2, st2, blob + P.ln2_g, dy, R, E,
                            dx, dx2);
         // attention: x2 = x + o W_proj + b_proj
-        if (int rc = wgrad(o, dx2, R, E, E, 0, part, dblob + G.proj_w, dblob + G.proj_b, st)) return rc;
-        hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dx2, blob + P.proj_w, R, E,
-                           E, nullptr, nullptr, dout);
-        hipLaunchKernelGGL(tr_attn_bwd_ds, dim3(row_blocks), dim3(kTrThreads), ds_lds, st, qkv, Pm, o, dout, d, dS);
-        hipLaunchKernelGGL(tr_attn_bwd_dq, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, dS, d, dqkv);
-        hipLaunchKernelGGL(tr_attn_bwd_dkv, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, Pm, dS, dout, d, dqkv);
-        if (int rc = wgrad(y1, dqkv, R, E, 3 * E, 0, part, dblob + G.attn_w, dblob + G.attn_b, st)) return rc;
-        hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dqkv, blob + P.attn_w, R, E,
-                           3 * E, nullptr, nullptr, dy);
+        if (fast) {
+            if (int rc = wgrad_fast(E, kMmProj, o, dx2, R, E, E, part, dblob + G.proj_w, dblob + G.proj_b, st)) return rc;
+            mm(E, kMmBdProj, dx2, blob + P.proj_w, nullptr, nullptr, nullptr, R, dout, st);
+        } else {
+            if (int rc = wgrad(o, dx2, R, E, E, 0, part, dblob + G.proj_w, dblob + G.proj_b, st)) return rc;
+            hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dx2, blob + P.proj_w,
+                               R, E, E, nullptr, nullptr, dout);
+        }
+        if (fast) {
+            attn_bwd_fast(E, qkv, Pm, o, dout, d, dS, dqkv, st);
+        } else {
+            hipLaunchKernelGGL(tr_attn_bwd_ds, dim3(row_blocks), dim3(kTrThreads), ds_lds, st, qkv, Pm, o, dout, d, dS);
+            hipLaunchKernelGGL(tr_attn_bwd_dq, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, dS, d, dqkv);
+            hipLaunchKernelGGL(tr_attn_bwd_dkv, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, Pm, dS, dout, d,
+                               dqkv);
+        }
+        if (fast) {
+            if (int rc = wgrad_fast(E, kMmQkv, y1, dqkv, R, E, 3 * E, part, dblob + G.attn_w, dblob + G.attn_b, st))
+                return rc;
+            mm(E, kMmBdQkv, dqkv, blob + P.attn_w, nullptr, nullptr, nullptr, R, dy, st);
+        } else {
+            if (int rc = wgrad(y1, dqkv, R, E, 3 * E, 0, part, dblob + G.attn_w, dblob + G.attn_b, st)) return rc;
+            hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dqkv, blob + P.attn_w,
+                               R, E, 3 * E, nullptr, nullptr, dy);
+        }
         if (int rc = ln_param_grad(x, st1, dy, R, E, part, dblob + G.ln1_g, dblob + G.ln1_b, st)) return rc;
         hipLaunchKernelGGL(tr_layernorm_bwd, dim3(row_blocks), dim3(kTrThreads), 0, st, x, st1, blob + P.ln1_g, dy, R, E,
                            dx2, dx);
