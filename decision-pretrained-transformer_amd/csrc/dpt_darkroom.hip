@@ -736,13 +736,15 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     {
                         // the MLP's fp16 two-part products at scale 2^(mlp_ew + mlp_ex) (mlp3_n)
                         const float xs_scale = exp2i(M.mlp_ex), down = exp2i(-(M.mlp_ew + M.mlp_ex));
+                        // this wave's mlp.c_proj tiles, in flight across the c_fc products and gelu
+                        const Split2 mp0 = f3.ld2(Frag3::mp + hw), mp1 = f3.ld2(Frag3::mp + 4 + hw);
                         const Split2 xs = split2(xn, xs_scale);
                         const floatx4 h0 = mfma_x3(fj0, xs, ld4(W + PL::fc_b + 2 * hw * 16 + 4 * g));
                         const floatx4 h1 = mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * hw + 1) * 16 + 4 * g));
                         const Split2 gs = gelu_split(h0, h1, GeluSplit(M.mlp_ew, M.mlp_ex));
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-                        const floatx4 y0 = mfma_x3(f3.ld2(Frag3::mp + hw), gs, zero) * down;
-                        const floatx4 y1 = mfma_x3(f3.ld2(Frag3::mp + 4 + hw), gs, zero) * down;
+                        const floatx4 y0 = mfma_x3(mp0, gs, zero) * down;
+                        const floatx4 y1 = mfma_x3(mp1, gs, zero) * down;
                         if ((lane_id() & 15) == 0) {
                             *reinterpret_cast<floatx4*>(&S.part_y[hw][4 * g]) = y0;
                             *reinterpret_cast<floatx4*>(&S.part_y[hw][16 + 4 * g]) = y1;

@@ -311,13 +311,14 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
     const GeluSplit gk(ew, ex);
     const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);  // scaled (PL)
     floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
+    // c_fc tiles one pair ahead (in flight across the pair's gelu + c_proj products; the first
+    // pair's across the split of xn), the pair's c_proj tiles at its start (in flight across its
+    // c_fc + gelu)
+    const int vo = FragSrc3::lane_off();
+    Split2 wf0 = f3.ld2(Frag3::fc, vo), wf1 = f3.ld2(Frag3::fc + 1, vo);
     Split2 xs[2];
 #pragma unroll
     for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], xs_scale);
-    // c_fc tiles one pair ahead (in flight across the pair's gelu + c_proj products), the
-    // pair's c_proj tiles at its start (in flight across its c_fc + gelu)
-    const int vo = FragSrc3::lane_off();
-    Split2 wf0 = f3.ld2(Frag3::fc, vo), wf1 = f3.ld2(Frag3::fc + 1, vo);
 #pragma unroll
     for (int p = 0; p < kFF / 32; ++p) {
         const Split2 w0 = f3.ld2(Frag3::mp + p, vo), w1 = f3.ld2(Frag3::mp + 4 + p, vo);
@@ -345,13 +346,13 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
 // products (mfma_x3) at scale 2^(attn_ew + attn_ey), scaled back exactly; xs = the blocks'
 // LayerNorm outputs split at 2^attn_ey
 template <int NB>
-__device__ inline void u_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&xs)[2], float (&q)[2][8],
+__device__ inline void u_proj3_w(const float* W, const Split2 (&wg)[2], const Split2 (&xs)[2], float (&q)[2][8],
                                  const ModelView& M) {
-    const int g = lane_id() >> 4, vo = FragSrc3::lane_off();
+    const int g = lane_id() >> 4;
     const float down = exp2i(-(M.attn_ew + M.attn_ey));
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
-        const Split2 w = f3.ld2(Frag3::attn + ob, vo);
+        const Split2& w = wg[ob];
         const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);  // scaled (PL)
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -360,6 +361,19 @@ __device__ inline void u_proj3_s(const float* W, const FragSrc3& f3, const Split
             for (int r = 0; r < 4; ++r) q[j][ob * 4 + r] = acc[r];
         }
     }
+}
+// the G tiles of u = xn G + g0 (both 16-column tiles), issued ahead of the work that precedes the product
+__device__ inline void ld_g(const FragSrc3& f3, Split2 (&wg)[2]) {
+    const int vo = FragSrc3::lane_off();
+    wg[0] = f3.ld2(Frag3::attn, vo);
+    wg[1] = f3.ld2(Frag3::attn + 1, vo);
+}
+template <int NB>
+__device__ inline void u_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&xs)[2], float (&q)[2][8],
+                                 const ModelView& M) {
+    Split2 wg[2];
+    ld_g(f3, wg);
+    u_proj3_w<NB>(W, wg, xs, q, M);
 }
 template <int NB>
 __device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8],
@@ -373,32 +387,42 @@ __device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float
 // attn_proj on mfma_x3: x^T += Wvp^T o^T + bvp (o, a convex combination of the values y,
 // shares their bound and scale)
 template <int NB>
-__device__ inline void attn_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&os)[2], float (&x)[2][8],
-                                    const ModelView& M) {
-    const int g = lane_id() >> 4, vo = FragSrc3::lane_off();
+__device__ inline void attn_proj3_w(const float* W, const Split2& w0, const Split2& w1, const Split2 (&os)[2],
+                                    float (&x)[2][8], const ModelView& M) {
+    const int g = lane_id() >> 4;
     const float down = exp2i(-(M.attn_ew + M.attn_ey));
-    const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
     const floatx4 b0 = ld4(W + PL::proj_b + 4 * g), b1 = ld4(W + PL::proj_b + 16 + 4 * g);  // scaled (PL)
 #pragma unroll
     for (int j = 0; j < NB; ++j) resid_add(x[j], mfma_x3(w0, os[j], b0), mfma_x3(w1, os[j], b1), down);
 }
 template <int NB>
+__device__ inline void attn_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&os)[2], float (&x)[2][8],
+                                    const ModelView& M) {
+    const int vo = FragSrc3::lane_off();
+    attn_proj3_w<NB>(W, f3.ld2(Frag3::proj, vo), f3.ld2(Frag3::proj + 1, vo), os, x, M);
+}
+template <int NB>
 __device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8],
                                   const ModelView& M) {
+    // the Wvp tiles ahead of the split
+    const int vo = FragSrc3::lane_off();
+    const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
     Split2 os[2];
 #pragma unroll
     for (int j = 0; j < NB; ++j) os[j] = split2(o[j], exp2i(M.attn_ey));
-    attn_proj3_s<NB>(W, f3, os, x, M);
+    attn_proj3_w<NB>(W, w0, w1, os, x, M);
 }
 // the same from attend's unnormalised (o, l): o / l is the attention output x 2^attn_ey already,
 // so the split takes 1 / l as its scale (one multiply per value)
 template <int NB>
 __device__ inline void attn_proj3_ol(const float* W, const FragSrc3& f3, const float (&o)[2][8], const float (&l)[2],
                                      float (&x)[2][8], const ModelView& M) {
+    const int vo = FragSrc3::lane_off();
+    const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
     Split2 os[2];
 #pragma unroll
     for (int j = 0; j < NB; ++j) os[j] = split2(o[j], 1.0f / l[j]);
-    attn_proj3_s<NB>(W, f3, os, x, M);
+    attn_proj3_w<NB>(W, w0, w1, os, x, M);
 }
 
 // Folded attention input of the NB blocks qb[]: keys and values are the
@@ -453,11 +477,14 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
 template <int NB, class KV>
 __device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8],
                                     KV& S, const int (&qb)[2], const ModelView& M) {
+    // the G tiles first: their L2 latency runs under the split and the K/V stores
+    Split2 wg[2];
+    ld_g(f3, wg);
     Split2 xs[2];
 #pragma unroll
     for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
-    u_proj3_s<NB>(W, f3, xs, q, M);
     kv_store<NB>(S, qb, xn, xs);
+    u_proj3_w<NB>(W, wg, xs, q, M);
 }
 
 // Causal flash attention of query block qb over keys [key_lo, 16*qb + c] (key_lo <= 16):
