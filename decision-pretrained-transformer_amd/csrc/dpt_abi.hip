@@ -58,7 +58,7 @@ int launch_derive_l0(const ModelView&, float*, hipStream_t);
 int64_t l0_numel(int n_layer);
 int launch_rollout_darkroom(const ModelView&, const float*, const dpt_darkroom_rollout_args&, hipStream_t);
 int darkroom_max_window();
-int64_t darkroom_workspace_numel(int N);
+int64_t darkroom_workspace_numel(int N, int64_t window);
 int prefill_max_window(const ModelView&);
 int launch_prefill(const ModelView&, const float*, const float*, const float*, const float*, const float*,
                    const float*, int, int, int, float*, hipStream_t);
@@ -472,7 +472,13 @@ int dpt_rollout_bandit(const dpt_model* m, const dpt_bandit_rollout_args* a, voi
 
 int dpt_darkroom_workspace_numel(int32_t N, int64_t* numel) {
     REQUIRE(numel && N >= 1, "N=%d", N);
-    *numel = darkroom_workspace_numel(N);
+    *numel = darkroom_workspace_numel(N, darkroom_max_window());
+    return DPT_OK;
+}
+
+int dpt_darkroom_workspace_numel_window(int32_t N, int32_t window, int64_t* numel) {
+    REQUIRE(numel && N >= 1 && window >= 1, "N=%d window=%d", N, window);
+    *numel = darkroom_workspace_numel(N, window);
     return DPT_OK;
 }
 

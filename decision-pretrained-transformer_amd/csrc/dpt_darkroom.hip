@@ -6,7 +6,7 @@
 // forward over the window [query, context transitions...] (models/net.py:41-60);
 // the prediction is the LAST position.  That is matrix-core work: one workgroup
 // owns one task for all Heps x horizon steps, and each wave owns two 16-token
-// blocks of the window (4 waves for T <= 128, 8 waves for T <= 256: DrGeom).
+// blocks of the window (4 waves for T <= 128, 8 for T <= 256, 16 for T <= 512: DrGeom).
 //
 // Dataflow is transposed (features x tokens): a wave keeps x^T of its 16
 // tokens in registers as MFMA 16x16x4 C-layout fragments -- lane (g = l>>4,
@@ -85,7 +85,8 @@ struct PTop {
 };
 
 // Window geometry of the kernel built with NW waves: 2 NW blocks of 16 tokens (NW = 4: windows
-// of up to 128 tokens, two workgroups per CU; NW = 8: up to 256, one per CU).
+// of up to 128 tokens, two workgroups per CU; NW = 8: up to 256, one per CU; NW = 16: up to 512,
+// one per CU at 128 VGPRs per wave, workspace only).
 template <int NW>
 struct DrGeom {
     static constexpr int kWaves = NW, kBlk = 2 * NW, kT = 16 * kBlk;
@@ -99,7 +100,9 @@ struct DrGeom {
 template <bool kWs, int NW>
 struct alignas(16) DrSmem {
     static constexpr int kFwdT = DrGeom<NW>::kT, kFwdBlocks = DrGeom<NW>::kBlk;
-    KVBuf<kFwdT, kSplitKeys, kSplitKeys && kWs> kv;
+    // keys and values of the current layer (the 16-wave geometry reads the keys from the values'
+    // rows: 512 tokens of both in LDS)
+    KVBuf<kFwdT, kSplitKeys, kSplitKeys && kWs, kWs && NW == 16> kv;
     int2 ctx[kFwdT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
     int2 cur[kFwdT];   // this episode's transitions
     // layer-0 episode cache: the causal softmax partial of every token over keys
@@ -148,11 +151,11 @@ struct DarkroomParams {
 // re-projecting; only the query token (position 0) is recomputed.  Layout per task:
 // [x | u | o][block][lane][8] fp32, each lane's 8 C-layout values contiguous (2 x 16 B);
 // o is the layer-0 episode partial (the prologue's attention over keys 1..t).
-// The workspace starts with the per-state table (kDrTab floats), then the task caches (sized
-// for the largest geometry, dpt_darkroom_workspace_numel; a launch uses its own stride).
+// The workspace starts with the per-state table (kDrTab floats), then the task caches, at the
+// stride of the launch's geometry (dpt_darkroom_workspace_numel_window).
 constexpr int kDrTabPerState = 2 * 4 * 8;
 constexpr int kDrTab = kMemoStates * kDrTabPerState;
-constexpr int kDrMaxWaves = 8;
+constexpr int kDrMaxWaves = 16;
 template <int NW>
 __device__ inline float* l0_cache(const DarkroomParams& p, int task, int which, int blk) {
     return p.ws + kDrTab + (size_t)task * DrGeom<NW>::kWsPerTask +
@@ -467,8 +470,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
                                        u_proj3_n<NB>(P, split0, xn, q, M)));
                     }
-                    if (own0) {  // block 0: key/value (= y) of the query token
-                        kv_from_y<1>(S.kv, qb, xn, M);
+                    if (own0) {  // block 0: key/value (= y) of the query token (the merge below reads them)
                         const int lane = lane_id();
                         if ((lane & 15) == 0) {  // token 0's y (folded attention: key = value = y)
 #pragma unroll
@@ -531,16 +533,17 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 
             for (int layer = 1; layer < L; ++layer) {
                 const bool last = layer == L - 1;
+                auto& kv = S.kv;
                 const float* W = P + layer * PL::size;
                 float q[2][8];
                 {
                     float xn[2][8];
                     if (!last) {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       u_proj_kv3_n<NB>(W, split0.layer(layer), xn, q, S.kv, qb, M)));
+                                       u_proj_kv3_n<NB>(W, split0.layer(layer), xn, q, kv, qb, M)));
                     } else {
                         // the last layer needs q only for token T-1 (block qlast)
-                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(S.kv, qb, xn, M)));
+                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(kv, qb, xn, M)));
 #pragma unroll
                         for (int j = 0; j < 2; ++j) {
                             if (j < nb && qb[j] == qlast) {
@@ -570,7 +573,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     for (int j = 0; j < 2; ++j) {
                         if (j >= nb) break;
                         float m;
-                        attend(S.kv, q[j], qb[j], 0, scale, m, l[j], o[j], M);
+                        attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M);
                     }
                     DPT_BLOCKS(nb, attn_proj3_ol<NB>(W, split0.layer(layer), o, l, x, M));
                 }
@@ -588,6 +591,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             {
                 const float* W = P + (L - 1) * PL::size;
                 const FragSrc3 f3 = split0.layer(L - 1);
+                const auto& kv = S.kv;
                 // this wave's tail weight tiles (c_proj, c_fc of hidden chunks 2 wave and
                 // 2 wave + 1), in flight across the first barrier; the MLP runs on waves
                 // 0..kMlpWaves-1 (with 8 waves the upper four only take key tiles in (1))
@@ -619,8 +623,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                                 for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
                                 continue;
                             }
-                            const Split2 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane]};
-                            const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
+                            const floatx4 sc = mfma_x3(key_split(kv, kt, lane), qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
                             for (int r = 0; r < 4; ++r) sv[4 * h + r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] : -INFINITY;
                         }
@@ -638,8 +641,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         const int pp = wave;
                         const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
                         const int vlo = vt_lane_off(lane);
-                        const floatx4 o0 = mfma_x3(vt_split(S.kv, pp, 0, vlo), ps, zero);
-                        const floatx4 o1 = mfma_x3(vt_split(S.kv, pp, 1, vlo), ps, zero);
+                        const floatx4 o0 = mfma_x3(vt_split(kv, pp, 0, vlo), ps, zero);
+                        const floatx4 o1 = mfma_x3(vt_split(kv, pp, 1, vlo), ps, zero);
                         if (c == 0) {
                             *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
                             *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;
@@ -658,7 +661,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         if (kt > qlast) break;
                         // split key tile x the split query, broadcast to every column
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
-                        const Split2 ks{S.kv.KS[kt][0][lane], S.kv.KS[kt][1][lane]};
+                        const Split2 ks = key_split(kv, kt, lane);
                         const floatx4 sc = mfma_x3(ks, split2(qv, exp2i(M.attn_eq)), floatx4{0.f, 0.f, 0.f, 0.f});
                         float sv[4], mt = -INFINITY;
 #pragma unroll
@@ -672,8 +675,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         for (int r = 0; r < 4; ++r) pr[r] = __builtin_amdgcn_exp2f(sv[r] - mt);
                         float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
                         lt = sum_cols(lt) * exp2i(kPExp);
-                        const floatx4 v0 = ld4(&S.kv.Vt[c][kt * 16 + 4 * g]);
-                        const floatx4 v1 = ld4(&S.kv.Vt[16 + c][kt * 16 + 4 * g]);
+                        const floatx4 v0 = ld4(&kv.Vt[c][kt * 16 + 4 * g]);
+                        const floatx4 v1 = ld4(&kv.Vt[16 + c][kt * 16 + 4 * g]);
                         floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                         for (int s4 = 0; s4 < 4; ++s4) o0 = mfma4(v0[s4], pr[s4], o0);
@@ -810,6 +813,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     DPT_TAIL_PRIO(0);
                 }
             }
+            // the end of the step (with the memo, the barrier after the memo-hit chain at the top of
+            // the loop would order the state and the partials as well, but dropping this one was
+            // 1 % slower at config 3)
             bar_lds();
             DR_STAMP(2 * L + 1);
         }
@@ -931,17 +937,31 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
         if (int rc = check_hip(hipGetLastError(), "state_tables_kernel launch")) return rc;
     }
     // the smallest geometry that holds the window: 4 waves (two workgroups per CU) up to 128
-    // tokens, else 8 waves (one per CU) up to 256
+    // tokens, 8 waves (one per CU) up to 256, 16 waves (one per CU, four per SIMD at 128 VGPRs,
+    // keys and values of 512 tokens in LDS) up to 512
     const int64_t window = 1 + (int64_t)a.ctx_episodes * a.horizon;
     const bool ws = a.workspace != nullptr;
     if (window <= DrGeom<4>::kT)
         return ws ? launch_darkroom_geom<true, 4>(M, p, st) : launch_darkroom_geom<false, 4>(M, p, st);
-    return ws ? launch_darkroom_geom<true, kDrMaxWaves>(M, p, st) : launch_darkroom_geom<false, kDrMaxWaves>(M, p, st);
+    if (window <= DrGeom<8>::kT)
+        return ws ? launch_darkroom_geom<true, 8>(M, p, st) : launch_darkroom_geom<false, 8>(M, p, st);
+    if (!ws) {
+        set_error(DPT_EUNSUPPORTED, "fused darkroom rollout: windows over %d tokens need the workspace",
+                  DrGeom<8>::kT);
+        return DPT_EUNSUPPORTED;
+    }
+    return launch_darkroom_geom<true, 16>(M, p, st);
 }
 
 int darkroom_max_window() { return DrGeom<kDrMaxWaves>::kT; }
 
-int64_t darkroom_workspace_numel(int N) { return kDrTab + (int64_t)N * DrGeom<kDrMaxWaves>::kWsPerTask; }
+// per task: the stride of the geometry that runs the window (launch_rollout_darkroom's choice)
+int64_t darkroom_workspace_numel(int N, int64_t window) {
+    const int64_t per = window <= DrGeom<4>::kT ? DrGeom<4>::kWsPerTask
+                        : window <= DrGeom<8>::kT ? DrGeom<8>::kWsPerTask
+                                                  : DrGeom<kDrMaxWaves>::kWsPerTask;
+    return kDrTab + (int64_t)N * per;
+}
 
 }  // namespace dpt
 

@@ -36,14 +36,18 @@ typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 // stores each as one 8-B write; the A operand of O^T += V^T P^T over a pair of key tiles
 // (element j of lane (g, c) = V[key 16 (2 pair + (j >> 2)) + 4g + (j & 3)][feature 16 half + c],
 // the lane group's k order of P^T's C-layout over the two tiles) is read back transposed by
-// two ds_read_b64_tr_b16 per part (vt_split).
+// two ds_read_b64_tr_b16 per part (vt_split).  With KEYS_VT (requires SPLITV) the score product's
+// key tiles are read from the same rows too (key_split) and KS is not kept: half the LDS, for the
+// 512-token windows; otherwise the keys keep their own pre-split tiles (one 16-B read per part).
 constexpr int kVTRow = kE + 4;  // halves per VT row: 72 B (8-B aligned rows for the transposed read)
-template <int TMAX, bool SPLITK = false, bool SPLITV = false>
+template <int TMAX, bool SPLITK = false, bool SPLITV = false, bool KEYS_VT = false>
 struct KVBuf {
     static_assert(SPLITK || !SPLITV, "split values need split keys");
-    static constexpr bool kSplitK = SPLITK, kSplitV = SPLITV;
+    static_assert(SPLITV || !KEYS_VT, "keys from VT need split values");
+    static constexpr bool kSplitK = SPLITK, kSplitV = SPLITV, kKeysVT = KEYS_VT;
+    static constexpr bool kKS = SPLITK && !KEYS_VT;
     float K[SPLITK ? 1 : TMAX][kKStride];
-    halfx8 KS[SPLITK ? TMAX / 16 : 1][SPLITK ? 2 : 1][SPLITK ? 64 : 1];  // (16 B when unused)
+    halfx8 KS[kKS ? TMAX / 16 : 1][kKS ? 2 : 1][kKS ? 64 : 1];  // (16 B when unused)
     _Float16 VT[SPLITV ? 2 : 1][SPLITV ? TMAX : 1][SPLITV ? kVTRow : 8];
     float Vt[SPLITV ? 1 : kE][TMAX + 4];
 };
@@ -132,6 +136,25 @@ __device__ inline Split2 vt_split(const KV& S, int pp, int half, int lo) {
     const i16x8 m = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
     return Split2{__builtin_bit_cast(halfx8, h), __builtin_bit_cast(halfx8, m)};
 }
+// The split A operand of the score product S^T = K Q^T for key tile kt: lane (g, c) holds the
+// k-elements j of key 16 kt + c, features 16 (j >> 2) + 4g + (j & 3) (the writer's C-layout order).
+// With KEYS_VT the keys are read from the token-major VT image (two 8-B runs of a row per part,
+// one ds_read2_b64; rows 72 B apart put the 16 lanes of a group on distinct banks), otherwise
+// from the pre-split key tiles KS.
+template <class KV>
+__device__ inline Split2 key_split(const KV& S, int kt, int lane) {
+    if constexpr (KV::kKeysVT) {
+        const int row = 16 * kt + (lane & 15), g = lane >> 4;
+        const uint2* h = reinterpret_cast<const uint2*>(&S.VT[0][row][4 * g]);
+        const uint2* m = reinterpret_cast<const uint2*>(&S.VT[1][row][4 * g]);
+        const uint2 h0 = h[0], h1 = h[4], m0 = m[0], m1 = m[4];
+        return Split2{__builtin_bit_cast(halfx8, uint4{h0.x, h0.y, h1.x, h1.y}),
+                      __builtin_bit_cast(halfx8, uint4{m0.x, m0.y, m1.x, m1.y})};
+    } else {
+        return Split2{S.KS[kt][0][lane], S.KS[kt][1][lane]};
+    }
+}
+
 // scale of the attention probabilities in P V (P <= 2^8, so P x 2^kPExp < 2^14)
 constexpr int kPExp = 2;
 
@@ -437,8 +460,10 @@ __device__ inline void kv_store(KV& S, const int (&qb)[2], const float (&xn)[2][
     for (int j = 0; j < NB; ++j) {
         const int tok = qb[j] * 16 + (lane & 15);
         if constexpr (KV::kSplitK) {
-            S.KS[qb[j]][0][lane] = xs[j].h;
-            S.KS[qb[j]][1][lane] = xs[j].m;
+            if constexpr (KV::kKS) {
+                S.KS[qb[j]][0][lane] = xs[j].h;
+                S.KS[qb[j]][1][lane] = xs[j].m;
+            }
             if constexpr (KV::kSplitV) {
                 // the same split parts, token-major: value k of lane (g, c) is feature
                 // 16 (k >> 2) + 4g + (k & 3) of token 16 b + c, so each half of the lane's 8
@@ -541,8 +566,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
                     for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
                     continue;
                 }
-                const Split2 ks{S.KS[kt][0][lane], S.KS[kt][1][lane]};
-                const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
+                const floatx4 sc = mfma_x3(key_split(S, kt, lane), qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
                 for (int r = 0; r < 4; ++r) sv[4 * h + r] = sc[r];
                 if constexpr (decltype(masked)::value) {

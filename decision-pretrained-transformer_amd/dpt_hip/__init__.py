@@ -187,7 +187,8 @@ class DeviceModel:
         int32, logits (Heps*horizon, N, 5) f32 and forwards (N, Heps) int32 (window
         forwards run per task and episode: one per distinct state per episode under
         set_darkroom_memo) if requested.  Raises
-        NotImplementedError outside sd=2 / A=5 / window <= 256 (use the per-step path).
+        NotImplementedError outside sd=2 / A=5 / window <= darkroom_max_window() (use the
+        per-step path).
         """
         dev = device()
         goals_d = _dev(goals, torch.int32, dev).contiguous()
@@ -205,7 +206,7 @@ class DeviceModel:
                     out[k].zero_()
             return out
         n_ws = ctypes.c_int64()
-        _lib.call("dpt_darkroom_workspace_numel", N, ctypes.byref(n_ws))
+        _lib.call("dpt_darkroom_workspace_numel_window", N, 1 + int(ctx_episodes) * int(horizon), ctypes.byref(n_ws))
         ws = torch.empty(n_ws.value, dtype=torch.float32, device=dev) if _darkroom_ws else None
         args = _lib.DarkroomRolloutArgs(
             N, int(Heps), int(horizon), int(ctx_episodes), int(dim), int(bool(sample)), int(first_task),
@@ -407,6 +408,12 @@ def set_select_fast(on):
 
 _darkroom_memo = True
 _darkroom_ws = True
+
+
+def darkroom_max_window():
+    """Largest window (1 + R*horizon tokens) of the fused DarkRoom rollout: 512 with the per-task
+    workspace (16 waves per task above 256 tokens), 256 without it."""
+    return 512 if _darkroom_ws else 256
 
 
 def set_darkroom_workspace(on):

@@ -173,6 +173,7 @@ SIGNATURES["dpt_regret_workspace_numel"] = (_i32, [_i32, _i32, ctypes.POINTER(_i
 SIGNATURES["dpt_regret_moments"] = (_i32, [_c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,
                                            _c_void_p, _c_void_p])
 SIGNATURES["dpt_darkroom_workspace_numel"] = (_i32, [_i32, ctypes.POINTER(_i64)])
+SIGNATURES["dpt_darkroom_workspace_numel_window"] = (_i32, [_i32, _i32, ctypes.POINTER(_i64)])
 
 
 class TrainDesc(ctypes.Structure):

@@ -3,7 +3,7 @@
 ``deploy_online_vec`` (evals/eval_darkroom.py:20-84): with the DPT controller
 over this package's ``Transformer`` and a ``DarkroomEnvVec`` the whole loop is
 one fused kernel launch (dpt_rollout_darkroom) when the window fits (1 + H <=
-256); otherwise it stays on the device step by step — per step one window forward (gfx950 kernel) over the fixed
+dpt_hip.darkroom_max_window(): 512 tokens); otherwise it stays on the device step by step — per step one window forward (gfx950 kernel) over the fixed
 in-context episodes with the current state as query, device sampling, the
 integer grid step kernel, and an on-device append into the episode buffers;
 returns are summed on device and copied once at the end.  Other controllers
@@ -67,12 +67,10 @@ def _episode_device(dm, ctrl, vec_env, ctx, horizon):
     return es, ea, ns, er
 
 
-_FUSED_MAX_WINDOW = 256  # dpt_rollout_darkroom: 1 + H tokens per forward
-
-
 def _fused_ok(vec_env, controller, H):
+    # dpt_rollout_darkroom: 1 + H tokens per forward
     return (_device_ok(vec_env, controller) and vec_env.state_dim == 2 and vec_env.action_dim == 5
-            and 1 + H <= _FUSED_MAX_WINDOW and vec_env.dim <= 255)
+            and 1 + H <= dpt_hip.darkroom_max_window() and vec_env.dim <= 255)
 
 
 def rollout_fused(vec_env, controller, Heps, H, horizon, want_actions=False, want_logits=False,

@@ -326,9 +326,10 @@ int dpt_rollout_policy(const dpt_policy_rollout_args* args_host, void* stream);
  * prediction at the last position.  Action a_t = select(logits, u_t) with
  * u_t = uniforms[(e*horizon+t)*N + i] or Philox(seed, counter + e*horizon + t,
  * first_task + i, DPT_STREAM_SELECT) -- the same draws as dpt_select_action.
- * Requires sd = 2, A = 5, 1 + R*horizon <= 256 and dim <= 255 (else
+ * Requires sd = 2, A = 5, 1 + R*horizon <= 512 and dim <= 255 (else
  * DPT_EUNSUPPORTED: use dpt_forward_window per step).  Windows of up to 128
- * tokens run 4 waves per task (two tasks per CU), longer ones 8 waves.       */
+ * tokens run 4 waves per task (two tasks per CU), up to 256 8 waves, up to
+ * 512 16 waves (one task per CU; these need the workspace).                 */
 typedef struct dpt_darkroom_rollout_args {
     int32_t N, Heps, horizon, ctx_episodes;
     int32_t dim, sample;
@@ -343,13 +344,16 @@ typedef struct dpt_darkroom_rollout_args {
     int32_t* actions_out;       /* (N, Heps*horizon) or NULL */
     float* logits_out;          /* (Heps*horizon, N, 5) or NULL */
     int32_t* forwards_out;      /* (N, Heps) window forwards run per task and episode, or NULL */
-    float* workspace;           /* dpt_darkroom_workspace_numel(N) floats, or NULL: the context
+    float* workspace;           /* dpt_darkroom_workspace_numel_window(N, 1 + R*horizon) floats
+                                 * (dpt_darkroom_workspace_numel(N): enough for any window), or
+                                 * NULL (windows up to 256 only): the context
                                  * tokens' layer-0 inputs, queries and attention partials, fixed
                                  * within an episode, are kept there instead of recomputed every
                                  * step (or kept in LDS: the partials) */
 } dpt_darkroom_rollout_args;
 
 int dpt_darkroom_workspace_numel(int32_t N, int64_t* numel_out_host);
+int dpt_darkroom_workspace_numel_window(int32_t N, int32_t window, int64_t* numel_out_host);
 
 int dpt_rollout_darkroom(const dpt_model* model, const dpt_darkroom_rollout_args* args_host,
                          void* stream);

@@ -314,8 +314,8 @@ def test_eval_darkroom_device_loop_matches_reference(fused):
 
 
 def test_eval_darkroom_per_step_memo_bit_identical():
-    """The per-step device loop (window 1 + 2*130 = 261 > 256 tokens, so not fused) forwards only
-    the tasks whose state is new in the episode; returns are identical with the memo off."""
+    """The per-step device loop (fused=False, window 1 + 2*130 = 261) forwards only the tasks
+    whose state is new in the episode; returns are identical with the memo off."""
     import dpt_hip
     from ctrls.ctrl_darkroom import DarkroomTransformerController
     from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec
@@ -330,15 +330,14 @@ def test_eval_darkroom_per_step_memo_bit_identical():
             np.random.seed(5)
             ctrl = DarkroomTransformerController(m, batch_size=48, sample=True)
             vec = DarkroomEnvVec(envs)
-            assert not eval_darkroom._fused_ok(vec, ctrl, 260)
-            outs.append(eval_darkroom.deploy_online_vec(vec, ctrl, 3, 260, 130))
+            outs.append(eval_darkroom.deploy_online_vec(vec, ctrl, 3, 260, 130, fused=False))
     finally:
         dpt_hip.set_darkroom_memo(True)
     assert np.array_equal(outs[0], outs[1])
 
 
 def test_eval_darkroom_per_step_shard_invariant():
-    """The per-step device loop (window 1 + 2*130 = 261 > 256 tokens, so not fused) keys its
+    """The per-step device loop (fused=False, window 1 + 2*130 = 261) keys its
     selection draws by the GLOBAL task id (DarkroomEnvVec.first_task), like the fused kernel:
     two shards of the tasks, each with the same controller seed, give the unsharded returns."""
     from ctrls.ctrl_darkroom import DarkroomTransformerController
@@ -353,8 +352,7 @@ def test_eval_darkroom_per_step_shard_invariant():
         ctrl = DarkroomTransformerController(m, batch_size=hi - lo, sample=True)
         ctrl._stream.seed = 31337
         vec = DarkroomEnvVec(envs, first_task=lo)
-        assert not eval_darkroom._fused_ok(vec, ctrl, 260)
-        return eval_darkroom.deploy_online_vec(vec, ctrl, 3, 260, 130)
+        return eval_darkroom.deploy_online_vec(vec, ctrl, 3, 260, 130, fused=False)
 
     full = run(0, 40)
     assert np.array_equal(np.concatenate([run(0, 17), run(17, 40)]), full)

@@ -377,8 +377,6 @@ def test_rollout_darkroom_large_properties():
     lo = m.rollout_darkroom(goals[:1000], 2, 100, 1, seed=11, want_actions=True)
     hi = m.rollout_darkroom(goals[1000:], 2, 100, 1, seed=11, first_task=1000, want_actions=True)
     assert np.array_equal(np.concatenate([lo["actions"].cpu().numpy(), hi["actions"].cpu().numpy()]), a1)
-    with pytest.raises(NotImplementedError):
-        m.rollout_darkroom(goals[:4], 1, 128, 2)  # window 257
     # greedy episode 1 logits == the per-step window kernel on the recorded context
     og = m.rollout_darkroom(goals[:64], 2, 100, 1, sample=False, want_actions=True, want_logits=True)
     acts = og["actions"].cpu().numpy()
@@ -770,6 +768,49 @@ def test_rollout_darkroom_dim12_workspace_without_state_table():
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(w, 4).numpy(), 4, 404, goals[tasks], Heps, horizon, R, u,
                                     True, dim=dim, threads=16, want_logits=True)
     check_darkroom_tasks(outs[1], tasks, ref, Heps, horizon)
+
+
+@pytest.mark.parametrize("Heps,horizon,R", [(4, 100, 3), (2, 511, 1)])
+def test_rollout_darkroom_windows_over_256(Heps, horizon, R):
+    """Windows of 257..512 tokens run the 16-wave kernel (one task per CU, keys and values of the
+    whole window in LDS): window 301 (the reference's H = 300 with horizon 100, episodes of 1, 101,
+    201 and 301 tokens) and 512 (the largest).  The logits memo is bit-identical to one forward per
+    step, and sampled tasks agree with the float64 C oracle fed the same Philox draws (logits within
+    1e-5, actions and returns exactly up to each task's first near-tie draw).  Without the
+    workspace these windows are rejected (NotImplementedError: use the per-step path)."""
+    import bench
+    import dpt_hip
+    from oracle import c_oracle
+    d = dh()
+    L, npos = 4, 512
+    sd, _ = bench.synthetic_state_dict(L, 2, 5, npos // 4 - 1)
+    m = dpt_hip.DeviceModel(sd, L, 2, 5, npos)
+    N, seed = 48, 5
+    goals = darkroom_config(N)
+    steps = Heps * horizon
+    outs = {}
+    try:
+        for memo in (True, False):
+            dpt_hip.set_darkroom_memo(memo)
+            o = m.rollout_darkroom(goals, Heps, horizon, R, seed=seed, want_actions=True, want_logits=True,
+                                   want_forwards=True)
+            outs[memo] = {k: o[k].cpu().numpy() for k in ("actions", "logits", "returns", "forwards")}
+        dpt_hip.set_darkroom_workspace(False)
+        with pytest.raises(NotImplementedError):
+            m.rollout_darkroom(goals[:2], 1, horizon, R)
+    finally:
+        dpt_hip.set_darkroom_workspace(True)
+        dpt_hip.set_darkroom_memo(True)
+    on, off = outs[True], outs[False]
+    for k in ("actions", "logits", "returns"):
+        assert np.array_equal(on[k], off[k]), k
+    assert (off["forwards"] == horizon).all() and on["forwards"].sum() < off["forwards"].sum()
+    tasks = np.arange(0, N, 3)
+    u = np.stack([philox_np.uniform(seed, k, tasks, d.STREAM_SELECT) for k in range(steps)])
+    ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, npos, goals[tasks], Heps, horizon, R, u,
+                                    True, threads=16, want_logits=True)
+    res = {k: torch.from_numpy(on[k]) for k in ("logits", "actions", "returns")}
+    assert check_darkroom_tasks(res, tasks, ref, Heps, horizon) >= len(tasks) // 2
 
 
 @pytest.mark.parametrize("Heps,horizon,R", [(4, 100, 2), (3, 85, 3)])
