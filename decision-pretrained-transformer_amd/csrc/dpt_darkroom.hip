@@ -115,10 +115,13 @@ struct alignas(16) DrSmem {
     float part_m[kFwdBlocks], part_l[kFwdBlocks];
     float part_y[kFF / 32][kE];       // last layer: MLP partials per pair of hidden chunks
     // per-episode logits memo, one row per grid state (dim * dim <= kMemoStates)
-    float memo_lg[kMemoStates][kDrA];
-    float memo_q[kMemoStates][kDrA];   // and their fp32 selection cdf (cdf_fast): a hit selects by 5 compares
-    // (no separate valid flag: an empty row holds memo_q[s][0] = -1 and memo_lg[s][0] = NaN, so a
-    // hit is decided by the row's own values, read in one LDS round trip)
+    // row s: the fp32 selection cdf q (cdf_fast: a hit selects by 5 compares) in [0, 5), the logits
+    // in [kMemoLg, kMemoLg + 5); 48-B rows, read by three 16-B loads in one round trip.  (No separate
+    // valid flag: an empty row holds q[0] = -1 and lg[0] = NaN, so a hit is decided by the row's
+    // own values.)
+    static constexpr int kMemoRow = 12, kMemoLg = 6;
+    static_assert(kMemoLg >= kDrA && kMemoLg + kDrA <= kMemoRow, "memo row layout");
+    alignas(16) float memo[kMemoStates][kMemoRow];
     double u_ep[kFwdT];                // this episode's selection uniforms, one per step
     int sx, sy, nfwd, tnext;
 };
@@ -322,8 +325,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         // the tail thread's copy of the state and the episode's return (it runs every selection)
         int cur_x = 0, cur_y = 0, cur_ret = 0;
         for (int i = tid; i < kMemoStates; i += blockDim.x) {
-            S.memo_q[i][0] = -1.0f;
-            S.memo_lg[i][0] = __builtin_nanf("");
+            S.memo[i][0] = -1.0f;
+            S.memo[i][S.kMemoLg] = __builtin_nanf("");
         }
         // the episode's selection uniforms up front, one thread per step (off the serial
         // select chain of thread 0; ordered before their use by the barriers below)
@@ -383,9 +386,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         // episode reuses that forward's logits (bit-identical to re-running it)
         // q: the fp32 selection cdf of lg (cdf_fast) when sampling; select_fast(q, lg, u) equals
         // select_fixed(lg, u) bit for bit (the exact fp64 cdf decides within 2^-15 of an edge)
-        auto finish_step = [&](const float (&lg)[kDrA], const float* q, int t, int sx, int sy) {
+        // u: this step's selection uniform (S.u_ep[t] when sampling)
+        auto finish_step = [&](const float (&lg)[kDrA], const float* q, int t, int sx, int sy, double u) {
             const int step = ep * p.horizon + t;
-            const double u = p.sample ? S.u_ep[t] : 0.0;
             const int a = p.sample ? select_fast<kDrA>(q, lg, p.temp, u) : select_fixed<kDrA>(lg, 0, p.temp, u);
             const int ea = p.perms ? perm[a] : a;
             int nx = sx + (ea == 0) - (ea == 1);
@@ -413,15 +416,14 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     int tt = t;
                     while (tt < p.horizon) {
                         const int sidx = cur_x * p.dim + cur_y;
-                        float lg[kDrA], qv[kDrA];
-#pragma unroll
-                        for (int k = 0; k < kDrA; ++k) {
-                            lg[k] = S.memo_lg[sidx][k];
-                            qv[k] = S.memo_q[sidx][k];
-                        }
+                        const floatx4* row = reinterpret_cast<const floatx4*>(&S.memo[sidx][0]);
+                        const floatx4 r0 = row[0], r1 = row[1], r2 = row[2];
+                        const double u = p.sample ? S.u_ep[tt] : 0.0;  // in the same LDS round trip
+                        const float qv[kDrA] = {r0[0], r0[1], r0[2], r0[3], r1[0]};
+                        const float lg[kDrA] = {r1[2], r1[3], r2[0], r2[1], r2[2]};
                         // a stored row: sampling reads its cdf (q[0] >= 0), greedy its logits
                         if (p.sample ? !(qv[0] >= 0.0f) : __builtin_isnan(lg[0])) break;
-                        finish_step(lg, qv, tt, cur_x, cur_y);
+                        finish_step(lg, qv, tt, cur_x, cur_y, u);
                         ++tt;
                     }
                     S.sx = cur_x;
@@ -473,11 +475,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     if (own0) {  // block 0: key/value (= y) of the query token (the merge below reads them)
                         const int lane = lane_id();
                         if ((lane & 15) == 0) {  // token 0's y (folded attention: key = value = y)
+                            const float ydown = exp2i(-M.attn_ey);  // ln_1 returns y x 2^attn_ey (PL)
 #pragma unroll
                             for (int k = 0; k < 8; ++k) {
                                 const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
-                                S.k0[d] = xn[0][k];
-                                S.v0[d] = xn[0][k];
+                                S.k0[d] = xn[0][k] * ydown;
+                                S.v0[d] = xn[0][k] * ydown;
                             }
                         }
                     }
@@ -504,11 +507,13 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             sdot = fmaf(q[j][4 + r], kc[r], sdot);
                         }
                         sdot = sum_cols(sdot);
-                        const float s0 = sdot * (scale * 1.4426950408889634f);  // exp2 domain, as attend's m
+                        // exp2 domain, as attend's m (q is at 2^attn_eq: u_proj3_w)
+                        const float s0 = sdot * ((scale * 1.4426950408889634f) * exp2i(-M.attn_eq));
                         const float mt = S.l0m[tok], lt = S.l0l[tok];
                         const float mn = fmaxf(mt, s0);
                         const float ea = __builtin_amdgcn_exp2f(mt - mn), eb = __builtin_amdgcn_exp2f(s0 - mn);
-                        const float inv = 1.0f / (lt * ea + eb);
+                        // 1 / l by v_rcp_f32 (1 ulp, attn_proj3_ol), with c_proj's split scale 2^attn_ey
+                        const float inv = __builtin_amdgcn_rcpf(lt * ea + eb) * exp2i(M.attn_ey);
                         floatx4 oa, ob;
                         if constexpr (kWs) {
                             const float* po = l0_cache<NW>(p, task, 2, qb[j]);
@@ -518,14 +523,21 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             oa = ld4(&S.l0o[qb[j]][lane][0]);
                             ob = ld4(&S.l0o[qb[j]][lane][4]);
                         }
+                        // on packed f32 ops (each half rounded as the scalar op)
+                        const floatx2 e2a = {ea, ea}, e2b = {eb, eb}, iv = {inv, inv};
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            o[j][r] = (oa[r] * ea + va[r] * eb) * inv;
-                            o[j][4 + r] = (ob[r] * ea + vb[r] * eb) * inv;
+                        for (int r = 0; r < 4; r += 2) {
+                            const floatx2 t0 = (floatx2{oa[r], oa[r + 1]} * e2a + floatx2{va[r], va[r + 1]} * e2b) * iv;
+                            const floatx2 t1 = (floatx2{ob[r], ob[r + 1]} * e2a + floatx2{vb[r], vb[r + 1]} * e2b) * iv;
+                            o[j][r] = t0.x;
+                            o[j][r + 1] = t0.y;
+                            o[j][4 + r] = t1.x;
+                            o[j][5 + r] = t1.y;
                         }
                     }
                     float xn[2][8];
-                    DPT_BLOCKS(nb, (attn_proj3<NB>(P, split0, o, x, M), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                    // o is the attention output x 2^attn_ey already (the merge's inv)
+                    DPT_BLOCKS(nb, (attn_proj3<NB>(P, split0, o, x, M, 1.0f), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
                                    mlp3_n<NB>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
                 }
                 DR_STAMP(1);
@@ -613,7 +625,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     if (kb <= qlast) {
                         const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
-                        const Split2 qs = split2(qv, exp2i(M.attn_eq));  // the query, broadcast to every column
+                        const Split2 qs = split2(qv, 1.0f);  // the query (x 2^attn_eq), broadcast to every column
                         float sv[8];
 #pragma unroll
                         for (int h = 0; h < 2; ++h) {
@@ -662,7 +674,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         // split key tile x the split query, broadcast to every column
                         const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
                         const Split2 ks = key_split(kv, kt, lane);
-                        const floatx4 sc = mfma_x3(ks, split2(qv, exp2i(M.attn_eq)), floatx4{0.f, 0.f, 0.f, 0.f});
+                        const floatx4 sc = mfma_x3(ks, split2(qv, 1.0f), floatx4{0.f, 0.f, 0.f, 0.f});
                         float sv[4], mt = -INFINITY;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -682,8 +694,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         for (int s4 = 0; s4 < 4; ++s4) o0 = mfma4(v0[s4], pr[s4], o0);
 #pragma unroll
                         for (int s4 = 0; s4 < 4; ++s4) o1 = mfma4(v1[s4], pr[s4], o1);
-                        o0 = o0 * exp2i(M.attn_ey + kPExp);
-                        o1 = o1 * exp2i(M.attn_ey + kPExp);
+                        o0 = o0 * exp2i(kPExp);  // the values are y x 2^attn_ey already
+                        o1 = o1 * exp2i(kPExp);
                         if (c == 0) {
                             *reinterpret_cast<floatx4*>(&S.part_o[kt][4 * g]) = o0;
                             *reinterpret_cast<floatx4*>(&S.part_o[kt][16 + 4 * g]) = o1;
@@ -725,7 +737,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
                     {
                         const float down = exp2i(-(M.attn_ew + M.attn_ey));
-                        const Split2 os = split2(o, 1.0f / lsum);
+                        const Split2 os = split2(o, __builtin_amdgcn_rcpf(lsum));
                         const floatx4 a0 = mfma_x3(pj0, os, ld4(W + PL::proj_b + 4 * g)) * down;
                         const floatx4 a1 = mfma_x3(pj1, os, ld4(W + PL::proj_b + 16 + 4 * g)) * down;
 #pragma unroll
@@ -738,10 +750,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     ln_cols(xl, xn, W + PL::ln2_g, W + PL::ln2_b);
                     {
                         // the MLP's fp16 two-part products at scale 2^(mlp_ew + mlp_ex) (mlp3_n)
-                        const float xs_scale = exp2i(M.mlp_ex), down = exp2i(-(M.mlp_ew + M.mlp_ex));
+                        const float down = exp2i(-(M.mlp_ew + M.mlp_ex));
                         // this wave's mlp.c_proj tiles, in flight across the c_fc products and gelu
                         const Split2 mp0 = f3.ld2(Frag3::mp + hw), mp1 = f3.ld2(Frag3::mp + 4 + hw);
-                        const Split2 xs = split2(xn, xs_scale);
+                        const Split2 xs = split2(xn, 1.0f);  // ln_2 returns x 2^mlp_ex (PL)
                         const floatx4 h0 = mfma_x3(fj0, xs, ld4(W + PL::fc_b + 2 * hw * 16 + 4 * g));
                         const floatx4 h1 = mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * hw + 1) * 16 + 4 * g));
                         const Split2 gs = gelu_split(h0, h1, GeluSplit(M.mlp_ew, M.mlp_ex));
@@ -800,12 +812,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             const int sidx = sx * p.dim + sy;
 #pragma unroll
                             for (int k = 0; k < kDrA; ++k) {
-                                S.memo_lg[sidx][k] = lg[k];
-                                S.memo_q[sidx][k] = q[k];
+                                S.memo[sidx][S.kMemoLg + k] = lg[k];
+                                S.memo[sidx][k] = q[k];
                             }
                         }
                         S.nfwd += 1;
-                        finish_step(lg, q, t, sx, sy);
+                        finish_step(lg, q, t, sx, sy, p.sample ? S.u_ep[t] : 0.0);
                         S.sx = cur_x;
                         S.sy = cur_y;
                     }

@@ -82,11 +82,13 @@ struct Split2 {
     halfx8 h, m;
 };
 __device__ inline Split2 split2(const float (&v)[8], float scale) {
-    // m = f16(x - h) (x = v scale) as one fma of the f32 value and the f16 h, rounded once to f16: the
-    // compiler emits v_fma_mix{lo,hi}_f16 (built with -fno-slp-vectorize; h is not converted
-    // back to fp32 first).  x - h is exact in fp32, so m equals f16(f32(x - h)).
-    // (an opaque 1.0 multiplier keeps the fma from folding into a plain subtraction, which
-    // would lose the mixed-precision form)
+    // m = f16(x - h) (x = v scale): x - h is exact in fp32, formed by one v_fma_mix_f32 per value
+    // (the f32 value times 1 minus the f16 h, no conversion of h back to fp32), and the pair is
+    // rounded to fp16 by one v_cvt_pk_f16_f32.  The same bits as v_fma_mix{lo,hi}_f16 (one fma
+    // rounded once to fp16), but those write half a register and issue at about 9.7 cycles each
+    // against 5.0 for v_fma_mix_f32 and 6.0 for the pack (scripts/valu_issue.hip,
+    // profiles/r4c/valu_issue.json): -2.1 % at config 3.  (An opaque 1.0 multiplier keeps the fma
+    // from folding into a plain subtraction, which would lose the mixed-precision form.)
     float one = 1.0f;
     asm volatile("" : "+s"(one));
     unsigned hh[4], mm[4];
@@ -94,8 +96,8 @@ __device__ inline Split2 split2(const float (&v)[8], float scale) {
     for (int p = 0; p < 4; ++p) {
         const floatx2 x = floatx2{v[2 * p], v[2 * p + 1]} * floatx2{scale, scale};
         const halfx2 h = __builtin_convertvector(x, halfx2);
-        const halfx2 m = {(_Float16)__builtin_fmaf(x.x, one, -(float)h.x),
-                          (_Float16)__builtin_fmaf(x.y, one, -(float)h.y)};
+        const halfx2 m = __builtin_convertvector(
+            floatx2{__builtin_fmaf(x.x, one, -(float)h.x), __builtin_fmaf(x.y, one, -(float)h.y)}, halfx2);
         hh[p] = __builtin_bit_cast(unsigned, h);
         mm[p] = __builtin_bit_cast(unsigned, m);
     }
@@ -279,7 +281,8 @@ struct GeluSplit {
 };
 __device__ inline Split2 gelu_split(const floatx4& a, const floatx4& b, const GeluSplit& k) {
     // pairs on the packed f32 ops (v_pk_mul / v_pk_fma: two values per issue, each rounded like
-    // the scalar op); hi from one v_cvt_pk_f16_f32 per pair, lo = f16(g - hi) by v_fma_mix as split2
+    // the scalar op); hi from one v_cvt_pk_f16_f32 per pair, lo = f16(g - hi) by v_fma_mix_f32 and a
+    // second pack, as split2
     float one = 1.0f;
     asm volatile("" : "+s"(one));
     const floatx2 c1 = {k.c1, k.c1}, c2 = {k.c2, k.c2}, sv = {k.s, k.s};
@@ -292,8 +295,8 @@ __device__ inline Split2 gelu_split(const floatx4& a, const floatx4& b, const Ge
         const floatx2 d = __builtin_elementwise_fma(e, sv, sv);
         const floatx2 g = y * floatx2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
         const halfx2 h = __builtin_convertvector(g, halfx2);
-        const halfx2 m = {(_Float16)__builtin_fmaf(g.x, one, -(float)h.x),
-                          (_Float16)__builtin_fmaf(g.y, one, -(float)h.y)};
+        const halfx2 m = __builtin_convertvector(
+            floatx2{__builtin_fmaf(g.x, one, -(float)h.x), __builtin_fmaf(g.y, one, -(float)h.y)}, halfx2);
         hh[p] = __builtin_bit_cast(unsigned, h);
         mm[p] = __builtin_bit_cast(unsigned, m);
     }
@@ -330,7 +333,7 @@ template <int NB>
 __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&x)[2][8],
                               int ew, int ex) {
     const int g = lane_id() >> 4;
-    const float xs_scale = exp2i(ex), down = exp2i(-(ew + ex));
+    const float down = exp2i(-(ew + ex));
     const GeluSplit gk(ew, ex);
     const floatx4 yb0 = ld4(W + PL::mp_b + 4 * g), yb1 = ld4(W + PL::mp_b + 16 + 4 * g);  // scaled (PL)
     floatx4 y0[2] = {yb0, yb0}, y1[2] = {yb1, yb1};
@@ -341,7 +344,7 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
     Split2 wf0 = f3.ld2(Frag3::fc, vo), wf1 = f3.ld2(Frag3::fc + 1, vo);
     Split2 xs[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], xs_scale);
+    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_2 output x 2^mlp_ex (PL)
 #pragma unroll
     for (int p = 0; p < kFF / 32; ++p) {
         const Split2 w0 = f3.ld2(Frag3::mp + p, vo), w1 = f3.ld2(Frag3::mp + 4 + p, vo);
@@ -366,13 +369,14 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
 }
 
 // u = xn G + g0 of the NB blocks (the folded c_attn: only its q part) on fp16 two-part
-// products (mfma_x3) at scale 2^(attn_ew + attn_ey), scaled back exactly; xs = the blocks'
-// LayerNorm outputs split at 2^attn_ey
+// products (mfma_x3) at scale 2^(attn_ew + attn_ey), returned at 2^attn_eq (the scale of the score
+// product's split query, so attend splits it as it stands); xs = the blocks' LayerNorm outputs
+// split at 2^attn_ey
 template <int NB>
 __device__ inline void u_proj3_w(const float* W, const Split2 (&wg)[2], const Split2 (&xs)[2], float (&q)[2][8],
                                  const ModelView& M) {
     const int g = lane_id() >> 4;
-    const float down = exp2i(-(M.attn_ew + M.attn_ey));
+    const float down = exp2i(M.attn_eq - (M.attn_ew + M.attn_ey));
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
         const Split2& w = wg[ob];
@@ -403,7 +407,7 @@ __device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float
                                  const ModelView& M) {
     Split2 xs[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
+    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
     u_proj3_s<NB>(W, f3, xs, q, M);
 }
 
@@ -424,19 +428,21 @@ __device__ inline void attn_proj3_s(const float* W, const FragSrc3& f3, const Sp
     const int vo = FragSrc3::lane_off();
     attn_proj3_w<NB>(W, f3.ld2(Frag3::proj, vo), f3.ld2(Frag3::proj + 1, vo), os, x, M);
 }
+// (oscale: the split's scale, 2^attn_ey for an attention output at its true scale)
 template <int NB>
 __device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8],
-                                  const ModelView& M) {
+                                  const ModelView& M, float oscale) {
     // the Wvp tiles ahead of the split
     const int vo = FragSrc3::lane_off();
     const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
     Split2 os[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], exp2i(M.attn_ey));
+    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], oscale);
     attn_proj3_w<NB>(W, w0, w1, os, x, M);
 }
 // the same from attend's unnormalised (o, l): o / l is the attention output x 2^attn_ey already,
-// so the split takes 1 / l as its scale (one multiply per value)
+// so the split takes 1 / l as its scale (one multiply per value; 1 / l by v_rcp_f32, 1 ulp, instead
+// of the dozen instructions of an IEEE division: -1.1 % at config 3 with the two below)
 template <int NB>
 __device__ inline void attn_proj3_ol(const float* W, const FragSrc3& f3, const float (&o)[2][8], const float (&l)[2],
                                      float (&x)[2][8], const ModelView& M) {
@@ -444,7 +450,7 @@ __device__ inline void attn_proj3_ol(const float* W, const FragSrc3& f3, const f
     const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
     Split2 os[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], 1.0f / l[j]);
+    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], __builtin_amdgcn_rcpf(l[j]));
     attn_proj3_w<NB>(W, w0, w1, os, x, M);
 }
 
@@ -493,7 +499,7 @@ __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2]
     Split2 xs[2];
     if constexpr (KV::kSplitK) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
+        for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
     }
     kv_store<NB>(S, qb, xn, xs);
 }
@@ -507,7 +513,7 @@ __device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const fl
     ld_g(f3, wg);
     Split2 xs[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], exp2i(M.attn_ey));
+    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
     kv_store<NB>(S, qb, xn, xs);
     u_proj3_w<NB>(W, wg, xs, q, M);
 }
@@ -529,10 +535,13 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     // and lsum, which shortens the per-tile chain (the test is one wave vote).
     constexpr float kSlack = 32.f;
     const int lane = lane_id(), g = lane >> 4, c = lane & 15;
+    // 1 / scale below without a division: the callers' scale is a constant, so 1 / (scale log2 e)
+    // folds at compile time and the power of two is exact (the same bits as the division)
+    const float inv_scale_c = 1.0f / (scale * 1.4426950408889634f);
     scale *= 1.4426950408889634f;  // log2(e): the exp2 domain
-    // scores on fp16 two-part products: keys x 2^attn_ey, queries x 2^attn_eq, and the
+    // scores on fp16 two-part products: keys x 2^attn_ey, queries x 2^attn_eq (as given), and the
     // exact power of two folded into the 1/sqrt(d) scale
-    const Split2 qs = split2(q, exp2i(M.attn_eq));
+    const Split2 qs = split2(q, 1.0f);  // q x 2^attn_eq already (u_proj3_w)
     scale *= exp2i(-(M.attn_ey + M.attn_eq));
     if constexpr (KV::kSplitV) {
         // both products on mfma_x3, key tiles in pairs: per tile S^T = K Q^T, per pair
@@ -548,7 +557,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         // the scaled score nor the P x 2^kPExp product is formed; masks only on the diagonal
         // tile and the tile holding key_lo.
         constexpr float kSlackP = 8.f;
-        const float inv_scale = 1.0f / scale;
+        const float inv_scale = inv_scale_c * exp2i(M.attn_ey + M.attn_eq);
         const int vlo = vt_lane_off(lane);
         m = -INFINITY;
         lsum = 0.f;
@@ -635,7 +644,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
             const floatx4 k0 = ld4(&S.K[kb * 16 + c][4 * g]);
             const floatx4 k1 = ld4(&S.K[kb * 16 + c][16 + 4 * g]);
             const float kv[8] = {k0[0], k0[1], k0[2], k0[3], k1[0], k1[1], k1[2], k1[3]};
-            ks = split2(kv, exp2i(M.attn_ey));
+            ks = split2(kv, 1.0f);  // y x 2^attn_ey already
         }
         const floatx4 sc = mfma_x3(ks, qs, floatx4{0.f, 0.f, 0.f, 0.f});
         float sv[4];
@@ -673,7 +682,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     }
     // the split-value form's scales (exact powers of two)
     lsum = sum_cols(lsum) * exp2i(kPExp);
-    const float up = exp2i(M.attn_ey + kPExp);
+    const float up = exp2i(kPExp);  // the values are y x 2^attn_ey already
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         o[r] = o0[r] * up;
@@ -695,20 +704,25 @@ __device__ inline int blocks_of_wave(int w, int nqb, int (&qb)[2]) {
 // Copy the small per-layer parameters of n_layer blocks into LDS (layout PL;
 // attention biases in the folded form: attn_b[0, E) = g0, proj_b = bvp).  The biases enter
 // the split products' accumulators, so they are stored at those products' scales (exact
-// powers of two): g0 and bvp x 2^(attn_ew + attn_ey), fc_b and mp_b x 2^(mlp_ew + mlp_ex).
+// powers of two): g0 and bvp x 2^(attn_ew + attn_ey), fc_b and mp_b x 2^(mlp_ew + mlp_ex).  The
+// LayerNorm parameters carry the scale of the split that consumes their output (ln_1: y x
+// 2^attn_ey, the keys, values and the u projection's B operand; ln_2: 2^mlp_ex, c_fc's B operand),
+// so ln_cols returns the scaled value and the split multiplies by nothing: exact powers of two, the
+// same bits as the scale applied after the LayerNorm.
 __device__ inline void load_layer_params(float* P, const ModelView& M, int tid, int nthreads) {
     const float sa = exp2i(M.attn_ew + M.attn_ey), sm = exp2i(M.mlp_ew + M.mlp_ex);
+    const float sy = exp2i(M.attn_ey), sx = exp2i(M.mlp_ex);
     for (int i = tid; i < M.n_layer * PL::size; i += nthreads) {
         const int l = i / PL::size, k = i % PL::size;
         const float* Wg = M.layers + (size_t)l * LayerOff::size;
         float v;
-        if (k < PL::ln1_b) v = Wg[LayerOff::ln1_g + k];
-        else if (k < PL::attn_b) v = Wg[LayerOff::ln1_b + k - PL::ln1_b];
+        if (k < PL::ln1_b) v = Wg[LayerOff::ln1_g + k] * sy;
+        else if (k < PL::attn_b) v = Wg[LayerOff::ln1_b + k - PL::ln1_b] * sy;
         else if (k < PL::attn_b + kE) v = M.l0[(size_t)l * L0Off::size + L0Off::g0 + k - PL::attn_b] * sa;  // folded
         else if (k < PL::proj_b) v = 0.f;                                                                 // unused
         else if (k < PL::ln2_g) v = M.l0[(size_t)l * L0Off::size + L0Off::bvp + k - PL::proj_b] * sa;     // folded
-        else if (k < PL::ln2_b) v = Wg[LayerOff::ln2_g + k - PL::ln2_g];
-        else if (k < PL::fc_b) v = Wg[LayerOff::ln2_b + k - PL::ln2_b];
+        else if (k < PL::ln2_b) v = Wg[LayerOff::ln2_g + k - PL::ln2_g] * sx;
+        else if (k < PL::fc_b) v = Wg[LayerOff::ln2_b + k - PL::ln2_b] * sx;
         else if (k < PL::mp_b) v = Wg[LayerOff::fc_b + k - PL::fc_b] * sm;
         else v = Wg[LayerOff::mp_b + k - PL::mp_b] * sm;
         P[i] = v;

@@ -82,7 +82,31 @@ __global__ void __launch_bounds__(512) kern(unsigned long long* out, float seed)
                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
                 : "v"(b[0]));
         }
-        if constexpr (K >= 4 && K != 8) {  // + 4 independent v_mfma_f32_16x16x32_f16
+        if constexpr (K == 11) {  // 8 v_fma_mix_f32 (f32 result: x * 1 - f32(f16 lo half))
+            asm volatile(
+                "v_fma_mix_f32 %0, %8, 1.0, %9 op_sel_hi:[0,0,1]\n v_fma_mix_f32 %1, %8, 1.0, %9 op_sel_hi:[0,0,1]\n"
+                "v_fma_mix_f32 %2, %8, 1.0, %9 op_sel_hi:[0,0,1]\n v_fma_mix_f32 %3, %8, 1.0, %9 op_sel_hi:[0,0,1]\n"
+                "v_fma_mix_f32 %4, %8, 1.0, %9 op_sel_hi:[0,0,1]\n v_fma_mix_f32 %5, %8, 1.0, %9 op_sel_hi:[0,0,1]\n"
+                "v_fma_mix_f32 %6, %8, 1.0, %9 op_sel_hi:[0,0,1]\n v_fma_mix_f32 %7, %8, 1.0, %9 op_sel_hi:[0,0,1]\n"
+                : "=v"(a[0]), "=v"(a[1]), "=v"(a[2]), "=v"(a[3]), "=v"(a[4]), "=v"(a[5]), "=v"(a[6]), "=v"(a[7])
+                : "v"(b[0]), "v"(b[1]));
+        }
+        if constexpr (K == 12) {  // 8 v_cvt_f32_f16
+            asm volatile(
+                "v_cvt_f32_f16 %0, %8\n v_cvt_f32_f16 %1, %8\n v_cvt_f32_f16 %2, %8\n v_cvt_f32_f16 %3, %8\n"
+                "v_cvt_f32_f16 %4, %8\n v_cvt_f32_f16 %5, %8\n v_cvt_f32_f16 %6, %8\n v_cvt_f32_f16 %7, %8\n"
+                : "=v"(a[0]), "=v"(a[1]), "=v"(a[2]), "=v"(a[3]), "=v"(a[4]), "=v"(a[5]), "=v"(a[6]), "=v"(a[7])
+                : "v"(b[0]));
+        }
+        if constexpr (K == 13) {  // 8 v_fma_mixlo_f16 into 8 fresh registers (no read of the old dst)
+            asm volatile(
+                "v_fma_mixlo_f16 %0, %8, %9, 0\n v_fma_mixlo_f16 %1, %8, %9, 0\n v_fma_mixlo_f16 %2, %8, %9, 0\n"
+                "v_fma_mixlo_f16 %3, %8, %9, 0\n v_fma_mixlo_f16 %4, %8, %9, 0\n v_fma_mixlo_f16 %5, %8, %9, 0\n"
+                "v_fma_mixlo_f16 %6, %8, %9, 0\n v_fma_mixlo_f16 %7, %8, %9, 0\n"
+                : "=v"(a[0]), "=v"(a[1]), "=v"(a[2]), "=v"(a[3]), "=v"(a[4]), "=v"(a[5]), "=v"(a[6]), "=v"(a[7])
+                : "v"(b[0]), "v"(b[1]));
+        }
+        if constexpr (K >= 4 && K != 8 && K <= 10) {  // + 4 independent v_mfma_f32_16x16x32_f16
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[j], 0, 0, 0);
         }
@@ -101,11 +125,12 @@ int main() {
     const char* names[] = {"16 v_mul_f32", "8 v_pk_mul_f32", "8 v_exp_f32", "8 v_fma_mixlo_f16",
                            "4 mfma16x16x32f16 alone", "4 mfma + 8 v_pk_mul_f32", "4 mfma + 8 v_exp_f32",
                            "4 mfma + 8 v_fma_mixlo_f16", "8 v_cvt_pk_f16_f32", "4 mfma + 8 v_cvt_pk_f16_f32",
-                           "4 mfma + 8 v_mul_f32"};
+                           "4 mfma + 8 v_mul_f32", "8 v_fma_mix_f32", "8 v_cvt_f32_f16", "8 v_fma_mixlo_f16 (write-only)"};
     void (*ks[])(unsigned long long*, float) = {kern<0>, kern<1>, kern<2>, kern<3>, kern<4>, kern<5>,
-                                                kern<6>, kern<7>, kern<8>, kern<9>, kern<10>};
+                                                kern<6>, kern<7>, kern<8>, kern<9>, kern<10>, kern<11>,
+                                                kern<12>, kern<13>};
     for (int waves_per_simd = 1; waves_per_simd <= 2; ++waves_per_simd) {
-        for (int k = 0; k < 11; ++k) {
+        for (int k = 0; k < 14; ++k) {
             unsigned long long h = 0;
             (void)hipMemset(d, 0, 16);
             // one workgroup per CU-sized slot: 4 or 8 waves (1 or 2 per SIMD)
