@@ -106,6 +106,29 @@ __global__ void __launch_bounds__(512) kern(unsigned long long* out, float seed)
                 : "=v"(a[0]), "=v"(a[1]), "=v"(a[2]), "=v"(a[3]), "=v"(a[4]), "=v"(a[5]), "=v"(a[6]), "=v"(a[7])
                 : "v"(b[0]), "v"(b[1]));
         }
+        // 8 independent instructions of one more form each (dst a[0..7], sources b[0..2])
+#define EIGHT(INS)                                                                                         \
+    asm volatile(INS(0) INS(1) INS(2) INS(3) INS(4) INS(5) INS(6) INS(7)                                   \
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]) \
+                 : "v"(b[0]), "v"(b[1]), "v"(b[2]))
+#define I_PKFMA(i) "v_fma_f32 %" #i ", %8, %9, %" #i "\n"
+#define I_PL16(i) "v_permlane16_swap_b32 %" #i ", %8\n"
+#define I_PL32(i) "v_permlane32_swap_b32 %" #i ", %8\n"
+#define I_MAX3(i) "v_max3_f32 %" #i ", %8, %9, %10\n"
+#define I_CND(i) "v_cndmask_b32 %" #i ", %8, %9, vcc\n"
+#define I_RCP(i) "v_rcp_f32 %" #i ", %8\n"
+#define I_MOV(i) "v_mov_b32 %" #i ", %8\n"
+#define I_FMAC(i) "v_fmac_f32 %" #i ", %8, %9\n"
+#define I_ADDU(i) "v_add_u32 %" #i ", %8, %9\n"
+        if constexpr (K == 14) EIGHT(I_PKFMA);
+        if constexpr (K == 15) EIGHT(I_PL16);
+        if constexpr (K == 16) EIGHT(I_PL32);
+        if constexpr (K == 17) EIGHT(I_MAX3);
+        if constexpr (K == 18) EIGHT(I_CND);
+        if constexpr (K == 19) EIGHT(I_RCP);
+        if constexpr (K == 20) EIGHT(I_MOV);
+        if constexpr (K == 21) EIGHT(I_FMAC);
+        if constexpr (K == 22) EIGHT(I_ADDU);
         if constexpr (K >= 4 && K != 8 && K <= 10) {  // + 4 independent v_mfma_f32_16x16x32_f16
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[j], 0, 0, 0);
@@ -125,12 +148,15 @@ int main() {
     const char* names[] = {"16 v_mul_f32", "8 v_pk_mul_f32", "8 v_exp_f32", "8 v_fma_mixlo_f16",
                            "4 mfma16x16x32f16 alone", "4 mfma + 8 v_pk_mul_f32", "4 mfma + 8 v_exp_f32",
                            "4 mfma + 8 v_fma_mixlo_f16", "8 v_cvt_pk_f16_f32", "4 mfma + 8 v_cvt_pk_f16_f32",
-                           "4 mfma + 8 v_mul_f32", "8 v_fma_mix_f32", "8 v_cvt_f32_f16", "8 v_fma_mixlo_f16 (write-only)"};
+                           "4 mfma + 8 v_mul_f32", "8 v_fma_mix_f32", "8 v_cvt_f32_f16", "8 v_fma_mixlo_f16 (write-only)", "8 v_fma_f32", "8 v_permlane16_swap_b32",
+                           "8 v_permlane32_swap_b32", "8 v_max3_f32", "8 v_cndmask_b32", "8 v_rcp_f32", "8 v_mov_b32",
+                           "8 v_fmac_f32", "8 v_add_u32"};
     void (*ks[])(unsigned long long*, float) = {kern<0>, kern<1>, kern<2>, kern<3>, kern<4>, kern<5>,
                                                 kern<6>, kern<7>, kern<8>, kern<9>, kern<10>, kern<11>,
-                                                kern<12>, kern<13>};
+                                                kern<12>, kern<13>, kern<14>, kern<15>, kern<16>, kern<17>,
+                                                kern<18>, kern<19>, kern<20>, kern<21>, kern<22>};
     for (int waves_per_simd = 1; waves_per_simd <= 2; ++waves_per_simd) {
-        for (int k = 0; k < 14; ++k) {
+        for (int k = 0; k < 23; ++k) {
             unsigned long long h = 0;
             (void)hipMemset(d, 0, 16);
             // one workgroup per CU-sized slot: 4 or 8 waves (1 or 2 per SIMD)
