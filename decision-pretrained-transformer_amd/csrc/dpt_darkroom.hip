@@ -123,6 +123,7 @@ struct alignas(16) DrSmem {
     static_assert(kMemoLg >= kDrA && kMemoLg + kDrA <= kMemoRow, "memo row layout");
     alignas(16) float memo[kMemoStates][kMemoRow];
     double u_ep[kFwdT];                // this episode's selection uniforms, one per step
+    alignas(16) float diag_bias[64 * 4];  // the diagonal score tile's causal mask (diag_bias_init)
     int sx, sy, nfwd, tnext;
 };
 
@@ -286,6 +287,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         for (int i = tid; i < (int)(sizeof(S.kv.VT) / 16); i += blockDim.x) vs[i] = uint4{0u, 0u, 0u, 0u};
     }
     for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
+    diag_bias_init(S.diag_bias, tid, blockDim.x);
 
     // the task's goal and action permutation, once (wave-uniform: scalar registers), not
     // reloaded from memory on thread 0's serial select chain every step
@@ -360,7 +362,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             for (int j = 0; j < 2; ++j) {
                 if (j >= nb) break;
                 float m, l, o[8];
-                attend(S.kv, q[j], qb[j], 1, scale, m, l, o, M);
+                attend(S.kv, q[j], qb[j], 1, scale, m, l, o, M, S.diag_bias);
                 // the partial at its true scale (attend's o, l carry 2^(attn_ey + kPExp), 2^kPExp)
                 l *= exp2i(-kPExp);
                 const float down = exp2i(-(M.attn_ey + kPExp));
@@ -585,7 +587,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     for (int j = 0; j < 2; ++j) {
                         if (j >= nb) break;
                         float m;
-                        attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M);
+                        attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, S.diag_bias);
                     }
                     DPT_BLOCKS(nb, attn_proj3_ol<NB>(W, split0.layer(layer), o, l, x, M));
                 }

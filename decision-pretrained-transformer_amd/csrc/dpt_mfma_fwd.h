@@ -526,7 +526,7 @@ __device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const fl
 // the attention output at the scale of the c_proj product's B operand (attn_proj3_ol).
 template <class KV>
 __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
-                              float& lsum, float (&o)[8], const ModelView& M) {
+                              float& lsum, float (&o)[8], const ModelView& M, const float* diag_bias = nullptr) {
     // The running reference m of a token column moves only when a key tile holds a
     // score more than kSlack above it (always for the first tile with a key): the
     // probabilities are exp(s - m) <= e^kSlack, so the sums cannot overflow, and the
@@ -579,9 +579,25 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
 #pragma unroll
                 for (int r = 0; r < 4; ++r) sv[4 * h + r] = sc[r];
                 if constexpr (decltype(masked)::value) {
+                    if (diag_bias) {
+                        // the causal mask of the diagonal tile as an additive 0 / -inf per (lane, r)
+                        // (diag_bias_init): one LDS read and four adds instead of a compare and a
+                        // v_cndmask per score (the latter issue at about 19 cycles each)
+                        if (kt == qb) {
+                            const floatx4 b = *reinterpret_cast<const floatx4*>(diag_bias + 4 * lane);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if ((kt == qb && 4 * g + r > c) || kt * 16 + 4 * g + r < key_lo) sv[4 * h + r] = -INFINITY;
+                            for (int r = 0; r < 4; ++r) sv[4 * h + r] += b[r];
+                        }
+                        if (key_lo > 0) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (kt * 16 + 4 * g + r < key_lo) sv[4 * h + r] = -INFINITY;
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if ((kt == qb && 4 * g + r > c) || kt * 16 + 4 * g + r < key_lo) sv[4 * h + r] = -INFINITY;
+                    }
                 }
             }
             const float mt = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
@@ -687,6 +703,15 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     for (int r = 0; r < 4; ++r) {
         o[r] = o0[r] * up;
         o[4 + r] = o1[r] * up;
+    }
+}
+
+// The diagonal score tile's causal mask as additive terms: element r of lane (g, c) is key 4g + r
+// of the tile against query c, masked (-inf) when 4g + r > c.  64 x 4 floats in LDS.
+__device__ inline void diag_bias_init(float* b, int tid, int nthreads) {
+    for (int i = tid; i < 64 * 4; i += nthreads) {
+        const int lane = i >> 2, r = i & 3;
+        b[i] = 4 * (lane >> 4) + r > (lane & 15) ? -INFINITY : 0.0f;
     }
 }
 

@@ -129,6 +129,22 @@ __global__ void __launch_bounds__(512) kern(unsigned long long* out, float seed)
         if constexpr (K == 20) EIGHT(I_MOV);
         if constexpr (K == 21) EIGHT(I_FMAC);
         if constexpr (K == 22) EIGHT(I_ADDU);
+#define I_BFI(i) "v_bfi_b32 %" #i ", %8, %9, %10\n"
+        if constexpr (K == 23) EIGHT(I_BFI);
+#define I_DPPQ(i) "v_add_f32_dpp %" #i ", %8, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+#define I_DPPM(i) "v_add_f32_dpp %" #i ", %8, %9 row_half_mirror row_mask:0xf bank_mask:0xf\n"
+        if constexpr (K == 25) EIGHT(I_DPPQ);
+        if constexpr (K == 26) EIGHT(I_DPPM);
+        if constexpr (K == 24) {  // 8 v_cndmask_b32_e64 on an SGPR-pair mask (the form the compiler emits)
+            unsigned long long msk = __builtin_amdgcn_read_exec();
+            asm volatile(
+                "v_cndmask_b32_e64 %0, %8, %9, %10\n v_cndmask_b32_e64 %1, %8, %9, %10\n"
+                "v_cndmask_b32_e64 %2, %8, %9, %10\n v_cndmask_b32_e64 %3, %8, %9, %10\n"
+                "v_cndmask_b32_e64 %4, %8, %9, %10\n v_cndmask_b32_e64 %5, %8, %9, %10\n"
+                "v_cndmask_b32_e64 %6, %8, %9, %10\n v_cndmask_b32_e64 %7, %8, %9, %10\n"
+                : "=v"(a[0]), "=v"(a[1]), "=v"(a[2]), "=v"(a[3]), "=v"(a[4]), "=v"(a[5]), "=v"(a[6]), "=v"(a[7])
+                : "v"(b[0]), "v"(b[1]), "s"(msk));
+        }
         if constexpr (K >= 4 && K != 8 && K <= 10) {  // + 4 independent v_mfma_f32_16x16x32_f16
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[j], 0, 0, 0);
@@ -150,13 +166,15 @@ int main() {
                            "4 mfma + 8 v_fma_mixlo_f16", "8 v_cvt_pk_f16_f32", "4 mfma + 8 v_cvt_pk_f16_f32",
                            "4 mfma + 8 v_mul_f32", "8 v_fma_mix_f32", "8 v_cvt_f32_f16", "8 v_fma_mixlo_f16 (write-only)", "8 v_fma_f32", "8 v_permlane16_swap_b32",
                            "8 v_permlane32_swap_b32", "8 v_max3_f32", "8 v_cndmask_b32", "8 v_rcp_f32", "8 v_mov_b32",
-                           "8 v_fmac_f32", "8 v_add_u32"};
+                           "8 v_fmac_f32", "8 v_add_u32", "8 v_bfi_b32", "8 v_cndmask_b32_e64 (SGPR mask)",
+                           "8 v_add_f32_dpp quad_perm", "8 v_add_f32_dpp row_half_mirror"};
     void (*ks[])(unsigned long long*, float) = {kern<0>, kern<1>, kern<2>, kern<3>, kern<4>, kern<5>,
                                                 kern<6>, kern<7>, kern<8>, kern<9>, kern<10>, kern<11>,
                                                 kern<12>, kern<13>, kern<14>, kern<15>, kern<16>, kern<17>,
-                                                kern<18>, kern<19>, kern<20>, kern<21>, kern<22>};
+                                                kern<18>, kern<19>, kern<20>, kern<21>, kern<22>, kern<23>,
+                                                kern<24>, kern<25>, kern<26>};
     for (int waves_per_simd = 1; waves_per_simd <= 2; ++waves_per_simd) {
-        for (int k = 0; k < 23; ++k) {
+        for (int k = 0; k < 27; ++k) {
             unsigned long long h = 0;
             (void)hipMemset(d, 0, 16);
             // one workgroup per CU-sized slot: 4 or 8 waves (1 or 2 per SIMD)
