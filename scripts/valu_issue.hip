@@ -133,6 +133,16 @@ __global__ void __launch_bounds__(512) kern(unsigned long long* out, float seed)
         if constexpr (K == 23) EIGHT(I_BFI);
 #define I_DPPQ(i) "v_add_f32_dpp %" #i ", %8, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
 #define I_DPPM(i) "v_add_f32_dpp %" #i ", %8, %9 row_half_mirror row_mask:0xf bank_mask:0xf\n"
+        if constexpr (K == 27) {  // 8 v_exp_f32 interleaved with 8 independent v_mul_f32 (trans / VALU overlap?)
+            asm volatile(
+                "v_exp_f32 %0, %0\n v_mul_f32 %8, %8, %16\n v_exp_f32 %1, %1\n v_mul_f32 %9, %9, %16\n"
+                "v_exp_f32 %2, %2\n v_mul_f32 %10, %10, %16\n v_exp_f32 %3, %3\n v_mul_f32 %11, %11, %16\n"
+                "v_exp_f32 %4, %4\n v_mul_f32 %12, %12, %16\n v_exp_f32 %5, %5\n v_mul_f32 %13, %13, %16\n"
+                "v_exp_f32 %6, %6\n v_mul_f32 %14, %14, %16\n v_exp_f32 %7, %7\n v_mul_f32 %15, %15, %16\n"
+                : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]),
+                  "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
+                : "v"(b[0]));
+        }
         if constexpr (K == 25) EIGHT(I_DPPQ);
         if constexpr (K == 26) EIGHT(I_DPPM);
         if constexpr (K == 24) {  // 8 v_cndmask_b32_e64 on an SGPR-pair mask (the form the compiler emits)
@@ -167,14 +177,15 @@ int main() {
                            "4 mfma + 8 v_mul_f32", "8 v_fma_mix_f32", "8 v_cvt_f32_f16", "8 v_fma_mixlo_f16 (write-only)", "8 v_fma_f32", "8 v_permlane16_swap_b32",
                            "8 v_permlane32_swap_b32", "8 v_max3_f32", "8 v_cndmask_b32", "8 v_rcp_f32", "8 v_mov_b32",
                            "8 v_fmac_f32", "8 v_add_u32", "8 v_bfi_b32", "8 v_cndmask_b32_e64 (SGPR mask)",
-                           "8 v_add_f32_dpp quad_perm", "8 v_add_f32_dpp row_half_mirror"};
+                           "8 v_add_f32_dpp quad_perm", "8 v_add_f32_dpp row_half_mirror",
+                           "8 v_exp_f32 + 8 v_mul_f32 interleaved"};
     void (*ks[])(unsigned long long*, float) = {kern<0>, kern<1>, kern<2>, kern<3>, kern<4>, kern<5>,
                                                 kern<6>, kern<7>, kern<8>, kern<9>, kern<10>, kern<11>,
                                                 kern<12>, kern<13>, kern<14>, kern<15>, kern<16>, kern<17>,
                                                 kern<18>, kern<19>, kern<20>, kern<21>, kern<22>, kern<23>,
-                                                kern<24>, kern<25>, kern<26>};
+                                                kern<24>, kern<25>, kern<26>, kern<27>};
     for (int waves_per_simd = 1; waves_per_simd <= 2; ++waves_per_simd) {
-        for (int k = 0; k < 27; ++k) {
+        for (int k = 0; k < 28; ++k) {
             unsigned long long h = 0;
             (void)hipMemset(d, 0, 16);
             // one workgroup per CU-sized slot: 4 or 8 waves (1 or 2 per SIMD)
