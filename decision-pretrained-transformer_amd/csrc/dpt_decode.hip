@@ -269,15 +269,18 @@ __device__ __attribute__((always_inline)) inline float4 attend_one(const float* 
     const floatx4 q4 = *reinterpret_cast<const floatx4*>(q + 4 * c);
     float m = -1e30f, l = 0.f;
     f2 alo = {0.f, 0.f}, ahi = {0.f, 0.f};
-    // one chunk of 8 * R positions; NT: non-temporal loads
-    auto chunk = [&](int base, auto ntc, auto nrc) {
+    // one chunk of 8 * R positions; NT: non-temporal loads; FULL: every position of the chunk is
+    // below pos (the whole chunks), so no row is predicated: the R loads issue back to back
+    // without a branch and an EXEC mask per row
+    auto chunk = [&](int base, auto ntc, auto nrc, auto fullc) {
         constexpr bool NT = decltype(ntc)::value;
         constexpr int R = decltype(nrc)::value;
+        constexpr bool FULL = decltype(fullc)::value;
         floatx4 kk[R], vv[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int p = base + 8 * r + g;
-            if (p < pos) {
+            if (FULL || p < pos) {
                 // non-temporal: each K/V row is read once per step by this CU only, so it
                 // must not evict the weights every workgroup re-reads from L2
                 const floatx4* ks = reinterpret_cast<const floatx4*>(kc + (size_t)p * PS) + c;
@@ -303,7 +306,7 @@ __device__ __attribute__((always_inline)) inline float4 attend_one(const float* 
             d = fmaf(q4.w, kk[r].w, d);
             d = dpp_sum8(d);
             const int p = base + 8 * r + g;
-            s[r] = (p < pos) ? d * scale : -INFINITY;
+            s[r] = (FULL || p < pos) ? d * scale : -INFINITY;
             mx = fmaxf(mx, s[r]);
         }
         const float mn = fmaxf(m, mx);
@@ -324,14 +327,16 @@ __device__ __attribute__((always_inline)) inline float4 attend_one(const float* 
     int base = 0;
     // whole chunks; the pinned ones (default cache policy) first
 #pragma unroll 1
-    for (const int pe = min(pos, pin) & ~(8 * NR - 1); base < pe; base += 8 * NR) chunk(base, std::false_type{}, full);
+    for (const int pe = min(pos, pin) & ~(8 * NR - 1); base < pe; base += 8 * NR)
+        chunk(base, std::false_type{}, full, std::true_type{});
 #pragma unroll 1
-    for (const int pe = pos & ~(8 * NR - 1); base < pe; base += 8 * NR) chunk(base, std::true_type{}, full);
+    for (const int pe = pos & ~(8 * NR - 1); base < pe; base += 8 * NR)
+        chunk(base, std::true_type{}, full, std::true_type{});
     if (base < pos) {  // the partial last chunk, with only as many rows as it needs
         const bool pinned = base < pin;
         tail_rows<NR>(pos - base, [&](auto nrc) {
-            if (pinned) chunk(base, std::false_type{}, nrc);
-            else chunk(base, std::true_type{}, nrc);
+            if (pinned) chunk(base, std::false_type{}, nrc, std::false_type{});
+            else chunk(base, std::true_type{}, nrc, std::false_type{});
         });
     }
     {   // the new position (group 0 only; all lanes run the shuffles)
