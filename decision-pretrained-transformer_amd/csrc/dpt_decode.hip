@@ -277,6 +277,28 @@ __device__ __attribute__((always_inline)) inline float4 attend_one(const float* 
         constexpr int R = decltype(nrc)::value;
         constexpr bool FULL = decltype(fullc)::value;
         floatx4 kk[R], vv[R];
+        if constexpr (FULL && KV_SAME) {
+            // whole chunk of the one y stream: buffer loads, the lane's byte offset (its g rows and c
+            // float4s) in a VGPR that stays fixed, the row base (base + 8 r positions) as the
+            // wave-uniform soffset: no 64-bit address arithmetic per row
+            // (the task's stream base is wave-uniform: read it into SGPRs so the descriptor is one)
+            const unsigned long long kb = reinterpret_cast<unsigned long long>(kc);
+            // (readfirstlane returns int: through unsigned first, or a set bit 31 of the low word
+            // would sign-extend over the high word)
+            const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)kb);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(kb >> 32));
+            const unsigned long long ku = (unsigned long long)lo | ((unsigned long long)hi << 32);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<void*>(ku), (short)0, 0x7fffffff, 0x00020000);
+            const int voff = (g * PS + 4 * c) * 4;
+            const int sbase = __builtin_amdgcn_readfirstlane(base * PS * 4);  // uniform: an SGPR offset
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int soff = sbase + 8 * r * PS * 4;
+                kk[r] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, NT ? 2 : 0));
+                vv[r] = kk[r];
+            }
+        } else
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int p = base + 8 * r + g;
