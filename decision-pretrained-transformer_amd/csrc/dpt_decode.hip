@@ -269,6 +269,17 @@ __device__ __attribute__((always_inline)) inline float4 attend_one(const float* 
     const floatx4 q4 = *reinterpret_cast<const floatx4*>(q + 4 * c);
     float m = -1e30f, l = 0.f;
     f2 alo = {0.f, 0.f}, ahi = {0.f, 0.f};
+    // KV_SAME (the rollout's one y stream per task): a buffer descriptor on the task's stream base,
+    // which is wave-uniform (read into SGPRs; readfirstlane returns int, so through unsigned first,
+    // or a set bit 31 of the low word would sign-extend over the high word)
+    __amdgpu_buffer_rsrc_t rs;
+    if constexpr (KV_SAME) {
+        const unsigned long long kb = reinterpret_cast<unsigned long long>(kc);
+        const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)kb);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(kb >> 32));
+        const unsigned long long ku = (unsigned long long)lo | ((unsigned long long)hi << 32);
+        rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ku), (short)0, 0x7fffffff, 0x00020000);
+    }
     // one chunk of 8 * R positions; NT: non-temporal loads; FULL: every position of the chunk is
     // below pos (the whole chunks), so no row is predicated: the R loads issue back to back
     // without a branch and an EXEC mask per row
@@ -277,19 +288,20 @@ __device__ __attribute__((always_inline)) inline float4 attend_one(const float* 
         constexpr int R = decltype(nrc)::value;
         constexpr bool FULL = decltype(fullc)::value;
         floatx4 kk[R], vv[R];
-        if constexpr (FULL && KV_SAME) {
-            // whole chunk of the one y stream: buffer loads, the lane's byte offset (its g rows and c
-            // float4s) in a VGPR that stays fixed, the row base (base + 8 r positions) as the
-            // wave-uniform soffset: no 64-bit address arithmetic per row
-            // (the task's stream base is wave-uniform: read it into SGPRs so the descriptor is one)
-            const unsigned long long kb = reinterpret_cast<unsigned long long>(kc);
-            // (readfirstlane returns int: through unsigned first, or a set bit 31 of the low word
-            // would sign-extend over the high word)
-            const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)kb);
-            const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(kb >> 32));
-            const unsigned long long ku = (unsigned long long)lo | ((unsigned long long)hi << 32);
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<void*>(ku), (short)0, 0x7fffffff, 0x00020000);
+        if constexpr (KV_SAME && !FULL) {
+            // the partial last chunk: rows past pos re-read position pos - 1 (masked in the scores
+            // below), so every load is unconditional and they issue back to back
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int pm = min(base + 8 * r + g, pos - 1);
+                kk[r] = __builtin_bit_cast(floatx4,
+                                           __builtin_amdgcn_raw_buffer_load_b128(rs, (pm * PS + 4 * c) * 4, 0, NT ? 2 : 0));
+                vv[r] = kk[r];
+            }
+        } else if constexpr (FULL && KV_SAME) {
+            // whole chunk: the lane's byte offset (its g rows and c float4s) in a VGPR that stays
+            // fixed, the row base (base + 8 r positions) as the wave-uniform soffset: no 64-bit
+            // address arithmetic per row
             const int voff = (g * PS + 4 * c) * 4;
             const int sbase = __builtin_amdgcn_readfirstlane(base * PS * 4);  // uniform: an SGPR offset
 #pragma unroll
