@@ -770,14 +770,15 @@ def test_rollout_darkroom_dim12_workspace_without_state_table():
     check_darkroom_tasks(outs[1], tasks, ref, Heps, horizon)
 
 
-@pytest.mark.parametrize("Heps,horizon,R", [(4, 100, 3), (2, 511, 1)])
-def test_rollout_darkroom_windows_over_256(Heps, horizon, R):
+@pytest.mark.parametrize("Heps,horizon,R,dim", [(4, 100, 3, 10), (2, 511, 1, 10), (2, 300, 1, 12)])
+def test_rollout_darkroom_windows_over_256(Heps, horizon, R, dim):
     """Windows of 257..512 tokens run the 16-wave kernel (one task per CU, keys and values of the
     whole window in LDS): window 301 (the reference's H = 300 with horizon 100, episodes of 1, 101,
     201 and 301 tokens) and 512 (the largest).  The logits memo is bit-identical to one forward per
     step, and sampled tasks agree with the float64 C oracle fed the same Philox draws (logits within
     1e-5, actions and returns exactly up to each task's first near-tie draw).  Without the
-    workspace these windows are rejected (NotImplementedError: use the per-step path)."""
+    workspace these windows are rejected (NotImplementedError: use the per-step path).  dim = 12
+    (144 states) runs without the per-state query table and the memo (both need <= 128 states)."""
     import bench
     import dpt_hip
     from oracle import c_oracle
@@ -792,7 +793,7 @@ def test_rollout_darkroom_windows_over_256(Heps, horizon, R):
     try:
         for memo in (True, False):
             dpt_hip.set_darkroom_memo(memo)
-            o = m.rollout_darkroom(goals, Heps, horizon, R, seed=seed, want_actions=True, want_logits=True,
+            o = m.rollout_darkroom(goals, Heps, horizon, R, dim=dim, seed=seed, want_actions=True, want_logits=True,
                                    want_forwards=True)
             outs[memo] = {k: o[k].cpu().numpy() for k in ("actions", "logits", "returns", "forwards")}
         dpt_hip.set_darkroom_workspace(False)
@@ -804,11 +805,12 @@ def test_rollout_darkroom_windows_over_256(Heps, horizon, R):
     on, off = outs[True], outs[False]
     for k in ("actions", "logits", "returns"):
         assert np.array_equal(on[k], off[k]), k
-    assert (off["forwards"] == horizon).all() and on["forwards"].sum() < off["forwards"].sum()
+    assert (off["forwards"] == horizon).all()
+    assert on["forwards"].sum() < off["forwards"].sum() if dim * dim <= 128 else (on["forwards"] == horizon).all()
     tasks = np.arange(0, N, 3)
     u = np.stack([philox_np.uniform(seed, k, tasks, d.STREAM_SELECT) for k in range(steps)])
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, npos, goals[tasks], Heps, horizon, R, u,
-                                    True, threads=16, want_logits=True)
+                                    True, dim=dim, threads=16, want_logits=True)
     res = {k: torch.from_numpy(on[k]) for k in ("logits", "actions", "returns")}
     assert check_darkroom_tasks(res, tasks, ref, Heps, horizon) >= len(tasks) // 2
 
