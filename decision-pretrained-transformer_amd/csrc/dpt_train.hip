@@ -260,18 +260,41 @@ __global__ void tr_wgrad_part(const float* __restrict__ X, const float* __restri
     part[(int64_t)c * (IN + 1) * OUT + k] = acc;
 }
 
-// dW (IN x OUT, the blob's [in][out] layout) and db (OUT) = the chunk partials summed in chunk order
-__global__ void tr_wgrad_reduce(const float* __restrict__ part, int nch, int IN, int OUT, float* __restrict__ dW,
-                                float* __restrict__ db) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= (IN + 1) * OUT) return;
+// dW (IN x OUT, the blob's [in][out] layout) and db (OUT) = the chunk partials summed in a fixed
+// order: 64 columns per workgroup (one per lane, 256-B coalesced rows), kTrRedWaves waves each
+// summing a contiguous run of chunks in chunk order (loads unrolled so several are in flight), the
+// run sums then added in wave order through LDS.  The same order every launch: deterministic.
+// (One thread per column over all chunks left ~17 workgroups per product serially reading ~500
+// partials: 61 % of a T = 501 training step.)
+constexpr int kTrRedWaves = 16;
+__global__ __launch_bounds__(64 * kTrRedWaves) void tr_wgrad_reduce(const float* __restrict__ part, int nch, int IN,
+                                                                    int OUT, float* __restrict__ dW,
+                                                                    float* __restrict__ db) {
+    __shared__ float runs[kTrRedWaves][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t K = (int64_t)(IN + 1) * OUT;
+    const int64_t k = (int64_t)blockIdx.x * 64 + lane;
+    const int c0 = (int)((int64_t)nch * w / kTrRedWaves), c1 = (int)((int64_t)nch * (w + 1) / kTrRedWaves);
     float acc = 0.f;
-    for (int c = 0; c < nch; ++c) acc += part[(int64_t)c * (IN + 1) * OUT + k];
-    if (k < IN * OUT) {
-        if (dW) dW[k] = acc;
-    } else if (db) {
-        db[k - IN * OUT] = acc;
+    if (k < K) {
+#pragma unroll 8
+        for (int c = c0; c < c1; ++c) acc += part[(int64_t)c * K + k];
     }
+    runs[w][lane] = acc;
+    __syncthreads();
+    if (w != 0 || k >= K) return;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kTrRedWaves; ++j) s += runs[j][lane];
+    if (k < (int64_t)IN * OUT) {
+        if (dW) dW[k] = s;
+    } else if (db) {
+        db[k - (int64_t)IN * OUT] = s;
+    }
+}
+static void reduce_parts(const float* part, int nch, int IN, int OUT, float* dW, float* db, hipStream_t st) {
+    const unsigned blocks = (unsigned)(((int64_t)(IN + 1) * OUT + 63) / 64);
+    hipLaunchKernelGGL(tr_wgrad_reduce, dim3(blocks), dim3(64 * kTrRedWaves), 0, st, part, nch, IN, OUT, dW, db);
 }
 
 // LayerNorm backward, one wave per row: n = (x - mean) rstd, dn = dy g,
@@ -451,7 +474,7 @@ __global__ __launch_bounds__(256) void tr_mm_rows(const float* __restrict__ X, c
 }
 
 // Weight-gradient partials of one chunk of kTrRowsPerChunk rows: part[c][i][o] = sum_r act(X[r][i])
-// dY[r][o] (i < IN) and part[c][IN][o] = sum_r dY[r][o], summed over the chunks in order by
+// dY[r][o] (i < IN) and part[c][IN][o] = sum_r dY[r][o], summed over the chunks in a fixed order by
 // tr_wgrad_reduce.  The chunk's rows are staged in LDS (zeros past R); each wave takes output
 // tiles (IN / 16) x (OUT / 16) round robin, 16 MFMA k-steps of 4 rows each.
 template <int IN, int OUT, bool ACT>
@@ -754,8 +777,7 @@ static int wgrad(const float* X, const float* dY, int R, int IN, int OUT, int ge
     const int nch = (R + kTrRowsPerChunk - 1) / kTrRowsPerChunk;
     hipLaunchKernelGGL(tr_wgrad_part, dim3(nch, blocks_for((int64_t)(IN + 1) * OUT)), dim3(kTrThreads), 0, st, X, dY,
                        R, IN, OUT, gelu, part);
-    hipLaunchKernelGGL(tr_wgrad_reduce, dim3(blocks_for((int64_t)(IN + 1) * OUT)), dim3(kTrThreads), 0, st, part, nch,
-                       IN, OUT, dW, db);
+    reduce_parts(part, nch, IN, OUT, dW, db, st);
     return launched("tr_wgrad");
 }
 
@@ -767,7 +789,7 @@ static int ln_param_grad(const float* x, const float* stt, const float* dy, int 
     else
         hipLaunchKernelGGL(tr_ln_param_part, dim3(nch, blocks_for(E)), dim3(kTrThreads), 0, st, x, stt, dy, R, E, part);
     // the (2, E) partials reduce like a bias-only weight gradient: IN = 1, OUT = E, [sum dy n | sum dy]
-    hipLaunchKernelGGL(tr_wgrad_reduce, dim3(blocks_for(2 * E)), dim3(kTrThreads), 0, st, part, nch, 1, E, dg, db);
+    reduce_parts(part, nch, 1, E, dg, db, st);
     return launched("tr_ln_param");
 }
 
@@ -835,8 +857,7 @@ static int wgrad_fast(int E, int kind, const float* X, const float* dY, int R, i
     else if (E == 32) wg_kind<32>(kind, X, dY, R, part, st);
     else wg_kind<64>(kind, X, dY, R, part, st);
     const int nch = (R + kTrRowsPerChunk - 1) / kTrRowsPerChunk;
-    hipLaunchKernelGGL(tr_wgrad_reduce, dim3(blocks_for((int64_t)(IN + 1) * OUT)), dim3(kTrThreads), 0, st, part, nch,
-                       IN, OUT, dW, db);
+    reduce_parts(part, nch, IN, OUT, dW, db, st);
     return launched("tr_wgrad_mfma");
 }
 

@@ -34,15 +34,23 @@ def param_list(model):
 def pack_params(params, dev=None):
     """Flatten the parameters (blob order) into one fp32 vector on ``dev`` (default: the
     parameters' own device).  The nn.Linear weights (the first and the second-to-last
-    parameter) are stored [out][in] by torch and [in][out] in the blob."""
+    parameter) are stored [out][in] by torch and [in][out] in the blob.  Called on every
+    training forward, so the common case (fp32, already on ``dev``) is one C++ flatten plus
+    the two transposed copies."""
     n = len(params)
-    parts = []
-    for i, p in enumerate(params):
-        v = p.detach()
-        if i in (0, n - 2):
-            v = v.t()
-        parts.append(v.to(device=dev or v.device, dtype=torch.float32).contiguous().reshape(-1))
-    return torch.cat(parts)
+    dev = dev or params[0].device
+    with torch.no_grad():
+        if all(p.dtype == torch.float32 and p.device == dev for p in params):
+            blob = torch._C._nn.flatten_dense_tensors([p.detach() for p in params])
+        else:
+            blob = torch.cat([p.detach().to(device=dev, dtype=torch.float32).reshape(-1) for p in params])
+        off = 0
+        for i, p in enumerate(params):
+            k = p.numel()
+            if i == 0 or i == n - 2:
+                blob[off:off + k].view(p.shape[1], p.shape[0]).copy_(p.detach().t())
+            off += k
+    return blob
 
 
 def _on_device(*tensors):
@@ -53,18 +61,31 @@ def _on_device(*tensors):
 
 
 def unpack_grads(dblob, params):
-    """Split a gradient blob into per-parameter gradients shaped like ``params``."""
-    out, off, n = [], 0, len(params)
-    for i, p in enumerate(params):
-        k = p.numel()
-        g = dblob[off:off + k]
+    """Split a gradient blob into per-parameter gradients shaped like ``params`` (views of the
+    blob; the two nn.Linear weights come back transposed to torch's [out][in])."""
+    return _unpack(dblob, [p.shape for p in params], [p.dtype for p in params])
+
+
+_META = {}
+
+
+def _unpack(dblob, shapes, dtypes):
+    key = tuple(shapes)
+    metas = _META.get(key)
+    if metas is None:  # shape templates for the C++ unflatten (no storage)
+        metas = _META[key] = [torch.empty(sh, device="meta") for sh in shapes]
+    total = sum(m.numel() for m in metas)
+    if total != dblob.numel():
+        raise ValueError(f"gradient blob {dblob.numel()} != parameters {total}")
+    out = list(torch._C._nn.unflatten_dense_tensors(dblob, metas))
+    n = len(shapes)
+    off = 0
+    for i, sh in enumerate(shapes):
+        k = metas[i].numel()
+        if i == 0 or i == n - 2:
+            out[i] = dblob[off:off + k].view(sh[1], sh[0]).t()
         off += k
-        if i in (0, n - 2):
-            g = g.reshape(p.shape[1], p.shape[0]).t()
-        out.append(g.reshape(p.shape).to(p.dtype))
-    if off != dblob.numel():
-        raise ValueError(f"gradient blob {dblob.numel()} != parameters {off}")
-    return out
+    return [g if dt == g.dtype else g.to(dt) for g, dt in zip(out, dtypes)]
 
 
 FORWARD_ONLY = _lib.TRAIN_FORWARD_ONLY  # inference workspace, no backward
@@ -122,7 +143,7 @@ class TransformerFunction(torch.autograd.Function):
         preds, ws = forward(d, blob, tok)
         if need:
             ctx.d, ctx.blob, ctx.tok, ctx.ws = d, blob, tok, ws
-            ctx.params_meta = [(p.shape, p.dtype, p.device) for p in params]
+            ctx.params_meta = ([p.shape for p in params], [p.dtype for p in params], [p.device for p in params])
         return preds
 
     @staticmethod
@@ -131,7 +152,7 @@ class TransformerFunction(torch.autograd.Function):
             raise RuntimeError("dpt_hip.train: the saved activations were released by the first backward; "
                                "a second backward through the same graph (retain_graph=True) is not supported")
         dblob = backward(ctx.d, ctx.blob, ctx.tok, ctx.ws, dpreds)
-        shapes = [torch.empty(s, dtype=dt, device="meta") for s, dt, _ in ctx.params_meta]
-        grads = [g.to(dv) for g, (_, _, dv) in zip(unpack_grads(dblob, shapes), ctx.params_meta)]
+        shapes, dtypes, devs = ctx.params_meta
+        grads = [g if g.device == dv else g.to(dv) for g, dv in zip(_unpack(dblob, shapes, dtypes), devs)]
         ctx.ws = None  # the saved activations are not needed again
         return (None, None) + tuple(g if need else None for g, need in zip(grads, ctx.needs_input_grad[2:]))
