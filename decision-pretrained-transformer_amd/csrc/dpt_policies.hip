@@ -14,7 +14,11 @@
 
 namespace dpt {
 
-constexpr int kPolThreads = 128;
+constexpr int kPolThreads = 128;  // launch bound
+#ifndef DPT_POL_BLOCK
+#define DPT_POL_BLOCK 64
+#endif
+constexpr int kPolBlock = DPT_POL_BLOCK;  // lanes per workgroup at launch
 
 // numpy pairwise_sum for float64 over a strided sequence x[k*stride], k < n
 // (loops_utils.h.src): blocks of <= 128 with 8 partials, recursive halving above.
@@ -103,7 +107,19 @@ __host__ __device__ inline double gemv_t_sum(Mk m, Rk r, int n) {
     for (int s0 = 0; s0 < m1; s0 += 2048) {
         const int nb = min(2048, m1 - s0);
         double l0 = 0.0, l1 = 0.0;
-        for (int k = s0; k < s0 + nb; k += 2) {
+        int k = s0;
+        // the products of 8 rows first (independent loads in flight), then the two chains in order
+        for (; k + 8 <= s0 + nb; k += 8) {
+            double pr[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) pr[t] = m(k + t) * r(k + t);
+#pragma unroll
+            for (int t = 0; t < 8; t += 2) {
+                l0 = l0 + pr[t];
+                l1 = l1 + pr[t + 1];
+            }
+        }
+        for (; k < s0 + nb; k += 2) {
             l0 = l0 + m(k) * r(k);
             l1 = l1 + m(k + 1) * r(k + 1);
         }
@@ -132,10 +148,17 @@ __host__ __device__ int linucb_choose(Act act, Rew rew, int n, const double* arm
         double acc[kMaxD * kMaxD];
         for (int p = 0; p < d; ++p)
             for (int q = p; q < d; ++q) acc[p * kMaxD + q] = 0.0;
-        for (int k = ls; k < ls + ml; ++k) {
-            const double* x = arms + (size_t)act(k) * d;
-            for (int p = 0; p < d; ++p)
-                for (int q = p; q < d; ++q) acc[p * kMaxD + q] = fma(x[p], x[q], acc[p * kMaxD + q]);
+        for (int k0 = ls; k0 < ls + ml; k0 += 8) {
+            // the arm indices of 8 transitions loaded together, then the fma chains in order
+            const int kn = min(8, ls + ml - k0);
+            int ak[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) ak[t] = t < kn ? act(k0 + t) : 0;
+            for (int t = 0; t < kn; ++t) {
+                const double* x = arms + (size_t)ak[t] * d;
+                for (int p = 0; p < d; ++p)
+                    for (int q = p; q < d; ++q) acc[p * kMaxD + q] = fma(x[p], x[q], acc[p * kMaxD + q]);
+            }
         }
         for (int p = 0; p < d; ++p)
             for (int q = p; q < d; ++q) cov[p * kMaxD + q] = cov[p * kMaxD + q] + acc[p * kMaxD + q];
@@ -252,7 +275,15 @@ struct PolicyParams {
     double* arm_value_out;
 };
 
+// LIN: the LinUCB instantiation (its own kernel, so the per-arm-sum policies keep their code and
+// registers); LinUCB's arm features (A x d) sit in LDS, read by every transition of every step.
+template <bool LIN>
 __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParams P) {
+    __shared__ double arms_s[LIN ? kMaxA * kMaxD : 1];
+    if constexpr (LIN) {
+        for (int t = threadIdx.x; t < P.A * P.d; t += blockDim.x) arms_s[t] = P.arms[t];
+        __syncthreads();
+    }
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
     const int A = P.A;
@@ -267,7 +298,7 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
     const size_t lstride = (size_t)L * P.N;    // arm stride of the lists
     // LinUCB keeps the context itself in the workspace (it re-reads it every step):
     // rewards [k][task] fp64, then arm indices [k][task] int32, lane-contiguous
-    const bool lin = P.policy == DPT_POLICY_LINUCB;
+    constexpr bool lin = LIN;
     double* lin_r = P.lists;
     int32_t* lin_a = reinterpret_cast<int32_t*>(P.lists + lstride);
     int n_ctx = 0;
@@ -285,16 +316,16 @@ __global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParam
         append(P.ctx_actions[(size_t)i * P.C + c], P.ctx_rewards[(size_t)i * P.C + c]);
     for (int h = 0; h < P.H; ++h) {
         int a = 0;
-        if (P.policy == DPT_POLICY_OPT) {
+        if (!LIN && P.policy == DPT_POLICY_OPT) {
             a = opt;
-        } else if (P.policy == DPT_POLICY_LINUCB) {
+        } else if constexpr (LIN) {
             if (P.C + h == 0) {  // np.random.choice(np.arange(dim)) for an empty context
                 const double u = P.policy_noise ? P.policy_noise[(size_t)i]
                                                 : philox_uniform(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_POLICY);
                 a = min((int)(u * A), A - 1);
             } else {
                 a = linucb_choose([&](int k) { return lin_a[(size_t)k * P.N + i]; },
-                                  [&](int k) { return lin_r[(size_t)k * P.N + i]; }, n_ctx, P.arms, A, P.d, P.c);
+                                  [&](int k) { return lin_r[(size_t)k * P.N + i]; }, n_ctx, arms_s, A, P.d, P.c);
             }
         } else {
             // per-arm sums over the context (numpy pairwise order, fp64)
@@ -387,8 +418,13 @@ int launch_rollout_policy(const dpt_policy_rollout_args& a, hipStream_t st) {
     P.ts_std = a.ts_std; P.ts_prior_mean = a.ts_prior_mean; P.ts_prior_var = a.ts_prior_var; P.seed = a.seed;
     P.means = a.means; P.arms = a.arms; P.noise = a.noise; P.policy_noise = a.policy_noise; P.lists = a.workspace;
     P.actions_out = a.actions_out; P.rewards_out = a.rewards_out; P.arm_value_out = a.arm_value_out;
-    hipLaunchKernelGGL(rollout_policy_kernel, dim3((a.N + kPolThreads - 1) / kPolThreads), dim3(kPolThreads), 0, st,
-                       P);
+    // one lane per task, so 4096 tasks fill only 32..64 CUs: 64-lane workgroups spread them wider
+    const int bs = kPolBlock;
+    const dim3 grid((a.N + bs - 1) / bs);
+    if (a.policy == DPT_POLICY_LINUCB)
+        hipLaunchKernelGGL(rollout_policy_kernel<true>, grid, dim3(bs), 0, st, P);
+    else
+        hipLaunchKernelGGL(rollout_policy_kernel<false>, grid, dim3(bs), 0, st, P);
     return check_hip(hipGetLastError(), "rollout_policy_kernel launch");
 }
 
