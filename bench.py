@@ -175,6 +175,151 @@ def cpu_baseline_darkroom(sd, goals, H, n_layer, n_tasks=None, n_eps=8):
                       "float64 C + OpenMP"}
 
 
+def stream_ceiling(N, H, n_layer, pin_positions, kernel_ms):
+    """The bandit rollout's read pattern alone (scripts/stream_probe.hip: every step's y rows of
+    blocks 1..L-1 exactly as attend_one reads them, no compute), timed here on the same GPU as the
+    headline: its time plus the token records' share at the same rate is the floor of the launch's
+    reads on this layout; frac = that floor / the rollout's kernel time."""
+    import ctypes
+    co = os.path.join(ROOT, "scripts", "stream_probe.co")
+    if not os.path.exists(co):
+        return None
+    nblk = n_layer - 1
+    y = torch.zeros(nblk * N * H * 32, dtype=torch.float32, device="cuda")
+    out = torch.zeros(1, device="cuda")
+    hip = ctypes.CDLL("libamdhip64.so")
+    mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+    if hip.hipModuleLoad(ctypes.byref(mod), co.encode()) or \
+            hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"stream_probe"):
+        return None
+    args = [ctypes.c_void_p(y.data_ptr()), ctypes.c_int(N), ctypes.c_int(H), ctypes.c_int(pin_positions),
+            ctypes.c_int(nblk), ctypes.c_void_p(out.data_ptr())]
+    ptrs = (ctypes.c_void_p * len(args))(*[ctypes.cast(ctypes.pointer(a), ctypes.c_void_p) for a in args])
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ts = []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        if hip.hipModuleLaunchKernel(fn, (N + 7) // 8, 1, 1, 512, 1, 1, 0, stream, ptrs, None):
+            return None
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    hip.hipModuleUnload(mod)
+    ms = min(ts)
+    ybytes = nblk * 128 * N * H * (H - 1) // 2
+    rec_ms = ms * (algorithmic_bytes(N, H, n_layer) - ybytes) / ybytes  # token records etc. at the probe's rate
+    return {"probe_ms": ms, "probe_TBps": ybytes / ms / 1e9, "floor_ms": ms + rec_ms,
+            "frac": (ms + rec_ms) / kernel_ms, "kernel": "scripts/stream_probe.hip (y reads only, same layout)",
+            "note": "floor = probe time of the y stream + the remaining algorithmic bytes at the probe's rate; "
+                    "frac = floor / rollout kernel_ms (1.0 = the launch reads at its layout's measured ceiling)"}
+
+
+def run_timed(one, steps, warmup, dist, backend, kernel_only):
+    """W untimed warmup steps, then K steps bracketed by a barrier + synchronize on both sides;
+    returns (elapsed s max over ranks, kernel ms: the rollout launch alone when kernel_only else
+    the whole step, max over ranks)."""
+    for w in range(warmup):
+        one(w)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record()
+        one(100 + k, kev[k])
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in (kev if kernel_only else ev)]))
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    return elapsed, kern_ms
+
+
+def darkroom_workload(L, H, Heps, N, first, count, n_total, dist, memo):
+    """BASELINE config 3 (config 5's per-GPU shard for --tasks 8192): the DarkRoom online eval
+    (evals/eval_darkroom.py:20-84, DPT sampling controller) over this rank's task block."""
+    import dpt_hip
+    from ctrls.ctrl_darkroom import DarkroomTransformerController
+    from dpt_hip.distributed import gather_rows
+    from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec
+    from evals import eval_darkroom
+    dpt_hip.set_darkroom_memo(memo)
+    sd, tmodel = synthetic_state_dict(L, 2, 5, H, seed=0)
+    tmodel.load_state_dict({**sd, "transformer.wte.weight": tmodel.transformer.wte.weight}, strict=True)
+    tmodel.cuda().eval()  # as eval.py:152 does
+    goals = np.array([(j, i) for j in range(10) for i in range(10)])
+    np.random.RandomState(0).shuffle(goals)   # collect_data.py:408-409 order, cycled to N
+    goals_all = goals[np.arange(n_total) % 100]
+    envs = [DarkroomEnv(10, g, H) for g in goals_all[first:first + count]]
+    vec = DarkroomEnvVec(envs, first_task=first)
+
+    def one(step_idx, ev=None):
+        np.random.seed(step_idx)
+        ctrl = DarkroomTransformerController(tmodel, batch_size=count, sample=True)
+        ret = eval_darkroom.deploy_online_vec(vec, ctrl, Heps, H, H)
+        if dist is not None:  # the per-task returns of every rank (online regret all-gather)
+            gather_rows(torch.from_numpy(ret).cuda(), n_total)
+        return ret
+
+    def roofline(kern_ms):
+        # The kernel runs one window forward per distinct query state per episode (the
+        # window is fixed within an episode, DESIGN.md): replay the first timed step
+        # (same np seed -> same draws -> same trajectory) untimed to count the forwards
+        # it ran, and price the roofline on those, not on one forward per env step.
+        np.random.seed(100)
+        ctrl = DarkroomTransformerController(tmodel, batch_size=count, sample=True)
+        fw = eval_darkroom.rollout_fused(vec, ctrl, Heps, H, H, want_forwards=True)["forwards"]
+        fw = fw.to(torch.int64).sum(0).cpu().numpy()  # (Heps,) forwards over all tasks
+        F = 2 * 2 + 5 + 1
+        ref_flops = count * H * (window_flops(1, L, F, 5, folded=False) +
+                                 (Heps - 1) * window_flops(1 + H, L, F, 5, folded=False))
+        flops = int(fw[0]) * window_flops(1, L, F, 5) + int(fw[1:].sum()) * window_flops(1 + H, L, F, 5)
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        # the ceiling of this mix: the blocks' products (mfma_x3 on the fp16 cores) at X3_PEAK_TF,
+        # the embedding and head (VALU) at the fp32 peak
+        parts = [window_flops(1, L, F, 5, split=True), window_flops(1 + H, L, F, 5, split=True)]
+        dense = int(fw[0]) * parts[0][0] + int(fw[1:].sum()) * parts[1][0]
+        peak = flops / (dense / X3_PEAK_TF + (flops - dense) / FP32_MFMA_PEAK_TF)
+        traffic = None  # HBM bytes read per launch (rocprofv3 FETCH_SIZE x2, scripts/profile_darkroom.sh)
+        pmc = os.path.join(ROOT, "profiles", "pmc_rollout_darkroom.json")
+        if os.path.exists(pmc) and count == 4096 and H == 100:
+            traffic = json.load(open(pmc)).get("hbm_fetch_bytes_corrected")
+        return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": achieved / peak, "traffic": traffic,
+                "peak_fp32_mfma": FP32_MFMA_PEAK_TF, "frac_of_fp32_mfma": achieved / FP32_MFMA_PEAK_TF,
+                "matrix_flops_per_launch": dense,
+                "kernel": "rollout_darkroom_kernel (one launch = one whole online eval)",
+                "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
+                "window_forwards_per_launch": int(fw.sum()),
+                "reference_flops_per_launch": ref_flops,
+                "note": "flops = window forwards the kernel ran (one per distinct state per episode) x "
+                        "FLOPs of that window with the folded attention; the reference runs one unfolded "
+                        "forward per env step (reference_flops_per_launch). peak = the ceiling of this "
+                        "FLOP mix: every product of the blocks (dense and attention) as fp32-accurate "
+                        "fp16 two-part split products (three 16x16x32 f16 MFMAs per K=32 tile: "
+                        "157.3 x 256/48 TFLOP/s), embedding and head at the fp32 peak (157.3)"}
+
+    workload = f"DarkRoom 10x10 online eval, DPT sampling policy, H=horizon={H}, Heps={Heps}, {N} tasks/GPU"
+    # rollout_darkroom_kernel: every matrix product as fp16 two-part splits on
+    # v_mfma_f32_16x16x32_f16 (h*h + h*m + m*h, fp32 accumulation: about 2^-21 relative per
+    # product, DESIGN.md); LayerNorm, softmax, gelu, embedding, head in fp32; selection cdf in fp32
+    # (the exact fp64 cdf within 2^-15 of an edge, select_fast)
+    dtype = ("f16x2-split MFMA products (fp32 accumulate, ~2^-21/product) + f32 VALU / "
+             "f32 selection cdf (f64 within 2^-15 of an edge); int32 grid")
+    return dict(one=one, roofline=roofline, env_steps=n_total * Heps * H, workload=workload, dtype=dtype,
+                cfg={"tasks_per_gpu": N, "horizon": H, "episodes": Heps}, sd=sd, goals=goals_all)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,6 +331,8 @@ def main():
     ap.add_argument("--var", type=float, default=0.3)
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-darkroom", action="store_true",
+                    help="bandit: skip the DarkRoom sub-object (darkroom_c3 / darkroom_c5_shard)")
     ap.add_argument("--darkroom-memo", type=int, choices=(0, 1), default=1,
                     help="darkroom: 1 = one window forward per distinct state per episode, 0 = one per step")
     args = ap.parse_args()
@@ -206,7 +353,7 @@ def main():
         else:
             dist.init_process_group(backend)
     import dpt_hip
-    from dpt_hip.distributed import gather_rows, regret_stats_allreduce, shard
+    from dpt_hip.distributed import regret_stats_allreduce, shard
 
     N, L, wl = args.tasks, args.layers, args.workload
     n_total = N * world
@@ -242,63 +389,12 @@ def main():
         # rollout_bandit_kernel: fp32 VALU + v_mfma_f32_16x16x4_f32 products; env arithmetic fp64
         dtype = "f32 (model: VALU + f32 MFMA) / f64 (env, rewards)"
     else:
-        from ctrls.ctrl_darkroom import DarkroomTransformerController
-        from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec
-        from evals import eval_darkroom
         H, Heps = args.H or 100, 40
-        dpt_hip.set_darkroom_memo(args.darkroom_memo)
-        sd, tmodel = synthetic_state_dict(L, 2, 5, H, seed=0)
-        tmodel.load_state_dict({**sd, "transformer.wte.weight": tmodel.transformer.wte.weight}, strict=True)
-        tmodel.cuda().eval()  # as eval.py:152 does
-        goals = np.array([(j, i) for j in range(10) for i in range(10)])
-        np.random.RandomState(0).shuffle(goals)   # collect_data.py:408-409 order, cycled to N
-        goals_all = goals[np.arange(n_total) % 100]
-        envs = [DarkroomEnv(10, g, H) for g in goals_all[first:first + count]]
-        vec = DarkroomEnvVec(envs, first_task=first)
+        dw = darkroom_workload(L, H, Heps, N, first, count, n_total, dist, args.darkroom_memo)
+        one, env_steps_per_step, workload, cfg, dtype = dw["one"], dw["env_steps"], dw["workload"], dw["cfg"], \
+            dw["dtype"]
 
-        def one(step_idx, ev=None):
-            np.random.seed(step_idx)
-            ctrl = DarkroomTransformerController(tmodel, batch_size=count, sample=True)
-            ret = eval_darkroom.deploy_online_vec(vec, ctrl, Heps, H, H)
-            if dist is not None:
-                gather_rows(torch.from_numpy(ret).cuda(), n_total)
-            return ret
-
-        env_steps_per_step = n_total * Heps * H
-        workload = f"DarkRoom 10x10 online eval, DPT sampling policy, H=horizon={H}, Heps={Heps}, {N} tasks/GPU"
-        cfg = {"tasks_per_gpu": N, "horizon": H, "episodes": Heps}
-        # rollout_darkroom_kernel: every matrix product as fp16 two-part splits on
-        # v_mfma_f32_16x16x32_f16 (h*h + h*m + m*h, fp32 accumulation: about 2^-21 relative per
-        # product); LayerNorm, softmax, gelu, embedding, head in fp32; selection cdf in fp32
-        # (the exact fp64 cdf within 2^-15 of an edge, select_fast)
-        dtype = ("f16x2-split MFMA products (fp32 accumulate, ~2^-21/product) + f32 VALU / "
-                 "f32 selection cdf (f64 within 2^-15 of an edge); int32 grid")
-
-    for w in range(args.warmup):
-        one(w)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record()
-        one(100 + k, kev[k])
-        ev[k][1].record()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    # bandit: the rollout kernel launch alone (kev); darkroom: the whole step (one fused launch)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in (kev if wl in ("bandit", "linear") else ev)]))
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
+    elapsed, kern_ms = run_timed(one, args.steps, args.warmup, dist, backend, wl in ("bandit", "linear"))
     value = env_steps_per_step * args.steps / elapsed
     if wl in ("bandit", "linear"):
         # kern_ms: HIP events around the one rollout launch (draws + rollout_bandit_kernel) on the
@@ -315,43 +411,13 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "rollout_bandit_kernel",
                 "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": abytes,
                 "kvcache_bytes_per_launch": kvcache_bytes(count, H, L)}
+        if rank == 0:
+            pin = ctypes_pin_positions(count, H, L)
+            sc = stream_ceiling(count, H, L, pin, kern_ms) if pin is not None else None
+            if sc is not None:
+                roof["stream_ceiling"] = sc
     else:
-        # The kernel runs one window forward per distinct query state per episode (the
-        # window is fixed within an episode): replay the first timed step
-        # (same np seed -> same draws -> same trajectory) untimed to count the forwards
-        # it ran, and price the roofline on those, not on one forward per env step.
-        np.random.seed(100)
-        ctrl = DarkroomTransformerController(tmodel, batch_size=count, sample=True)
-        fw = eval_darkroom.rollout_fused(vec, ctrl, Heps, H, H, want_forwards=True)["forwards"]
-        fw = fw.to(torch.int64).sum(0).cpu().numpy()  # (Heps,) forwards over all tasks
-        F = 2 * 2 + 5 + 1
-        ref_flops = count * H * (window_flops(1, L, F, 5, folded=False) +
-                                 (Heps - 1) * window_flops(1 + H, L, F, 5, folded=False))
-        flops = int(fw[0]) * window_flops(1, L, F, 5) + int(fw[1:].sum()) * window_flops(1 + H, L, F, 5)
-        achieved = flops / (kern_ms * 1e-3) / 1e12
-        # the ceiling of this mix: the blocks' products (mfma_x3 on the fp16 cores) at X3_PEAK_TF,
-        # the embedding and head (VALU) at the fp32 peak
-        parts = [window_flops(1, L, F, 5, split=True), window_flops(1 + H, L, F, 5, split=True)]
-        dense = int(fw[0]) * parts[0][0] + int(fw[1:].sum()) * parts[1][0]
-        peak = flops / (dense / X3_PEAK_TF + (flops - dense) / FP32_MFMA_PEAK_TF)
-        traffic = None  # HBM bytes read per launch (rocprofv3 FETCH_SIZE x2, scripts/profile_darkroom.sh)
-        pmc = os.path.join(ROOT, "profiles", "pmc_rollout_darkroom.json")
-        if os.path.exists(pmc) and count == 4096 and H == 100:
-            traffic = json.load(open(pmc)).get("hbm_fetch_bytes_corrected")
-        roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": achieved / peak, "traffic": traffic,
-                "peak_fp32_mfma": FP32_MFMA_PEAK_TF, "frac_of_fp32_mfma": achieved / FP32_MFMA_PEAK_TF,
-                "matrix_flops_per_launch": dense,
-                "kernel": "rollout_darkroom_kernel (one launch = one whole online eval)",
-                "kernel_ms": kern_ms, "algorithmic_flops_per_launch": flops,
-                "window_forwards_per_launch": int(fw.sum()),
-                "reference_flops_per_launch": ref_flops,
-                "note": "flops = window forwards the kernel ran (one per distinct state per episode) x "
-                        "FLOPs of that window with the folded attention; the reference runs one unfolded "
-                        "forward per env step (reference_flops_per_launch). peak = the ceiling of this "
-                        "FLOP mix: every product of the blocks (dense and attention) as fp32-accurate "
-                        "fp16 two-part split products (three 16x16x32 f16 MFMAs per K=32 tile: "
-                        "157.3 x 256/48 TFLOP/s), embedding and head at the fp32 peak (157.3)"}
+        roof = dw["roofline"](kern_ms)
     line = {
         "metric": "env-steps/sec/GPU (DPT policy in loop), 5-arm bandit H=500, 1/2/4/8 MI355X",
         "value": value,
@@ -377,11 +443,38 @@ def main():
         line["cpu_baseline"] = base
         line["cpu_baseline_kvcache"] = kv
     if rank == 0 and world == 1 and wl == "darkroom" and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline_darkroom(sd, goals_all, H, L)
+        line["cpu_baseline"] = cpu_baseline_darkroom(dw["sd"], dw["goals"], H, L)
+    if wl == "bandit" and not args.no_darkroom:
+        # BASELINE config 3 (one GPU: 4096 tasks) or, on more GPUs, config 5's per-GPU shard (8192
+        # tasks per GPU: config 5 itself at 8 GPUs), on the driver's clock beside the headline
+        n_dr = 4096 if world == 1 else 8192
+        f_dr, c_dr = shard(n_dr * world, world, rank)
+        dw = darkroom_workload(L, 100, 40, n_dr, f_dr, c_dr, n_dr * world, dist, 1)
+        dr_steps, dr_warm = 2, 1
+        el, km = run_timed(dw["one"], dr_steps, dr_warm, dist, backend, False)
+        sub = {"metric": "env-steps/sec (DarkRoom online eval, DPT policy in loop)",
+               "value": dw["env_steps"] * dr_steps / el, "unit": "env-steps/s (whole job, all GPUs)",
+               "steps": dr_steps, "warmup": dr_warm, "ms_per_step": el / dr_steps * 1e3, "dtype": dw["dtype"],
+               "config": dict(workload=dw["workload"], env_steps_per_step=dw["env_steps"], **dw["cfg"]),
+               "roofline": dw["roofline"](km)}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            sub["cpu_baseline"] = cpu_baseline_darkroom(dw["sd"], dw["goals"], 100, L)
+        line["darkroom_c3" if world == 1 else "darkroom_c5_shard"] = sub
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def ctypes_pin_positions(N, H, n_layer, budget=224 << 20, chunk=64):
+    """The Infinity-Cache residency of the rollout launch at the default budget (rollout_pin,
+    dpt_decode.hip: whole 64-position stream chunks split over blocks 1..L-1), for the stream
+    probe: the first pin positions are read with the default cache policy."""
+    nb = n_layer - 1
+    row = N * 32 * 4
+    if nb <= 0:
+        return None
+    return int(min((budget // (row * chunk)) // nb * chunk, H))
 
 
 if __name__ == "__main__":

@@ -147,11 +147,13 @@ class DeviceModel:
         return logits
 
     def rollout_bandit(self, means, H, var, sample=True, bandit_type=BANDIT_GAUSSIAN, seed=0,
-                       first_task=0, uniforms=None, noise=None, want_logits=False, counter=0):
+                       first_task=0, uniforms=None, noise=None, want_logits=False, counter=0, kvcache=None):
         """Fused online bandit rollout (evals/eval_bandit.py:56-103) on device.
 
         Step h draws at Philox counter ``counter + h`` (global task id first_task + i),
         the counters the per-step path's selects would consume from ``counter`` on.
+        ``kvcache``, optional: the caller's fp32 device workspace (at least ``kv_numel(N, H)``
+        elements, e.g. a view into a larger allocation); by default one is allocated.
 
         Returns dict of device tensors: actions (N,H) int32, rewards (N,H) f64,
         arm_value (N,H) f64 (= cum_means.T), logits (H,N,A) f32 if requested.
@@ -166,7 +168,13 @@ class DeviceModel:
         out["logits"] = (torch.empty((H, N, A), dtype=torch.float32, device=dev) if want_logits else None)
         if N == 0 or H == 0:  # no tasks or no steps: empty curves, nothing to run
             return out
-        kv = torch.empty(self.kv_numel(N, H), dtype=torch.float32, device=dev)
+        if kvcache is None:
+            kv = torch.empty(self.kv_numel(N, H), dtype=torch.float32, device=dev)
+        else:
+            kv = kvcache
+            if not (kv.is_cuda and kv.dtype == torch.float32 and kv.is_contiguous()
+                    and kv.numel() >= self.kv_numel(N, H)):
+                raise ValueError(f"kvcache must be a contiguous fp32 device tensor of >= {self.kv_numel(N, H)} elements")
         u_d = None if uniforms is None else _dev(uniforms, torch.float64, dev)
         g_d = None if noise is None else _dev(noise, torch.float64, dev)
         args = _lib.BanditRolloutArgs(
@@ -338,6 +346,15 @@ def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=Tr
         keep.append(t)
         return _p(t).value
 
+    if policy_noise is not None:
+        # the kernel indexes the injected draws by the policy's own layout (dpt_policies.hip):
+        # Thompson (H, N, A) when sampling, (H, 100, N, A) for the 100-draw vote; LinUCB (N,)
+        # uniforms for an empty context's random arm; no other policy reads them
+        want = {POLICY_THOMPSON: H * N * A if sample else H * 100 * N * A, POLICY_LINUCB: N}.get(int(policy))
+        got = int(policy_noise.numel() if isinstance(policy_noise, torch.Tensor) else np.asarray(policy_noise).size)
+        if want is not None and got != want:
+            raise ValueError(f"policy_noise has {got} draws; policy {int(policy)} (sample={bool(sample)}) "
+                             f"reads {want}")
     n = ctypes.c_int64()
     _lib.call("dpt_policy_workspace_numel", N, A, C + H, ctypes.byref(n))
     ws = torch.empty(n.value, dtype=torch.float64, device=dev)

@@ -144,10 +144,16 @@ class TransformerFunction(torch.autograd.Function):
         if need:
             ctx.d, ctx.blob, ctx.tok, ctx.ws = d, blob, tok, ws
             ctx.params_meta = ([p.shape for p in params], [p.dtype for p in params], [p.device for p in params])
+        # forward-only requested although a parameter requires grad: nothing is saved, so a
+        # backward through this node must say so (not the retain_graph message below)
+        ctx.forward_only = bool(flags & FORWARD_ONLY) and any(ctx.needs_input_grad[2:])
         return preds
 
     @staticmethod
     def backward(ctx, dpreds):
+        if getattr(ctx, "forward_only", False):
+            raise RuntimeError("dpt_hip.train: this forward ran with FORWARD_ONLY (no activations saved) while "
+                               "parameters require grad; drop the FORWARD_ONLY flag to train through it")
         if getattr(ctx, "ws", None) is None:
             raise RuntimeError("dpt_hip.train: the saved activations were released by the first backward; "
                                "a second backward through the same graph (retain_graph=True) is not supported")

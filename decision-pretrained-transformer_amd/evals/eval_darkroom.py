@@ -98,7 +98,14 @@ def rollout_fused(vec_env, controller, Heps, H, horizon, want_actions=False, wan
 def deploy_online_vec(vec_env, controller, Heps, H, horizon, fused=True):
     assert H % horizon == 0
     if fused and _fused_ok(vec_env, controller, H):
-        return rollout_fused(vec_env, controller, Heps, H, horizon)["returns"].to(torch.int64).cpu().numpy()
+        # the fused kernel holds the model's parameter block in LDS next to the window's K/V; a
+        # deep model whose block does not fit beside a long window is refused (DPT_EUNSUPPORTED ->
+        # NotImplementedError) before anything ran or any draw was consumed: take the per-step loop
+        ctr = controller._stream.counter
+        try:
+            return rollout_fused(vec_env, controller, Heps, H, horizon)["returns"].to(torch.int64).cpu().numpy()
+        except NotImplementedError:
+            controller._stream.counter = ctr
     ctx_rollouts = H // horizon
     num_envs = vec_env.num_envs
     dev = dpt_hip.device()

@@ -4,7 +4,10 @@ import os
 
 import numpy as np
 
-_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libdpt_oracle.so")
+# DPT_ORACLE_LIB selects another build of the same source (make -C oracle asan: the
+# AddressSanitizer / UBSan build that tests/test_oracle_sanitized.py runs the checks on)
+_LIB = os.environ.get("DPT_ORACLE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "build",
+                                                        "libdpt_oracle.so")
 _lib = None
 
 

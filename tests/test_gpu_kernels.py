@@ -507,13 +507,15 @@ def first_tie(margin, bar=1e-5):
 
 
 @pytest.mark.parametrize("A,H,var,N", [(5, 500, 0.3, 4096), (20, 1000, 0.3, 4096), (5, 500, 0.3, 4093)])
-def test_rollout_full_config_sampled_tasks(A, H, var, N):
+def test_rollout_full_config_all_tasks(A, H, var, N):
     """BASELINE configs 2 (5 arms, H=500) and 4 (20 arms, H=1000; one GPU's 4096-task shard) at full
-    size, and config 2 with a partial last tile (4093 tasks): the fused rollout agrees, on >= 64
-    sampled tasks (every slot of the first two tiles, the last tile, random ones), with the
-    float64 C oracle (pinned to the reference's rollouts by test_c_bandit_oracle_matches_reference)
-    fed the same Philox draws -- logits within 1e-5 at every step and actions / arm values
-    exactly, each task up to its first near-tie draw (a uniform within 1e-5 of a cdf edge)."""
+    size, and config 2 with a partial last tile (4093 tasks): EVERY task of the fused rollout agrees
+    with the float64 C oracle (pinned to the reference's rollouts by
+    test_c_bandit_oracle_matches_reference; K/V-cache form, bit-identical to its re-forward form)
+    fed the same Philox draws -- logits within 1e-5 at every compared step and actions / arm values
+    exactly, each task up to its first near-tie draw (a uniform within 1e-5 of a cdf edge, where
+    numpy's own expf decides).  The fraction of tasks compared over the whole horizon is printed
+    (reference: eval_bandit.py:56-103 / ctrl_bandit.py:422-444)."""
     import bench
     import dpt_hip
     from oracle import c_oracle
@@ -529,24 +531,32 @@ def test_rollout_full_config_sampled_tasks(A, H, var, N):
     out = m.rollout_bandit(means, H, var, True, seed=seed, want_logits=True)
     acts = out["actions"].cpu().numpy()
     av = out["arm_value"].cpu().numpy()
+    lg = out["logits"].cpu().numpy()
+    del out
+    torch.cuda.empty_cache()
     assert np.array_equal(av, means[np.arange(N)[:, None], acts])
-    tasks = sampled_tasks(N)
-    assert len(tasks) >= 64
+    tasks = np.arange(N)
     u = np.stack([philox_np.uniform(seed, h, tasks, dpt_hip.STREAM_SELECT) for h in range(H)])
     g = np.stack([philox_np.normal(seed, h, tasks, dpt_hip.STREAM_REWARD) for h in range(H)])
     blob = dpt_hip.pack_weights(sd, L).numpy()
-    ref = c_oracle.bandit_rollout_f64(blob, L, A, 4 * (1 + H), means[tasks], H, var, u, g, True, False, 16,
-                                      want_logits=True)
-    lg = out["logits"].cpu().numpy()[:, tasks]
-    margin = ref["margin"]  # (H, n)
-    full = 0
-    for j, t in enumerate(tasks):
-        n = first_tie(margin[:, j])  # steps 0..n-1 agree exactly; a near-tie may flip step n's action
-        full += n == H
-        assert_logits(lg[:min(n + 1, H), j], ref["logits"][:min(n + 1, H), j])
-        assert np.array_equal(acts[t, :n], ref["actions"][j, :n]), t
-        assert np.array_equal(av[t, :n], ref["arm_value"][j, :n]), t
-    assert full >= len(tasks) // 2  # most tasks never meet a near-tie: compared over all H steps
+    ref = c_oracle.bandit_rollout_f64(blob, L, A, 4 * (1 + H), means, H, var, u, g, True, False,
+                                      bench.host_cpus()[0], want_logits=True)
+    margin = ref["margin"]  # (H, N)
+    tie = margin < 1e-5
+    n_cmp = np.where(tie.any(0), tie.argmax(0), H)  # steps 0..n-1 agree exactly; a near-tie may flip step n
+    step = np.arange(H)[:, None]
+    # logits: every step up to and including each task's first near-tie
+    sel = step <= np.minimum(n_cmp, H - 1)[None, :]
+    got, want = lg[sel], ref["logits"][sel]
+    bad = np.abs(got - want) > 1e-5 * np.maximum(1, np.abs(want))
+    assert not bad.any(), (int(bad.sum()), float(np.abs(got - want).max()))
+    okmask = (step < n_cmp[None, :]).T  # (N, H)
+    assert np.array_equal(acts[okmask], ref["actions"][okmask])
+    assert np.array_equal(av[okmask], ref["arm_value"][okmask])
+    full = float((n_cmp == H).mean())
+    print(f"\nA={A} H={H} N={N}: {full:.4f} of tasks compared over all {H} steps, "
+          f"{okmask.mean():.5f} of all task-steps compared exactly")
+    assert okmask.mean() >= 0.9  # near-ties are rare (~8e-5 per step): nearly every step is compared
 
 
 def check_darkroom_tasks(out, tasks, ref, Heps, horizon):
@@ -576,7 +586,7 @@ def darkroom_config(N_total, seed=0):
 
 def test_rollout_darkroom_full_config3_sampled_tasks():
     """BASELINE config 3 at full size (4096 tasks, Heps=40, horizon=100, goals in collect_data.py's
-    shuffled order, logits memo on): 64 sampled tasks agree with the float64 C oracle fed the same
+    shuffled order, logits memo on): 256+ sampled tasks agree with the float64 C oracle fed the same
     Philox draws -- logits within 1e-5, actions and per-episode returns exactly, each task up to
     its first near-tie draw."""
     import bench
@@ -588,13 +598,15 @@ def test_rollout_darkroom_full_config3_sampled_tasks():
     m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + horizon))
     goals = darkroom_config(N)
     out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, counter=ctr, want_actions=True, want_logits=True)
-    tasks = sampled_tasks(N, tile=1, n_random=64)
+    tasks = sampled_tasks(N, tile=1, n_random=256)
     steps = Heps * horizon
     u = np.stack([philox_np.uniform(seed, ctr + k, tasks, d.STREAM_SELECT) for k in range(steps)])
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + horizon), goals[tasks], Heps,
-                                    horizon, 1, u, True, threads=16, want_logits=True)
-    assert len(tasks) >= 64
-    assert check_darkroom_tasks(out, tasks, ref, Heps, horizon) >= len(tasks) // 2
+                                    horizon, 1, u, True, threads=bench.host_cpus()[0], want_logits=True)
+    assert len(tasks) >= 256
+    full = check_darkroom_tasks(out, tasks, ref, Heps, horizon)
+    print(f"\nC3: {full} of {len(tasks)} sampled tasks compared over all {steps} steps")
+    assert full >= len(tasks) // 2
 
 
 @pytest.mark.parametrize("first_task", [0, 57344])
@@ -619,7 +631,7 @@ def test_rollout_darkroom_config5_shard(first_task):
     steps = Heps * horizon
     u = np.stack([philox_np.uniform(seed, k, first_task + tasks, d.STREAM_SELECT) for k in range(steps)])
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + horizon), goals[tasks], Heps,
-                                    horizon, 1, u, True, threads=16, want_logits=True)
+                                    horizon, 1, u, True, threads=bench.host_cpus()[0], want_logits=True)
     assert len(tasks) >= 64
     assert check_darkroom_tasks(out, tasks, ref, Heps, horizon) >= len(tasks) // 2
 
@@ -861,3 +873,30 @@ def test_rollout_darkroom_long_windows(Heps, horizon, R):
            "returns": torch.from_numpy(on["returns"])}
     assert len(tasks) >= 64
     assert check_darkroom_tasks(res, tasks, ref, Heps, horizon) >= len(tasks) // 2
+
+
+def test_rollout_bandit_stream_base_bit31():
+    """Regression for the round-4 GPU fault: rollout_bandit_kernel builds a buffer descriptor per
+    task stream from its base address, which once went through readfirstlane(int) and was
+    sign-extended when bit 31 of the base's low word was set (an illegal address).  The K/V
+    workspace is placed inside a larger allocation so that every stream base of the launch has
+    bit 31 of its low word set; the rollout must equal the one on an ordinary allocation bit for
+    bit.  Run once per suite; it is not a fault reproducer to loop on."""
+    _, m, _ = model_from_golden("bandit5")
+    N, H, seed = 64, 40, 77
+    means = np.random.RandomState(5).uniform(0, 1, (N, 5))
+    ref = m.rollout_bandit(means, H, 0.3, True, seed=seed, want_logits=True)
+    need = m.kv_numel(N, H)
+    assert need * 4 < (1 << 30)  # the whole workspace stays inside one 2 GiB half of the low word
+    big = torch.empty((1 << 30) + need + 1024, dtype=torch.float32, device="cuda")  # 4 GiB + workspace
+    off = ((0x80000000 + 0x400) - (big.data_ptr() & 0xFFFFFFFF)) % (1 << 32)
+    assert off % 4 == 0
+    kv = big[off // 4:off // 4 + need]
+    lo, hi = kv.data_ptr() & 0xFFFFFFFF, (kv.data_ptr() + 4 * need - 1) & 0xFFFFFFFF
+    assert lo >> 31 == 1 and hi >> 31 == 1 and hi > lo
+    out = m.rollout_bandit(means, H, 0.3, True, seed=seed, want_logits=True, kvcache=kv)
+    torch.cuda.synchronize()
+    for k in ("actions", "rewards", "arm_value", "logits"):
+        assert torch.equal(out[k], ref[k]), k
+    del big, kv, out
+    torch.cuda.empty_cache()

@@ -144,6 +144,62 @@ def test_train_gradients_full_windows_vs_oracle(name, B, C):
         assert e <= 5 * GRAD_TOL, (k, e)
 
 
+@pytest.mark.parametrize("E,sd,T", [(16, 2, 103), (64, 2, 103), (16, 1, 38), (64, 1, 38)])
+def test_train_gradients_other_widths_vs_oracle(E, sd, T):
+    """The matrix-core training kernels at widths 16 and 64 (tr_mm_rows / tr_wgrad_mfma /
+    tr_attn_*_mfma instantiations other than E = 32): every parameter's gradient against the
+    float64 oracle.  Windows with T % 16 != 0 and T % 4 != 0 cover the padded P / dS rows and the
+    partial key tiles."""
+    from models.net import Transformer
+    from oracle import dpt_oracle_torch as OT
+    A, L, B, C = 5, 3, 6, T - 1
+    torch.manual_seed(E + T)
+    m = Transformer(dict(horizon=C, state_dim=sd, action_dim=A, n_layer=L, n_embd=E, n_head=1, dropout=0.0,
+                         test=False))
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    w = {k: v.detach().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    m = m.cuda()
+    rs = np.random.RandomState(E * 7 + T)
+    hb = {"query_states": rs.randint(0, 10, (B, sd)).astype(np.float64),
+          "context_states": rs.randint(0, 10, (B, C, sd)).astype(np.float64),
+          "context_actions": np.eye(A)[rs.randint(0, A, (B, C))],
+          "context_next_states": rs.randint(0, 10, (B, C, sd)).astype(np.float64),
+          "context_rewards": rs.normal(0.5, 0.5, (B, C, 1)), "optimal_actions": np.eye(A)[rs.randint(0, A, B)]}
+    loss_ref, preds_ref, grads_ref = OT.grads(w, hb, L, sd, A)
+    batch = {k: torch.tensor(hb[k], dtype=torch.float32, device="cuda") for k in KEYS}
+    batch["zeros"] = torch.zeros((B, sd * sd + A + 1), device="cuda")
+    m.train()
+    pred = m(batch)
+    true = torch.tensor(hb["optimal_actions"], dtype=torch.float32, device="cuda")
+    true = true.unsqueeze(1).repeat(1, pred.shape[1], 1).reshape(-1, A)
+    loss = torch.nn.CrossEntropyLoss(reduction="sum")(pred.reshape(-1, A), true)
+    m.zero_grad()
+    loss.backward()
+    assert abs(loss.item() - loss_ref) <= 1e-5 * abs(loss_ref)
+    assert (np.abs(pred.detach().cpu().numpy() - preds_ref) <= 1e-5 * np.maximum(1, np.abs(preds_ref))).all()
+    for k, p in m.named_parameters():
+        if k.endswith("wte.weight"):
+            continue
+        e = rel_err(p.grad.detach().cpu().numpy(), grads_ref[k])
+        assert e <= 5 * GRAD_TOL, (k, e)
+
+
+def test_forward_only_flag_under_autograd_raises():
+    """FORWARD_ONLY requested while parameters require grad: the backward names that cause."""
+    from dpt_hip import train as tr
+    g = golden("train_grads.npz")
+    _, m = model_from_fixture("bandit5")
+    batch, _ = batch_from(g, "bandit5")
+    tok = m._tokens(batch)
+    dims = (m.n_layer, m.n_embd, m.state_dim, m.action_dim, m.n_positions, tok.shape[0], tok.shape[1],
+            tr.FORWARD_ONLY)
+    preds = tr.TransformerFunction.apply(tok, dims, *tr.param_list(m))
+    with pytest.raises(RuntimeError, match="FORWARD_ONLY"):
+        preds.square().sum().backward()
+
+
 def test_train_backward_deterministic():
     """Two backward passes of the same batch give bit-identical gradients (fixed-order sums)."""
     g = golden("train_grads.npz")
