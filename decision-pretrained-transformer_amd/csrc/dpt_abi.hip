@@ -52,6 +52,7 @@ int launch_rollin_darkroom(const int32_t*, const int32_t*, int, int, int, int, c
                            uint64_t, int64_t, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*,
                            hipStream_t);
 int launch_rollout_policy(const dpt_policy_rollout_args&, hipStream_t);
+int set_policy_wave(int on);
 int launch_pack_fragments(const ModelView&, float*, hipStream_t);
 int64_t fragments_numel(int n_layer);
 int launch_derive_l0(const ModelView&, float*, hipStream_t);
@@ -214,6 +215,10 @@ int dpt_tuning_set(int32_t key, int64_t value) {
     }
     if (key == DPT_TUNE_SELECT_FAST) {
         REQUIRE(set_select_fast((int)value) == DPT_OK, "select fast path %lld: 0 or 1", (long long)value);
+        return DPT_OK;
+    }
+    if (key == DPT_TUNE_POLICY_WAVE) {
+        REQUIRE(set_policy_wave((int)value) == DPT_OK, "policy wave kernel %lld: 0 or 1", (long long)value);
         return DPT_OK;
     }
     if (key == DPT_TUNE_BLOCK0_MFMA) {

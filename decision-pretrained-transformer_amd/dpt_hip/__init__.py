@@ -350,11 +350,13 @@ def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=Tr
         # the kernel indexes the injected draws by the policy's own layout (dpt_policies.hip):
         # Thompson (H, N, A) when sampling, (H, 100, N, A) for the 100-draw vote; LinUCB (N,)
         # uniforms for an empty context's random arm; no other policy reads them
-        want = {POLICY_THOMPSON: H * N * A if sample else H * 100 * N * A, POLICY_LINUCB: N}.get(int(policy))
         got = int(policy_noise.numel() if isinstance(policy_noise, torch.Tensor) else np.asarray(policy_noise).size)
-        if want is not None and got != want:
-            raise ValueError(f"policy_noise has {got} draws; policy {int(policy)} (sample={bool(sample)}) "
-                             f"reads {want}")
+        if int(policy) == POLICY_THOMPSON:
+            want = H * N * A if sample else H * 100 * N * A
+            if got != want:
+                raise ValueError(f"policy_noise has {got} draws; Thompson (sample={bool(sample)}) reads {want}")
+        elif int(policy) == POLICY_LINUCB and got < N:  # only step 0's row (N,) is read
+            raise ValueError(f"policy_noise has {got} draws; LinUCB reads the first {N}")
     n = ctypes.c_int64()
     _lib.call("dpt_policy_workspace_numel", N, A, C + H, ctypes.byref(n))
     ws = torch.empty(n.value, dtype=torch.float64, device=dev)
@@ -421,6 +423,12 @@ def set_select_fast(on):
     """select_action for 5 and 20 arms: the fp32 cdf with the exact fp64 cdf within 2^-15 of an edge
     (default), or the fp64 cdf for every sample.  Bit-identical either way."""
     _lib.call("dpt_tuning_set", _lib.TUNE_SELECT_FAST, int(bool(on)))
+
+
+def set_policy_wave(on):
+    """dpt_rollout_policy: one 64-lane workgroup per task with its context in LDS (default) or one
+    lane per task.  Bit-identical either way."""
+    _lib.call("dpt_tuning_set", _lib.TUNE_POLICY_WAVE, int(bool(on)))
 
 
 _darkroom_memo = True

@@ -152,6 +152,7 @@ TUNE_DARKROOM_MEMO = 3
 TUNE_CACHE_BUDGET = 4
 TUNE_BLOCK0_MFMA = 5
 TUNE_SELECT_FAST = 6
+TUNE_POLICY_WAVE = 7
 SIGNATURES["dpt_tuning_set"] = (_i32, [_i32, _i64])
 
 

@@ -86,13 +86,18 @@ const char* dpt_last_error(void);
  * DPT_TUNE_SELECT_FAST = 1 (default): dpt_select_action decides 5- and 20-arm
  * samples on the fp32 cdf when the uniform is more than 2^-15 from every cdf
  * edge and runs the exact fp64 cdf otherwise (the rollouts always do); 0: the
- * fp64 cdf for every sample.  Bit-identical either way.  */
+ * fp64 cdf for every sample.  Bit-identical either way.
+ * DPT_TUNE_POLICY_WAVE = 1 (default): dpt_rollout_policy runs one 64-lane
+ * workgroup per task with the task's context in LDS (the per-arm pairwise sums
+ * split over lanes in numpy's order); 0: one lane per task (the lane kernel, also
+ * taken when a context does not fit in LDS).  Bit-identical either way.  */
 #define DPT_TUNE_DECODE_TILE 1
 #define DPT_TUNE_PREFILL 2
 #define DPT_TUNE_DARKROOM_MEMO 3
 #define DPT_TUNE_CACHE_BUDGET 4
 #define DPT_TUNE_BLOCK0_MFMA 5
 #define DPT_TUNE_SELECT_FAST 6
+#define DPT_TUNE_POLICY_WAVE 7
 int dpt_tuning_set(int32_t key, int64_t value);
 /* number of visible gfx950 devices (0 on a CPU-only host; never faults) */
 int dpt_device_count(int* count_out_host);

@@ -556,7 +556,9 @@ def test_rollout_full_config_all_tasks(A, H, var, N):
     full = float((n_cmp == H).mean())
     print(f"\nA={A} H={H} N={N}: {full:.4f} of tasks compared over all {H} steps, "
           f"{okmask.mean():.5f} of all task-steps compared exactly")
-    assert okmask.mean() >= 0.9  # near-ties are rare (~8e-5 per step): nearly every step is compared
+    # near-ties are rare (a uniform within 1e-5 of one of the A - 1 interior edges: ~2e-5 (A - 1) per
+    # step), so most task-steps are compared: ~0.97 at 5 arms x 500 steps, ~0.84 at 20 arms x 1000
+    assert okmask.mean() >= 0.75
 
 
 def check_darkroom_tasks(out, tasks, ref, Heps, horizon):
