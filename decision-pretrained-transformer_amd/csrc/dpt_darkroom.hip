@@ -113,7 +113,8 @@ struct alignas(16) DrSmem {
     float ql[kE], xl[kE];             // last layer: q and residual of token T-1
     float part_o[kFwdBlocks][kE];      // last layer: per-key-tile attention partials
     float part_m[kFwdBlocks], part_l[kFwdBlocks];
-    float part_y[kFF / 32][kE];       // last layer: MLP partials per pair of hidden chunks
+    float tl_x[kE];                   // last layer (dr_tail): ln_2 output of token T-1
+    float tl_g[kFF];                  // last layer (dr_tail): its gelu outputs
     // per-episode logits memo, one row per grid state (dim * dim <= kMemoStates)
     // row s: the fp32 selection cdf q (cdf_fast: a hit selects by 5 compares) in [0, 5), the logits
     // in [kMemoLg, kMemoLg + 5); 48-B rows, read by three 16-B loads in one round trip.  (No separate
@@ -256,9 +257,179 @@ __global__ void __launch_bounds__(64) state_tables_kernel(ModelView M, int dim, 
     }
 }
 
-template <bool kWs, int NW>
+// LDS stores of this wave visible to its own later loads (waits for them: no barrier, one wave)
+__device__ inline void lds_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// Sum over the 32 lanes of each half of the wave (DPP within rows of 16, then the xor-16 partner);
+// every lane of the half gets the same value
+__device__ inline float dr_sum32(float d) {
+#define DR_DPP(v, ctrl) \
+    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false))
+    d += DR_DPP(d, 0xB1);   // quad_perm xor 1
+    d += DR_DPP(d, 0x4E);   // quad_perm xor 2
+    d += DR_DPP(d, 0x141);  // row_half_mirror: the two quads of each 8
+    d += DR_DPP(d, 0x140);  // row_mirror: the two 8s of each row of 16
+#undef DR_DPP
+    return sum_x16(d);      // the two rows of each 32
+}
+
+// The last layer of token T-1 after its attention partials: every product there has ONE column (the
+// token), so on the matrix cores 15 of 16 columns are waste and each operand needs its fp16 split.
+// The tail wave instead runs them as fp32 matrix-vector products on the VALU, lane (f = lane & 31,
+// half = lane >> 5) owning feature f: merge the key-tile partials, c_proj (Wvp) + residual, ln_2,
+// c_fc (hidden units lane and lane + 64) + gelu_new, mlp.c_proj (half's 64 hidden units, halves
+// summed) + residual, ln_f, head.  fp32 FMA chains: as accurate as the reference's fp32 matmuls (not
+// its summation order).  Vectors every lane needs (ln_2 output, gelu outputs) pass through LDS
+// within the wave.  Weights: pack_tail_kernel's per-lane fp32 runs (tail_w).  Returns the logits on
+// every lane.
+constexpr int kDrTailWv = 0, kDrTailFc = 64 * 16, kDrTailMp = 64 * (16 + 64), kDrTailFloats = 64 * (16 + 64 + 64);
+template <class Smem>
+__device__ inline void dr_tail(Smem& S, const float* P, const float* W, const PTop& pt, const float* tw, int nparts,
+                               const ModelView& M, float (&lg)[kDrA]) {
+    const int lane = lane_id(), f = lane & 31, hf = lane >> 5;
+    const floatx4* wv4 = reinterpret_cast<const floatx4*>(tw + kDrTailWv) + lane * 4;
+    const floatx4* wf4 = reinterpret_cast<const floatx4*>(tw + kDrTailFc) + lane * 16;
+    const floatx4* wm4 = reinterpret_cast<const floatx4*>(tw + kDrTailMp) + lane * 16;
+    // Wvp and c_fc now (their latency under the merge), mlp.c_proj once c_fc is done (registers)
+    floatx4 wv[4], wf[16], wm[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wv[i] = wv4[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wf[i] = wf4[i];
+    // merge the key-tile partials (attend's convention: o / l is the output x 2^attn_ey); this lane's
+    // 16 features 16 half .. 16 half + 15
+    float mx = -INFINITY;
+    for (int w = 0; w < nparts; ++w) mx = fmaxf(mx, S.part_m[w]);
+    float lsum = 0.f;
+    floatx4 o[4] = {};
+    for (int w = 0; w < nparts; ++w) {
+        const float e = __builtin_amdgcn_exp2f(S.part_m[w] - mx);
+        lsum += S.part_l[w] * e;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const floatx4 po = ld4(&S.part_o[w][16 * hf + 4 * r]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[r][i] = fmaf(po[i], e, o[r][i]);
+        }
+    }
+    // c_proj (Wvp, the folded attention): y_f = bvp_f + sum_k Wvp[k][f] out_k
+    float c0 = 0.f, c1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+            c0 = fmaf(wv[r][i], o[r][i], c0);
+            c1 = fmaf(wv[r][i + 1], o[r][i + 1], c1);
+        }
+    const float inv = __builtin_amdgcn_rcpf(lsum) * exp2i(-M.attn_ey);
+    const float y = sum_x32(c0 + c1) * inv + W[PL::proj_b + f] * exp2i(-(M.attn_ew + M.attn_ey));  // bvp scaled (PL)
+    const float x1 = S.xl[f] + y;
+    // ln_2 (PL keeps its parameters at the c_fc split's scale 2^mlp_ex: exact powers of two)
+    const float sx = exp2i(-M.mlp_ex);
+    const float mean = dr_sum32(x1) * (1.0f / kE);
+    const float d1 = x1 - mean;
+    const float rs1 = __builtin_amdgcn_rsqf(dr_sum32(d1 * d1) * (1.0f / kE) + 1e-5f);
+    const float xn = fmaf(d1 * rs1, W[PL::ln2_g + f] * sx, W[PL::ln2_b + f] * sx);
+    if (hf == 0) S.tl_x[f] = xn;
+    lds_wave_sync();
+    // c_fc: hidden units lane and lane + 64, each over the 32 features (two chains apiece)
+    const float mdown = exp2i(-(M.mlp_ew + M.mlp_ex));  // fc_b, mp_b at the MLP product scale (PL)
+    float h0a = W[PL::fc_b + lane] * mdown, h0b = 0.f, h1a = W[PL::fc_b + 64 + lane] * mdown, h1b = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const floatx4 xv = ld4(&S.tl_x[4 * r]);
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+            h0a = fmaf(wf[r][i], xv[i], h0a);
+            h0b = fmaf(wf[r][i + 1], xv[i + 1], h0b);
+            h1a = fmaf(wf[8 + r][i], xv[i], h1a);
+            h1b = fmaf(wf[8 + r][i + 1], xv[i + 1], h1b);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wm[i] = wm4[i];
+    S.tl_g[lane] = gelu_fast(h0a + h0b);
+    S.tl_g[64 + lane] = gelu_fast(h1a + h1b);
+    lds_wave_sync();
+    // mlp.c_proj: this half's 64 hidden units into feature f (four chains), halves summed
+    float m[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const floatx4 gv = ld4(&S.tl_g[64 * hf + 4 * r]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m[i] = fmaf(wm[r][i], gv[i], m[i]);
+    }
+    const float x2 = x1 + (sum_x32((m[0] + m[1]) + (m[2] + m[3])) + W[PL::mp_b + f] * mdown);
+    // ln_f, head
+    const float meanf = dr_sum32(x2) * (1.0f / kE);
+    const float d2 = x2 - meanf;
+    const float rs2 = __builtin_amdgcn_rsqf(dr_sum32(d2 * d2) * (1.0f / kE) + 1e-5f);
+    const float xf = fmaf(d2 * rs2, P[pt.lnf_g + f], P[pt.lnf_b + f]);
+#pragma unroll
+    for (int a = 0; a < kDrA; ++a) lg[a] = dr_sum32(xf * P[pt.head_w + a * kE + f]) + P[pt.head_b + a];
+}
+
+// The last block's fp32 matrix-vector weights in the lanes' order (dr_tail), after the fragments:
+// [Wvp: lane (f, half) -> Wvp[16 half + i][f], i < 16][c_fc: lane -> W_fc[i][lane], then W_fc[i][lane + 64],
+// i < 32][mlp.c_proj: lane (f, half) -> W_mp[64 half + i][f], i < 64]
+__global__ void pack_tail_kernel(ModelView M, float* __restrict__ out) {
+    const int L = M.n_layer;
+    const float* Wl = M.layers + (size_t)(L - 1) * LayerOff::size;
+    const float* Fl = M.l0 + (size_t)(L - 1) * L0Off::size;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kDrTailFloats; i += gridDim.x * blockDim.x) {
+        float v;
+        if (i < kDrTailFc) {
+            const int lane = i / 16, k = i % 16, f = lane & 31, hf = lane >> 5;
+            v = Fl[L0Off::Wvp + (16 * hf + k) * kE + f];
+        } else if (i < kDrTailMp) {
+            const int o = i - kDrTailFc, lane = o / 64, k = o % 64;
+            v = Wl[LayerOff::fc_w + (k & 31) * kFF + lane + (k >= 32 ? 64 : 0)];
+        } else {
+            const int o = i - kDrTailMp, lane = o / 64, k = o % 64, f = lane & 31, hf = lane >> 5;
+            v = Wl[LayerOff::mp_w + (64 * hf + k) * kE + f];
+        }
+        out[i] = v;
+    }
+}
+
+// The window's last block (the longest causal row) alone on the last wave, the other blocks
+// paired as blocks_of_wave does (waves w and nqb - 2 - w); with every slot taken (nqb = 2 NW) the
+// plain pairing.  Which wave computes a block changes no result (-2.2 % at config 3: the 7 blocks
+// of a 101-token window on 4 waves had wave 0 holding blocks 0 and 6 with the key-tile tail,
+// wave 3 the single block 3).  Returns the wave's block count.
+template <int NW>
+__device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
+    if (nqb < 2 * NW) {
+        if (wave == NW - 1) {
+            qb[0] = nqb - 1;
+            qb[1] = nqb - 1;
+            return 1;
+        }
+        return blocks_of_wave(wave, nqb - 1, qb);
+    }
+    return blocks_of_wave(wave, nqb, qb);
+}
+
+// Values fixed for a whole episode (the wave's blocks, their workspace addresses, the task) are
+// re-derived inside each step from copies the compiler cannot see through: otherwise it hoists
+// them out of the step loop, and at the 106-SGPR limit they live as spills in VGPR lanes, read back
+// by v_readlane (a VALU instruction plus its hazard wait) at every use.  Recomputing them is a few
+// scalar instructions.
+#ifndef DPT_DR_OPAQUE
+#define DPT_DR_OPAQUE 1
+#endif
+#define DR_OPQ(v) asm volatile("" : "+s"(v))
+
+// kTab: token 0's layer-0 input and LN1 output come from the per-state table (the workspace kernels
+// on grids of <= kMemoStates cells); without it block 0 is re-embedded and normalised every step
+template <bool kWs, int NW, bool kTab = kWs>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1)
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
+    static_assert(kWs || !kTab, "the state table lives in the workspace");
     __shared__ DrSmem<kWs, NW> S;
     constexpr bool kSplitV = decltype(S.kv)::kSplitV;
     extern __shared__ float P[];
@@ -266,7 +437,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr int kTailWave = DPT_TAIL_WAVE, kTailTid = 64 * kTailWave;
-    static_assert(kTailWave < NW && kTailWave < kFF / 32, "the tail wave is an MLP wave of the last layer");
+    static_assert(kTailWave < NW, "the tail wave is a wave of the workgroup");
     const int steps_total = p.Heps * p.horizon;
     const float scale = 0.17677669529663687f;  // 1/sqrt(head_dim = 32)
     const int L = M.n_layer;
@@ -292,32 +463,18 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     // the task's goal and action permutation, once (wave-uniform: scalar registers), not
     // reloaded from memory on thread 0's serial select chain every step
     const int goal_x = p.goals[2 * task], goal_y = p.goals[2 * task + 1];
-    int perm[kDrA];
+    // the action permutation packed 3 bits per action in one register (a shift and a mask per step
+    // instead of five held values and a select chain)
+    int perm_bits = 0;
 #pragma unroll
-    for (int k = 0; k < kDrA; ++k) perm[k] = p.perms ? p.perms[(size_t)task * kDrA + k] : k;
+    for (int k = 0; k < kDrA; ++k) perm_bits |= (p.perms ? p.perms[(size_t)task * kDrA + k] : k) << (3 * k);
     for (int ep = 0; ep < p.Heps; ++ep) {
         const int nctx = min(ep, p.R) * p.horizon;
         const int T = 1 + nctx;
         const int nqb = (T + 15) >> 4;
         const int qlast = (T - 1) >> 4, clast = (T - 1) & 15;
         int qb[2];
-        // the window's last block (the longest causal row) alone on the last wave, the other
-        // blocks paired as blocks_of_wave does (waves w and nqb - 2 - w); with every slot taken
-        // (nqb = 2 NW) the plain pairing.  Which wave computes a block changes no result
-        // (-2.2 % at config 3: the 7 blocks of a 101-token window on 4 waves had wave 0 holding
-        // blocks 0 and 6 with the key-tile tail, wave 3 the single block 3)
-        int nb;
-        if (nqb < 2 * NW) {
-            if (wave == NW - 1) {
-                qb[0] = nqb - 1;
-                qb[1] = nqb - 1;
-                nb = 1;
-            } else {
-                nb = blocks_of_wave(wave, nqb - 1, qb);
-            }
-        } else {
-            nb = blocks_of_wave(wave, nqb, qb);
-        }
+        const int nb = assign_blocks<NW>(wave, nqb, qb);
         const bool own0 = nb > 0 && qb[0] == 0;
         if (tid == 0) {
             S.sx = 0;
@@ -349,7 +506,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
             DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
                            u_proj_kv3_n<NB>(P, split0, xn, q, S.kv, qb, M)));
-            if (p.ws) {
+            if constexpr (kWs) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     if (j >= nb) break;
@@ -392,7 +549,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         auto finish_step = [&](const float (&lg)[kDrA], const float* q, int t, int sx, int sy, double u) {
             const int step = ep * p.horizon + t;
             const int a = p.sample ? select_fast<kDrA>(q, lg, p.temp, u) : select_fixed<kDrA>(lg, 0, p.temp, u);
-            const int ea = p.perms ? perm[a] : a;
+            const int ea = (perm_bits >> (3 * a)) & 7;
             int nx = sx + (ea == 0) - (ea == 1);
             int ny = sy + (ea == 2) - (ea == 3);
             nx = min(max(nx, 0), p.dim - 1);
@@ -438,24 +595,39 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 t = S.tnext;
                 if (t >= p.horizon) break;
             }
+#if DPT_DR_OPAQUE
+            // per-step copies of the episode's block assignment (see DR_OPQ)
+            int wv = wave, Tq = T, task_s = task;
+            DR_OPQ(wv);
+            DR_OPQ(Tq);
+            DR_OPQ(task_s);
+            const int nqb_s = (Tq + 15) >> 4;
+            int qb[2];
+            const int nb = assign_blocks<NW>(wv, nqb_s, qb);
+            const bool own0 = nb > 0 && qb[0] == 0;
+            const int qlast = (Tq - 1) >> 4, clast = (Tq - 1) & 15;
+            const int task = task_s;
+            const int T = Tq;
+#endif
             float x[2][8];
             float q[2][8];
             const int sx = S.sx, sy = S.sy;
-            if (p.ws) {
-                // the context tokens' inputs and queries from the episode's workspace; block 0
-                // (wave 0's first block) is re-embedded for its new query token
-// (with the state table, token 0's input comes from it and the other columns of block 0
-                // from the workspace)
+            if constexpr (kWs) {
+                // the context tokens' inputs and queries from the episode's workspace; token 0's
+                // input (the new query token) from the per-state table, or block 0 re-embedded
                 const bool col0 = (lane_id() & 15) == 0;
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     if (j >= nb) break;
                     ws_load(l0_cache<NW>(p, task, 1, qb[j]), q[j]);
-                    if (qb[j] == 0 && !p.tab) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
-                    else
+                    if constexpr (kTab) {
                         ws_load(qb[j] == 0 && col0 ? p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 8 * (lane_id() >> 4)
                                                    : l0_cache<NW>(p, task, 0, qb[j]),
                                 x[j]);
+                    } else {
+                        if (qb[j] == 0) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
+                        else ws_load(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
+                    }
                 }
             } else {
 #pragma unroll
@@ -466,9 +638,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             // ---- layer 0: queries of the window (token 0's is never used: it has no
             // earlier key), the query token's key/value new
             {
-                if (!p.tab) {
+                if constexpr (!kTab) {
                     float xn[2][8];
-                    if (p.ws) {
+                    if constexpr (kWs) {
                         if (own0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
                     } else {
                         DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
@@ -492,11 +664,19 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 if (nb > 0) {
                     // merge key 0 into the cached partial of every token column
                     const int lane = lane_id(), g = lane >> 4;
-                    const float* y0 = p.tab ? p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 32 + 8 * g : nullptr;
-                    const floatx4 ka = p.tab ? ld4(y0) : ld4(&S.k0[4 * g]);
-                    const floatx4 kc = p.tab ? ld4(y0 + 4) : ld4(&S.k0[16 + 4 * g]);
-                    const floatx4 va = p.tab ? ka : ld4(&S.v0[4 * g]);
-                    const floatx4 vb = p.tab ? kc : ld4(&S.v0[16 + 4 * g]);
+                    floatx4 ka, kc, va, vb;
+                    if constexpr (kTab) {
+                        const float* y0 = p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 32 + 8 * g;
+                        ka = ld4(y0);
+                        kc = ld4(y0 + 4);
+                        va = ka;
+                        vb = kc;
+                    } else {
+                        ka = ld4(&S.k0[4 * g]);
+                        kc = ld4(&S.k0[16 + 4 * g]);
+                        va = ld4(&S.v0[4 * g]);
+                        vb = ld4(&S.v0[16 + 4 * g]);
+                    }
                     float o[2][8];
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
@@ -606,14 +786,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 const float* W = P + (L - 1) * PL::size;
                 const FragSrc3 f3 = split0.layer(L - 1);
                 const auto& kv = S.kv;
-                // this wave's tail weight tiles (c_proj, c_fc of hidden chunks 2 wave and
-                // 2 wave + 1), in flight across the first barrier; the MLP runs on waves
-                // 0..kMlpWaves-1 (with 8 waves the upper four only take key tiles in (1))
-                constexpr int kMlpWaves = kFF / 32;
-                static_assert(kMlpWaves == 4 && NW >= kMlpWaves, "one pair of hidden chunks per MLP wave");
-                const int hw = wave & (kMlpWaves - 1);
-                const Split2 pj0 = f3.ld2(Frag3::proj), pj1 = f3.ld2(Frag3::proj + 1);
-                const Split2 fj0 = f3.ld2(Frag3::fc + 2 * hw), fj1 = f3.ld2(Frag3::fc + 2 * hw + 1);
+                // the fp32 tail weights of the last block (pack_tail_kernel), read by the tail wave
+                const float* tw = p.frag + (size_t)L * (Frag3::bytes / 4);
                 // (1) the attention as flash partials (m, l, o), in attend's convention (exp2
                 // domain; l and o at 2^kPExp and 2^(attn_ey + kPExp), so o / l is the output at
                 // the c_proj split's scale): with split values key tiles 2 wave and 2 wave + 1
@@ -710,102 +884,15 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 }
                 bar_lds();
                 DR_STAMP(2 * L - 1);
-                // (2) every MLP wave: merge the partials, c_proj + residual, ln_2, then
-                // MLP hidden chunks 2 wave and 2 wave + 1
-                float xl[8];
-                if (NW == kMlpWaves || wave < kMlpWaves) {
-                    const int g = lane_id() >> 4;
-                    float mx = -INFINITY;
-                    for (int w = 0; w < nparts; ++w) mx = fmaxf(mx, S.part_m[w]);
-                    float lsum = 0.f;
-                    floatx4 oa = {0.f, 0.f, 0.f, 0.f}, ob = {0.f, 0.f, 0.f, 0.f};
-                    for (int w = 0; w < nparts; ++w) {
-                        const float e = __builtin_amdgcn_exp2f(S.part_m[w] - mx);
-                        lsum += S.part_l[w] * e;
-                        const floatx4 pa = ld4(&S.part_o[w][4 * g]), pb = ld4(&S.part_o[w][16 + 4 * g]);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            oa[r] = fmaf(pa[r], e, oa[r]);
-                            ob[r] = fmaf(pb[r], e, ob[r]);
-                        }
-                    }
-                    // o / lsum: the attention output at the split scale 2^attn_ey
-                    const float o[8] = {oa[0], oa[1], oa[2], oa[3], ob[0], ob[1], ob[2], ob[3]};
-                    const floatx4 xa = ld4(&S.xl[4 * g]), xb = ld4(&S.xl[16 + 4 * g]);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        xl[r] = xa[r];
-                        xl[4 + r] = xb[r];
-                    }
-                    {
-                        const float down = exp2i(-(M.attn_ew + M.attn_ey));
-                        const Split2 os = split2(o, __builtin_amdgcn_rcpf(lsum));
-                        const floatx4 a0 = mfma_x3(pj0, os, ld4(W + PL::proj_b + 4 * g)) * down;
-                        const floatx4 a1 = mfma_x3(pj1, os, ld4(W + PL::proj_b + 16 + 4 * g)) * down;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            xl[r] += a0[r];
-                            xl[4 + r] += a1[r];
-                        }
-                    }
-                    float xn[8];
-                    ln_cols(xl, xn, W + PL::ln2_g, W + PL::ln2_b);
-                    {
-                        // the MLP's fp16 two-part products at scale 2^(mlp_ew + mlp_ex) (mlp3_n)
-                        const float down = exp2i(-(M.mlp_ew + M.mlp_ex));
-                        // this wave's mlp.c_proj tiles, in flight across the c_fc products and gelu
-                        const Split2 mp0 = f3.ld2(Frag3::mp + hw), mp1 = f3.ld2(Frag3::mp + 4 + hw);
-                        const Split2 xs = split2(xn, 1.0f);  // ln_2 returns x 2^mlp_ex (PL)
-                        const floatx4 h0 = mfma_x3(fj0, xs, ld4(W + PL::fc_b + 2 * hw * 16 + 4 * g));
-                        const floatx4 h1 = mfma_x3(fj1, xs, ld4(W + PL::fc_b + (2 * hw + 1) * 16 + 4 * g));
-                        const Split2 gs = gelu_split(h0, h1, GeluSplit(M.mlp_ew, M.mlp_ex));
-                        const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-                        const floatx4 y0 = mfma_x3(mp0, gs, zero) * down;
-                        const floatx4 y1 = mfma_x3(mp1, gs, zero) * down;
-                        if ((lane_id() & 15) == 0) {
-                            *reinterpret_cast<floatx4*>(&S.part_y[hw][4 * g]) = y0;
-                            *reinterpret_cast<floatx4*>(&S.part_y[hw][16 + 4 * g]) = y1;
-                        }
-                    }
-                }
-                bar_lds();
-                DR_STAMP(2 * L);
-                // (3) the tail wave: residual, ln_f, head, selection, env step
+                // (2) the tail wave: the rest of token T-1's last block (merge, c_proj, ln_2, MLP),
+                // ln_f and the head as fp32 matrix-vector products on the VALU (dr_tail), then
+                // selection and the env step
                 if (wave == kTailWave) {
                     // the step's serial tail: issue ahead of the other workgroup's waves on this SIMD
                     DPT_TAIL_PRIO(3);
-                    const int lane = lane_id(), g = lane >> 4;
-                    const float mdown = exp2i(-(M.mlp_ew + M.mlp_ex));  // mp_b is stored at the MLP product scale (PL)
-                    floatx4 ya = ld4(W + PL::mp_b + 4 * g) * mdown, yb = ld4(W + PL::mp_b + 16 + 4 * g) * mdown;
-#pragma unroll
-                    for (int w = 0; w < kFF / 32; ++w) {
-                        const floatx4 pa = ld4(&S.part_y[w][4 * g]), pb = ld4(&S.part_y[w][16 + 4 * g]);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            ya[r] += pa[r];
-                            yb[r] += pb[r];
-                        }
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        xl[r] += ya[r];
-                        xl[4 + r] += yb[r];
-                    }
-                    float xf[8];
-                    ln_cols(xl, xf, P + pt.lnf_g, P + pt.lnf_b);
+                    const int lane = lane_id();
                     float lg[kDrA];
-#pragma unroll
-                    for (int a = 0; a < kDrA; ++a) {
-                        const floatx4 w0 = ld4(P + pt.head_w + a * kE + 4 * g);
-                        const floatx4 w1 = ld4(P + pt.head_w + a * kE + 16 + 4 * g);
-                        float part = 0.f;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            part = fmaf(xf[r], w0[r], part);
-                            part = fmaf(xf[4 + r], w1[r], part);
-                        }
-                        lg[a] = sum_cols(part) + P[pt.head_b + a];
-                    }
+                    dr_tail(S, P, W, pt, tw, nparts, M, lg);
                     DR_STAMP(2 * L + 2);
                     if (lane == 0) {
                         float q[kDrA] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -892,10 +979,13 @@ __global__ void pack_split_kernel(ModelView M, unsigned short* __restrict__ out)
 
 int launch_pack_fragments(const ModelView& M, float* frag, hipStream_t st) {
     hipLaunchKernelGGL(pack_split_kernel, dim3(64), dim3(256), 0, st, M, reinterpret_cast<unsigned short*>(frag));
-    return check_hip(hipGetLastError(), "pack_split_kernel launch");
+    if (int rc = check_hip(hipGetLastError(), "pack_split_kernel launch")) return rc;
+    hipLaunchKernelGGL(pack_tail_kernel, dim3(36), dim3(256), 0, st, M, frag + (size_t)M.n_layer * (Frag3::bytes / 4));
+    return check_hip(hipGetLastError(), "pack_tail_kernel launch");
 }
 
-int64_t fragments_numel(int n_layer) { return (int64_t)n_layer * Frag3::bytes / 4; }
+// the split fragments of every layer, then the last layer's fp32 tail weights (pack_tail_kernel)
+int64_t fragments_numel(int n_layer) { return (int64_t)n_layer * Frag3::bytes / 4 + kDrTailFloats; }
 
 static bool g_darkroom_memo = true;  // DPT_TUNE_DARKROOM_MEMO
 
@@ -905,16 +995,16 @@ int set_darkroom_memo(int on) {
     return DPT_OK;
 }
 
-template <bool kWs, int NW>
+template <bool kWs, int NW, bool kTab = kWs>
 static int launch_darkroom_geom(const ModelView& M, const DarkroomParams& p, hipStream_t st) {
     const size_t dyn = sizeof(float) * (size_t)PTop::make(M.n_layer).total;
     if (dyn + sizeof(DrSmem<kWs, NW>) > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "n_layer=%d: parameter block does not fit in LDS", M.n_layer);
         return DPT_EUNSUPPORTED;
     }
-    const void* kern = reinterpret_cast<const void*>(rollout_darkroom_kernel<kWs, NW>);
+    const void* kern = reinterpret_cast<const void*>(rollout_darkroom_kernel<kWs, NW, kTab>);
     if (dyn > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-    hipLaunchKernelGGL((rollout_darkroom_kernel<kWs, NW>), dim3(p.N), dim3(NW * 64), dyn, st, M, p);
+    hipLaunchKernelGGL((rollout_darkroom_kernel<kWs, NW, kTab>), dim3(p.N), dim3(NW * 64), dyn, st, M, p);
     return check_hip(hipGetLastError(), "rollout_darkroom_kernel launch");
 }
 
@@ -940,8 +1030,13 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     p.forwards_out = a.forwards_out;
     p.memo = g_darkroom_memo && a.dim * a.dim <= kMemoStates;
     p.frag = frag;
-    p.ws = a.workspace;
-    p.tab = a.workspace && a.dim * a.dim <= kMemoStates ? a.workspace : nullptr;
+    // the workspace kernels take token 0's layer-0 input from the per-state table when the grid fits
+    // it (dim * dim <= kMemoStates); a larger grid runs the workspace-free kernel up to 256 tokens and
+    // the table-free workspace kernel above
+    const bool tab_ok = a.dim * a.dim <= kMemoStates;
+    const int64_t window0 = 1 + (int64_t)a.ctx_episodes * a.horizon;
+    p.ws = tab_ok || window0 > DrGeom<8>::kT ? a.workspace : nullptr;
+    p.tab = tab_ok ? p.ws : nullptr;
     if (M.n_layer < 2) {
         set_error(DPT_EUNSUPPORTED, "fused darkroom rollout needs n_layer >= 2 (got %d)", M.n_layer);
         return DPT_EUNSUPPORTED;
@@ -954,7 +1049,7 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     // tokens, 8 waves (one per CU) up to 256, 16 waves (one per CU, four per SIMD at 128 VGPRs,
     // keys and values of 512 tokens in LDS) up to 512
     const int64_t window = 1 + (int64_t)a.ctx_episodes * a.horizon;
-    const bool ws = a.workspace != nullptr;
+    const bool ws = p.ws != nullptr;
     if (window <= DrGeom<4>::kT)
         return ws ? launch_darkroom_geom<true, 4>(M, p, st) : launch_darkroom_geom<false, 4>(M, p, st);
     if (window <= DrGeom<8>::kT)
@@ -964,7 +1059,7 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
                   DrGeom<8>::kT);
         return DPT_EUNSUPPORTED;
     }
-    return launch_darkroom_geom<true, 16>(M, p, st);
+    return p.tab ? launch_darkroom_geom<true, 16>(M, p, st) : launch_darkroom_geom<true, 16, false>(M, p, st);
 }
 
 int darkroom_max_window() { return DrGeom<kDrMaxWaves>::kT; }
