@@ -113,8 +113,9 @@ struct alignas(16) DrSmem {
     float ql[kE], xl[kE];             // last layer: q and residual of token T-1
     float part_o[kFwdBlocks][kE];      // last layer: per-key-tile attention partials
     float part_m[kFwdBlocks], part_l[kFwdBlocks];
-    float tl_x[kE];                   // last layer (dr_tail): ln_2 output of token T-1
-    float tl_g[kFF];                  // last layer (dr_tail): its gelu outputs
+    float tl_x[kFF / 32][kE];         // last layer (dr_tail_mlp): ln_2 output of token T-1, per MLP wave
+    float tl_g[kFF / 32][32];         // last layer (dr_tail_mlp): the wave's gelu outputs
+    float part_y[kFF / 32][kE];       // last layer: mlp.c_proj shares per MLP wave
     // per-episode logits memo, one row per grid state (dim * dim <= kMemoStates)
     // row s: the fp32 selection cdf q (cdf_fast: a hit selects by 5 compares) in [0, 5), the logits
     // in [kMemoLg, kMemoLg + 5); 48-B rows, read by three 16-B loads in one round trip.  (No separate
@@ -279,54 +280,71 @@ __device__ inline float dr_sum32(float d) {
 
 // The last layer of token T-1 after its attention partials: every product there has ONE column (the
 // token), so on the matrix cores 15 of 16 columns are waste and each operand needs its fp16 split.
-// The tail wave instead runs them as fp32 matrix-vector products on the VALU, lane (f = lane & 31,
-// half = lane >> 5) owning feature f: merge the key-tile partials, c_proj (Wvp) + residual, ln_2,
-// c_fc (hidden units lane and lane + 64) + gelu_new, mlp.c_proj (half's 64 hidden units, halves
-// summed) + residual, ln_f, head.  fp32 FMA chains: as accurate as the reference's fp32 matmuls (not
-// its summation order).  Vectors every lane needs (ln_2 output, gelu outputs) pass through LDS
-// within the wave.  Weights: pack_tail_kernel's per-lane fp32 runs (tail_w).  Returns the logits on
-// every lane.
-constexpr int kDrTailWv = 0, kDrTailFc = 64 * 16, kDrTailMp = 64 * (16 + 64), kDrTailFloats = 64 * (16 + 64 + 64);
-template <class Smem>
-__device__ inline void dr_tail(Smem& S, const float* P, const float* W, const PTop& pt, const float* tw, int nparts,
-                               const ModelView& M, float (&lg)[kDrA]) {
-    const int lane = lane_id(), f = lane & 31, hf = lane >> 5;
+// They run instead as fp32 matrix-vector products on the VALU (fp32 FMA chains: as accurate as the
+// reference's fp32 matmuls, not its summation order), spread over the four MLP waves:
+//  dr_tail_mlp (wave w < 4, lane (f = lane & 31, half = lane >> 5)): merge the key-tile partials
+//    (every wave, the same values), c_proj (Wvp) + residual and ln_2 for feature f, then hidden units
+//    32 w .. 32 w + 31 of c_fc (unit 32 w + f, the half's 16 inputs, halves summed) + gelu_new, and
+//    their share of mlp.c_proj into feature f (the half's 16 units, halves summed) -> part_y[w];
+//  dr_tail_head (the tail wave, after a barrier): the four shares + residual, ln_f, head.
+// Each lane's 48 weights (pack_tail_kernel): Wvp and c_fc loaded before the attention partials, mlp.c_proj
+// after their barrier (dr_tail_ld_*).
+constexpr int kDrTailWv = 0, kDrTailFc = 64 * 16, kDrTailMp = 64 * 16 + 4 * 64 * 16,
+              kDrTailFloats = 64 * 16 + 2 * 4 * 64 * 16;
+struct DrTailW {
+    floatx4 wv[4], wf[4], wm[4];
+};
+// Wvp and c_fc, then mlp.c_proj (used after the merge, c_proj, ln_2 and c_fc)
+__device__ inline void dr_tail_ld_early(const float* tw, int w, DrTailW& t) {
+    const int lane = lane_id();
     const floatx4* wv4 = reinterpret_cast<const floatx4*>(tw + kDrTailWv) + lane * 4;
-    const floatx4* wf4 = reinterpret_cast<const floatx4*>(tw + kDrTailFc) + lane * 16;
-    const floatx4* wm4 = reinterpret_cast<const floatx4*>(tw + kDrTailMp) + lane * 16;
-    // Wvp and c_fc now (their latency under the merge), mlp.c_proj once c_fc is done (registers)
-    floatx4 wv[4], wf[16], wm[16];
+    const floatx4* wf4 = reinterpret_cast<const floatx4*>(tw + kDrTailFc) + (w * 64 + lane) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) wv[i] = wv4[i];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) wf[i] = wf4[i];
-    // merge the key-tile partials (attend's convention: o / l is the output x 2^attn_ey); this lane's
-    // 16 features 16 half .. 16 half + 15
-    float mx = -INFINITY;
-    for (int w = 0; w < nparts; ++w) mx = fmaxf(mx, S.part_m[w]);
-    float lsum = 0.f;
-    floatx4 o[4] = {};
-    for (int w = 0; w < nparts; ++w) {
-        const float e = __builtin_amdgcn_exp2f(S.part_m[w] - mx);
-        lsum += S.part_l[w] * e;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const floatx4 po = ld4(&S.part_o[w][16 * hf + 4 * r]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[r][i] = fmaf(po[i], e, o[r][i]);
-        }
+    for (int i = 0; i < 4; ++i) {
+        t.wv[i] = wv4[i];
+        t.wf[i] = wf4[i];
     }
-    // c_proj (Wvp, the folded attention): y_f = bvp_f + sum_k Wvp[k][f] out_k
+}
+__device__ inline void dr_tail_ld_late(const float* tw, int w, DrTailW& t) {
+    const floatx4* wm4 = reinterpret_cast<const floatx4*>(tw + kDrTailMp) + (w * 64 + lane_id()) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t.wm[i] = wm4[i];
+}
+// sum of the lane's 16 products with a 16-vector held as 4 floatx4 (two chains)
+__device__ inline float dot16(const floatx4 (&w)[4], const floatx4 (&v)[4]) {
     float c0 = 0.f, c1 = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int i = 0; i < 4; i += 2) {
-            c0 = fmaf(wv[r][i], o[r][i], c0);
-            c1 = fmaf(wv[r][i + 1], o[r][i + 1], c1);
+            c0 = fmaf(w[r][i], v[r][i], c0);
+            c1 = fmaf(w[r][i + 1], v[r][i + 1], c1);
         }
+    return c0 + c1;
+}
+// returns x1 (the residual after c_proj) for feature f
+template <class Smem>
+__device__ inline float dr_tail_mlp(Smem& S, const float* W, const DrTailW& t, int w, int nparts, const ModelView& M) {
+    const int lane = lane_id(), f = lane & 31, hf = lane >> 5;
+    // merge the key-tile partials (attend's convention: o / l is the output x 2^attn_ey); this lane's
+    // 16 features 16 half .. 16 half + 15
+    float mx = -INFINITY;
+    for (int k = 0; k < nparts; ++k) mx = fmaxf(mx, S.part_m[k]);
+    float lsum = 0.f;
+    floatx4 o[4] = {};
+    for (int k = 0; k < nparts; ++k) {
+        const float e = __builtin_amdgcn_exp2f(S.part_m[k] - mx);
+        lsum += S.part_l[k] * e;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const floatx4 po = ld4(&S.part_o[k][16 * hf + 4 * r]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[r][i] = fmaf(po[i], e, o[r][i]);
+        }
+    }
+    // c_proj (Wvp, the folded attention): y_f = bvp_f + sum_k Wvp[k][f] out_k
     const float inv = __builtin_amdgcn_rcpf(lsum) * exp2i(-M.attn_ey);
-    const float y = sum_x32(c0 + c1) * inv + W[PL::proj_b + f] * exp2i(-(M.attn_ew + M.attn_ey));  // bvp scaled (PL)
+    const float y = sum_x32(dot16(t.wv, o)) * inv + W[PL::proj_b + f] * exp2i(-(M.attn_ew + M.attn_ey));  // bvp scaled (PL)
     const float x1 = S.xl[f] + y;
     // ln_2 (PL keeps its parameters at the c_fc split's scale 2^mlp_ex: exact powers of two)
     const float sx = exp2i(-M.mlp_ex);
@@ -334,37 +352,36 @@ __device__ inline void dr_tail(Smem& S, const float* P, const float* W, const PT
     const float d1 = x1 - mean;
     const float rs1 = __builtin_amdgcn_rsqf(dr_sum32(d1 * d1) * (1.0f / kE) + 1e-5f);
     const float xn = fmaf(d1 * rs1, W[PL::ln2_g + f] * sx, W[PL::ln2_b + f] * sx);
-    if (hf == 0) S.tl_x[f] = xn;
+    // this half's 16 inputs of xn (features 16 half ..): from the lanes that hold them, via LDS
+    float* xw = &S.tl_x[w][0];
+    if (hf == 0) xw[f] = xn;
     lds_wave_sync();
-    // c_fc: hidden units lane and lane + 64, each over the 32 features (two chains apiece)
+    floatx4 xv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xv[r] = ld4(xw + 16 * hf + 4 * r);
+    // c_fc unit j = 32 w + f over the half's inputs, halves summed; gelu_new
     const float mdown = exp2i(-(M.mlp_ew + M.mlp_ex));  // fc_b, mp_b at the MLP product scale (PL)
-    float h0a = W[PL::fc_b + lane] * mdown, h0b = 0.f, h1a = W[PL::fc_b + 64 + lane] * mdown, h1b = 0.f;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const floatx4 xv = ld4(&S.tl_x[4 * r]);
-#pragma unroll
-        for (int i = 0; i < 4; i += 2) {
-            h0a = fmaf(wf[r][i], xv[i], h0a);
-            h0b = fmaf(wf[r][i + 1], xv[i + 1], h0b);
-            h1a = fmaf(wf[8 + r][i], xv[i], h1a);
-            h1b = fmaf(wf[8 + r][i + 1], xv[i + 1], h1b);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) wm[i] = wm4[i];
-    S.tl_g[lane] = gelu_fast(h0a + h0b);
-    S.tl_g[64 + lane] = gelu_fast(h1a + h1b);
+    const float h = sum_x32(dot16(t.wf, xv)) + W[PL::fc_b + 32 * w + f] * mdown;
+    const float g = gelu_fast(h);
+    float* gw = &S.tl_g[w][0];
+    if (hf == 0) gw[f] = g;
     lds_wave_sync();
-    // mlp.c_proj: this half's 64 hidden units into feature f (four chains), halves summed
-    float m[4] = {0.f, 0.f, 0.f, 0.f};
+    floatx4 gv[4];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const floatx4 gv = ld4(&S.tl_g[64 * hf + 4 * r]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) m[i] = fmaf(wm[r][i], gv[i], m[i]);
-    }
-    const float x2 = x1 + (sum_x32((m[0] + m[1]) + (m[2] + m[3])) + W[PL::mp_b + f] * mdown);
-    // ln_f, head
+    for (int r = 0; r < 4; ++r) gv[r] = ld4(gw + 16 * hf + 4 * r);
+    // mlp.c_proj share of units 32 w + 16 half .. into feature f, halves summed
+    const float ym = sum_x32(dot16(t.wm, gv));
+    if (hf == 0) S.part_y[w][f] = ym;
+    return x1;
+}
+// the tail wave: the four mlp.c_proj shares + bias + residual, ln_f, head -> logits on every lane
+template <class Smem>
+__device__ inline void dr_tail_head(const Smem& S, const float* P, const float* W, const PTop& pt, float x1,
+                                    const ModelView& M, float (&lg)[kDrA]) {
+    const int f = lane_id() & 31;
+    const float mdown = exp2i(-(M.mlp_ew + M.mlp_ex));
+    const float ym = (S.part_y[0][f] + S.part_y[1][f]) + (S.part_y[2][f] + S.part_y[3][f]);
+    const float x2 = x1 + (ym + W[PL::mp_b + f] * mdown);
     const float meanf = dr_sum32(x2) * (1.0f / kE);
     const float d2 = x2 - meanf;
     const float rs2 = __builtin_amdgcn_rsqf(dr_sum32(d2 * d2) * (1.0f / kE) + 1e-5f);
@@ -373,9 +390,10 @@ __device__ inline void dr_tail(Smem& S, const float* P, const float* W, const PT
     for (int a = 0; a < kDrA; ++a) lg[a] = dr_sum32(xf * P[pt.head_w + a * kE + f]) + P[pt.head_b + a];
 }
 
-// The last block's fp32 matrix-vector weights in the lanes' order (dr_tail), after the fragments:
-// [Wvp: lane (f, half) -> Wvp[16 half + i][f], i < 16][c_fc: lane -> W_fc[i][lane], then W_fc[i][lane + 64],
-// i < 32][mlp.c_proj: lane (f, half) -> W_mp[64 half + i][f], i < 64]
+// The last block's fp32 matrix-vector weights in the lanes' order (dr_tail_mlp), after the fragments:
+// [Wvp: lane (f, half) -> Wvp[16 half + i][f], i < 16]
+// [c_fc: wave w, lane (f, half) -> W_fc[16 half + i][32 w + f], i < 16]
+// [mlp.c_proj: wave w, lane (f, half) -> W_mp[32 w + 16 half + i][f], i < 16]
 __global__ void pack_tail_kernel(ModelView M, float* __restrict__ out) {
     const int L = M.n_layer;
     const float* Wl = M.layers + (size_t)(L - 1) * LayerOff::size;
@@ -386,11 +404,11 @@ __global__ void pack_tail_kernel(ModelView M, float* __restrict__ out) {
             const int lane = i / 16, k = i % 16, f = lane & 31, hf = lane >> 5;
             v = Fl[L0Off::Wvp + (16 * hf + k) * kE + f];
         } else if (i < kDrTailMp) {
-            const int o = i - kDrTailFc, lane = o / 64, k = o % 64;
-            v = Wl[LayerOff::fc_w + (k & 31) * kFF + lane + (k >= 32 ? 64 : 0)];
+            const int o = i - kDrTailFc, w = o / 1024, lane = (o / 16) & 63, k = o % 16, f = lane & 31, hf = lane >> 5;
+            v = Wl[LayerOff::fc_w + (16 * hf + k) * kFF + 32 * w + f];
         } else {
-            const int o = i - kDrTailMp, lane = o / 64, k = o % 64, f = lane & 31, hf = lane >> 5;
-            v = Wl[LayerOff::mp_w + (64 * hf + k) * kE + f];
+            const int o = i - kDrTailMp, w = o / 1024, lane = (o / 16) & 63, k = o % 16, f = lane & 31, hf = lane >> 5;
+            v = Wl[LayerOff::mp_w + (32 * w + 16 * hf + k) * kE + f];
         }
         out[i] = v;
     }
@@ -423,6 +441,20 @@ __device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
 #define DPT_DR_OPAQUE 1
 #endif
 #define DR_OPQ(v) asm volatile("" : "+s"(v))
+// one phase over the wave's blocks inside the step: specialised on NBC when it is known at compile
+// time (no-op for 0), else dispatched on the run-time count (DPT_BLOCKS)
+#define DR_BLOCKS(...)                        \
+    do {                                      \
+        if constexpr (NBC >= 0) {             \
+            if constexpr (NBC > 0) {          \
+                constexpr int NB = NBC;       \
+                __VA_ARGS__;                  \
+            }                                 \
+        } else {                              \
+            DPT_BLOCKS(nb, __VA_ARGS__);      \
+        }                                     \
+    } while (0)
+
 
 // kTab: token 0's layer-0 input and LN1 output come from the per-state table (the workspace kernels
 // on grids of <= kMemoStates cells); without it block 0 is re-embedded and normalised every step
@@ -609,310 +641,354 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             const int task = task_s;
             const int T = Tq;
 #endif
-            float x[2][8];
-            float q[2][8];
-            const int sx = S.sx, sy = S.sy;
-            if constexpr (kWs) {
-                // the context tokens' inputs and queries from the episode's workspace; token 0's
-                // input (the new query token) from the per-state table, or block 0 re-embedded
-                const bool col0 = (lane_id() & 15) == 0;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    if (j >= nb) break;
-                    ws_load(l0_cache<NW>(p, task, 1, qb[j]), q[j]);
-                    if constexpr (kTab) {
-                        ws_load(qb[j] == 0 && col0 ? p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 8 * (lane_id() >> 4)
-                                                   : l0_cache<NW>(p, task, 0, qb[j]),
-                                x[j]);
-                    } else {
-                        if (qb[j] == 0) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
-                        else ws_load(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
+            // The window forward of this step, specialised on the wave's block count (2, 1 or 0):
+            // one dispatch per step instead of a branch per phase, so no register copies merge the
+            // two paths' activations after every phase
+            auto forward = [&](auto nb_c) {
+                // NBC = the wave's block count, or -1: taken at run time (each phase dispatches)
+                constexpr int NBC = decltype(nb_c)::value;
+                const int NBR = NBC >= 0 ? NBC : nb;
+                float x[2][8];
+                float q[2][8];
+                const int sx = S.sx, sy = S.sy;
+                if constexpr (kWs) {
+                    // the context tokens' inputs and queries from the episode's workspace; token 0's
+                    // input (the new query token) from the per-state table, or block 0 re-embedded
+                    const bool col0 = (lane_id() & 15) == 0;
+    #pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        if (j >= NBR) break;
+                        ws_load(l0_cache<NW>(p, task, 1, qb[j]), q[j]);
+                        if constexpr (kTab) {
+                            ws_load(qb[j] == 0 && col0 ? p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 8 * (lane_id() >> 4)
+                                                       : l0_cache<NW>(p, task, 0, qb[j]),
+                                    x[j]);
+                        } else {
+                            if (qb[j] == 0) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
+                            else ws_load(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
+                        }
                     }
+                } else {
+    #pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        if (j < NBR) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
                 }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
-            }
 
-            // ---- layer 0: queries of the window (token 0's is never used: it has no
-            // earlier key), the query token's key/value new
-            {
-                if constexpr (!kTab) {
-                    float xn[2][8];
-                    if constexpr (kWs) {
-                        if (own0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
-                    } else {
-                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                                       u_proj3_n<NB>(P, split0, xn, q, M)));
-                    }
-                    if (own0) {  // block 0: key/value (= y) of the query token (the merge below reads them)
-                        const int lane = lane_id();
-                        if ((lane & 15) == 0) {  // token 0's y (folded attention: key = value = y)
-                            const float ydown = exp2i(-M.attn_ey);  // ln_1 returns y x 2^attn_ey (PL)
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) {
-                                const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
-                                S.k0[d] = xn[0][k] * ydown;
-                                S.v0[d] = xn[0][k] * ydown;
+                // ---- layer 0: queries of the window (token 0's is never used: it has no
+                // earlier key), the query token's key/value new
+                {
+                    if constexpr (!kTab) {
+                        float xn[2][8];
+                        if constexpr (kWs) {
+                            if (own0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
+                        } else {
+                            DR_BLOCKS((ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
+                                           u_proj3_n<NB>(P, split0, xn, q, M)));
+                        }
+                        if (own0) {  // block 0: key/value (= y) of the query token (the merge below reads them)
+                            const int lane = lane_id();
+                            if ((lane & 15) == 0) {  // token 0's y (folded attention: key = value = y)
+                                const float ydown = exp2i(-M.attn_ey);  // ln_1 returns y x 2^attn_ey (PL)
+    #pragma unroll
+                                for (int k = 0; k < 8; ++k) {
+                                    const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
+                                    S.k0[d] = xn[0][k] * ydown;
+                                    S.v0[d] = xn[0][k] * ydown;
+                                }
                             }
                         }
+                        bar_lds();
                     }
-                    bar_lds();
-                }
-                DR_STAMP(0);
-                if (nb > 0) {
-                    // merge key 0 into the cached partial of every token column
-                    const int lane = lane_id(), g = lane >> 4;
-                    floatx4 ka, kc, va, vb;
-                    if constexpr (kTab) {
-                        const float* y0 = p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 32 + 8 * g;
-                        ka = ld4(y0);
-                        kc = ld4(y0 + 4);
-                        va = ka;
-                        vb = kc;
-                    } else {
-                        ka = ld4(&S.k0[4 * g]);
-                        kc = ld4(&S.k0[16 + 4 * g]);
-                        va = ld4(&S.v0[4 * g]);
-                        vb = ld4(&S.v0[16 + 4 * g]);
-                    }
-                    float o[2][8];
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        if (j >= nb) break;
-                        const int tok = qb[j] * 16 + (lane & 15);
-                        float sdot = 0.f;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            sdot = fmaf(q[j][r], ka[r], sdot);
-                            sdot = fmaf(q[j][4 + r], kc[r], sdot);
-                        }
-                        sdot = sum_cols(sdot);
-                        // exp2 domain, as attend's m (q is at 2^attn_eq: u_proj3_w)
-                        const float s0 = sdot * ((scale * 1.4426950408889634f) * exp2i(-M.attn_eq));
-                        const float mt = S.l0m[tok], lt = S.l0l[tok];
-                        const float mn = fmaxf(mt, s0);
-                        const float ea = __builtin_amdgcn_exp2f(mt - mn), eb = __builtin_amdgcn_exp2f(s0 - mn);
-                        // 1 / l by v_rcp_f32 (1 ulp, attn_proj3_ol), with c_proj's split scale 2^attn_ey
-                        const float inv = __builtin_amdgcn_rcpf(lt * ea + eb) * exp2i(M.attn_ey);
-                        floatx4 oa, ob;
-                        if constexpr (kWs) {
-                            const float* po = l0_cache<NW>(p, task, 2, qb[j]);
-                            oa = ld4(po);
-                            ob = ld4(po + 4);
+                    DR_STAMP(0);
+                    if (NBR > 0) {
+                        // merge key 0 into the cached partial of every token column
+                        const int lane = lane_id(), g = lane >> 4;
+                        floatx4 ka, kc, va, vb;
+                        if constexpr (kTab) {
+                            const float* y0 = p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 32 + 8 * g;
+                            ka = ld4(y0);
+                            kc = ld4(y0 + 4);
+                            va = ka;
+                            vb = kc;
                         } else {
-                            oa = ld4(&S.l0o[qb[j]][lane][0]);
-                            ob = ld4(&S.l0o[qb[j]][lane][4]);
+                            ka = ld4(&S.k0[4 * g]);
+                            kc = ld4(&S.k0[16 + 4 * g]);
+                            va = ld4(&S.v0[4 * g]);
+                            vb = ld4(&S.v0[16 + 4 * g]);
                         }
-                        // on packed f32 ops (each half rounded as the scalar op)
-                        const floatx2 e2a = {ea, ea}, e2b = {eb, eb}, iv = {inv, inv};
-#pragma unroll
-                        for (int r = 0; r < 4; r += 2) {
-                            const floatx2 t0 = (floatx2{oa[r], oa[r + 1]} * e2a + floatx2{va[r], va[r + 1]} * e2b) * iv;
-                            const floatx2 t1 = (floatx2{ob[r], ob[r + 1]} * e2a + floatx2{vb[r], vb[r + 1]} * e2b) * iv;
-                            o[j][r] = t0.x;
-                            o[j][r + 1] = t0.y;
-                            o[j][4 + r] = t1.x;
-                            o[j][5 + r] = t1.y;
-                        }
-                    }
-                    float xn[2][8];
-                    // o is the attention output x 2^attn_ey already (the merge's inv)
-                    DPT_BLOCKS(nb, (attn_proj3<NB>(P, split0, o, x, M, 1.0f), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
-                                   mlp3_n<NB>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
-                }
-                DR_STAMP(1);
-            }
-
-            for (int layer = 1; layer < L; ++layer) {
-                const bool last = layer == L - 1;
-                auto& kv = S.kv;
-                const float* W = P + layer * PL::size;
-                float q[2][8];
-                {
-                    float xn[2][8];
-                    if (!last) {
-                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                       u_proj_kv3_n<NB>(W, split0.layer(layer), xn, q, kv, qb, M)));
-                    } else {
-                        // the last layer needs q only for token T-1 (block qlast)
-                        DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(kv, qb, xn, M)));
-#pragma unroll
+                        float o[2][8];
+    #pragma unroll
                         for (int j = 0; j < 2; ++j) {
-                            if (j < nb && qb[j] == qlast) {
-                                float xn1[2][8], q1[2][8];
-#pragma unroll
-                                for (int k = 0; k < 8; ++k) xn1[0][k] = xn[j][k];
-                                u_proj3_n<1>(W, split0.layer(layer), xn1, q1, M);
-                                const int lane = lane_id();
-                                if ((lane & 15) == clast) {
-#pragma unroll
-                                    for (int k = 0; k < 8; ++k) {
-                                        const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
-                                        S.ql[d] = q1[0][k];
-                                        S.xl[d] = x[j][k];
+                            if (j >= NBR) break;
+                            const int tok = qb[j] * 16 + (lane & 15);
+                            float sdot = 0.f;
+    #pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                sdot = fmaf(q[j][r], ka[r], sdot);
+                                sdot = fmaf(q[j][4 + r], kc[r], sdot);
+                            }
+                            sdot = sum_cols(sdot);
+                            // exp2 domain, as attend's m (q is at 2^attn_eq: u_proj3_w)
+                            const float s0 = sdot * ((scale * 1.4426950408889634f) * exp2i(-M.attn_eq));
+                            const float mt = S.l0m[tok], lt = S.l0l[tok];
+                            const float mn = fmaxf(mt, s0);
+                            const float ea = __builtin_amdgcn_exp2f(mt - mn), eb = __builtin_amdgcn_exp2f(s0 - mn);
+                            // 1 / l by v_rcp_f32 (1 ulp, attn_proj3_ol), with c_proj's split scale 2^attn_ey
+                            const float inv = __builtin_amdgcn_rcpf(lt * ea + eb) * exp2i(M.attn_ey);
+                            floatx4 oa, ob;
+                            if constexpr (kWs) {
+                                const float* po = l0_cache<NW>(p, task, 2, qb[j]);
+                                oa = ld4(po);
+                                ob = ld4(po + 4);
+                            } else {
+                                oa = ld4(&S.l0o[qb[j]][lane][0]);
+                                ob = ld4(&S.l0o[qb[j]][lane][4]);
+                            }
+                            // on packed f32 ops (each half rounded as the scalar op)
+                            const floatx2 e2a = {ea, ea}, e2b = {eb, eb}, iv = {inv, inv};
+    #pragma unroll
+                            for (int r = 0; r < 4; r += 2) {
+                                const floatx2 t0 = (floatx2{oa[r], oa[r + 1]} * e2a + floatx2{va[r], va[r + 1]} * e2b) * iv;
+                                const floatx2 t1 = (floatx2{ob[r], ob[r + 1]} * e2a + floatx2{vb[r], vb[r + 1]} * e2b) * iv;
+                                o[j][r] = t0.x;
+                                o[j][r + 1] = t0.y;
+                                o[j][4 + r] = t1.x;
+                                o[j][5 + r] = t1.y;
+                            }
+                        }
+                        float xn[2][8];
+                        // o is the attention output x 2^attn_ey already (the merge's inv)
+    #ifndef DPT_DR_SKIP_MLP  // (timing-only diagnostic builds: DPT_DR_SKIP_* leave phases out; results wrong)
+                        DR_BLOCKS((attn_proj3<NB>(P, split0, o, x, M, 1.0f), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                                       mlp3_n<NB>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
+    #else
+                        DR_BLOCKS(attn_proj3<NB>(P, split0, o, x, M, 1.0f));
+    #endif
+                    }
+                    DR_STAMP(1);
+                }
+
+                for (int layer = 1; layer < L; ++layer) {
+                    const bool last = layer == L - 1;
+                    auto& kv = S.kv;
+                    const float* W = P + layer * PL::size;
+                    float q[2][8];
+                    {
+                        float xn[2][8];
+                        if (!last) {
+                            DR_BLOCKS((ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
+                                           u_proj_kv3_n<NB>(W, split0.layer(layer), xn, q, kv, qb, M)));
+                        } else {
+                            // the last layer needs q only for token T-1 (block qlast)
+                            DR_BLOCKS((ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(kv, qb, xn, M)));
+    #pragma unroll
+                            for (int j = 0; j < 2; ++j) {
+                                if (j < NBR && qb[j] == qlast) {
+                                    float xn1[2][8], q1[2][8];
+    #pragma unroll
+                                    for (int k = 0; k < 8; ++k) xn1[0][k] = xn[j][k];
+                                    u_proj3_n<1>(W, split0.layer(layer), xn1, q1, M);
+                                    const int lane = lane_id();
+                                    if ((lane & 15) == clast) {
+    #pragma unroll
+                                        for (int k = 0; k < 8; ++k) {
+                                            const int d = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);
+                                            S.ql[d] = q1[0][k];
+                                            S.xl[d] = x[j][k];
+                                        }
                                     }
                                 }
                             }
                         }
                     }
-                }
-                bar_lds();
-                DR_STAMP(2 * layer);
-                if (last) break;
-                if (nb > 0) {
-                    float o[2][8], l[2];
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        if (j >= nb) break;
-                        float m;
-                        attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, S.diag_bias);
+                    bar_lds();
+                    DR_STAMP(2 * layer);
+                    if (last) break;
+    #ifndef DPT_DR_SKIP_ATTN
+                    if (NBR > 0) {
+                        float o[2][8], l[2];
+    #pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            if (j >= NBR) break;
+                            float m;
+                            attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, S.diag_bias);
+                        }
+                        DR_BLOCKS(attn_proj3_ol<NB>(W, split0.layer(layer), o, l, x, M));
                     }
-                    DPT_BLOCKS(nb, attn_proj3_ol<NB>(W, split0.layer(layer), o, l, x, M));
+    #endif
+                    bar_lds();  // every read of this layer's K/V is done
+                    DR_STAMP(2 * layer + 1);
+    #ifndef DPT_DR_SKIP_MLP
+                    {
+                        float xn[2][8];
+                        DR_BLOCKS((ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b),
+                                       mlp3_n<NB>(W, split0.layer(layer), xn, x, M.mlp_ew, M.mlp_ex)));
+                    }
+    #endif
                 }
-                bar_lds();  // every read of this layer's K/V is done
-                DR_STAMP(2 * layer + 1);
-                {
-                    float xn[2][8];
-                    DPT_BLOCKS(nb, (ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b),
-                                   mlp3_n<NB>(W, split0.layer(layer), xn, x, M.mlp_ew, M.mlp_ex)));
-                }
-            }
 
-            // ---- last layer for the one token T-1, spread over the waves.  Every
-            // column of these MFMAs carries the same token (B operands broadcast).
-            {
-                const float* W = P + (L - 1) * PL::size;
-                const FragSrc3 f3 = split0.layer(L - 1);
-                const auto& kv = S.kv;
-                // the fp32 tail weights of the last block (pack_tail_kernel), read by the tail wave
-                const float* tw = p.frag + (size_t)L * (Frag3::bytes / 4);
-                // (1) the attention as flash partials (m, l, o), in attend's convention (exp2
-                // domain; l and o at 2^kPExp and 2^(attn_ey + kPExp), so o / l is the output at
-                // the c_proj split's scale): with split values key tiles 2 wave and 2 wave + 1
-                // (one pair, both products on mfma_x3), else key tiles wave and wave + NW
-                const int nparts = kSplitV ? (qlast >> 1) + 1 : qlast + 1;
-                // raw score product -> exp2-domain score
-                const float sl = scale * 1.4426950408889634f * exp2i(-(M.attn_ey + M.attn_eq));
-                if constexpr (kSplitV) {
-                    const int lane = lane_id(), g = lane >> 4, c = lane & 15;
-                    const int kb = 2 * wave;
-                    if (kb <= qlast) {
+                // ---- last layer for the one token T-1, spread over the waves.  Every
+                // column of these MFMAs carries the same token (B operands broadcast).
+                {
+                    const float* W = P + (L - 1) * PL::size;
+                    const FragSrc3 f3 = split0.layer(L - 1);
+                    const auto& kv = S.kv;
+                    // the fp32 tail weights of the last block (pack_tail_kernel): each MLP wave's 48 per
+                    // lane, in flight across the attention partials and their barrier
+                    constexpr int kMlpWaves = kFF / 32;
+                    static_assert(kMlpWaves == 4 && NW >= kMlpWaves && kTailWave < kMlpWaves, "four MLP waves");
+                    const float* tw = p.frag + (size_t)L * (Frag3::bytes / 4);
+                    DrTailW tlw;
+                    // (1) the attention as flash partials (m, l, o), in attend's convention (exp2
+                    // domain; l and o at 2^kPExp and 2^(attn_ey + kPExp), so o / l is the output at
+                    // the c_proj split's scale): with split values key tiles 2 wave and 2 wave + 1
+                    // (one pair, both products on mfma_x3), else key tiles wave and wave + NW
+                    const int nparts = kSplitV ? (qlast >> 1) + 1 : qlast + 1;
+                    // raw score product -> exp2-domain score
+                    const float sl = scale * 1.4426950408889634f * exp2i(-(M.attn_ey + M.attn_eq));
+                    if constexpr (kSplitV) {
+                        const int lane = lane_id(), g = lane >> 4, c = lane & 15;
+                        const int kb = 2 * wave;
+                        if (kb <= qlast) {
+                            const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
+                            const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
+                            const Split2 qs = split2(qv, 1.0f);  // the query (x 2^attn_eq), broadcast to every column
+                            float sv[8];
+    #pragma unroll
+                            for (int h = 0; h < 2; ++h) {
+                                const int kt = kb + h;
+                                if (kt > qlast) {
+    #pragma unroll
+                                    for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
+                                    continue;
+                                }
+                                const floatx4 sc = mfma_x3(key_split(kv, kt, lane), qs, floatx4{0.f, 0.f, 0.f, 0.f});
+    #pragma unroll
+                                for (int r = 0; r < 4; ++r) sv[4 * h + r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] : -INFINITY;
+                            }
+                            const float mt = max_cols(fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
+                                                            fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])))) *
+                                             sl;
+                            // P x 2^kPExp <= 2^kPExp (mt is the exact max): fp16 two-part as in attend
+                            const float bm = (float)kPExp - mt;
+                            float pr[8];
+    #pragma unroll
+                            for (int r = 0; r < 8; ++r) pr[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], sl, bm));
+                            float lt = ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
+                            lt = sum_cols(lt);
+                            const Split2 ps = split2(pr, 1.0f);
+                            const int pp = wave;
+                            const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+                            const int vlo = vt_lane_off(lane);
+                            const floatx4 o0 = mfma_x3(vt_split(kv, pp, 0, vlo), ps, zero);
+                            const floatx4 o1 = mfma_x3(vt_split(kv, pp, 1, vlo), ps, zero);
+                            if (c == 0) {
+                                *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
+                                *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;
+                            }
+                            if (lane == 0) {
+                                S.part_m[wave] = mt;
+                                S.part_l[wave] = lt;
+                            }
+                        }
+                    } else {
+                        const int lane = lane_id(), g = lane >> 4, c = lane & 15;
                         const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
-                        const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
-                        const Split2 qs = split2(qv, 1.0f);  // the query (x 2^attn_eq), broadcast to every column
-                        float sv[8];
-#pragma unroll
+    #pragma unroll
                         for (int h = 0; h < 2; ++h) {
-                            const int kt = kb + h;
-                            if (kt > qlast) {
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
-                                continue;
+                            const int kt = wave + NW * h;
+                            if (kt > qlast) break;
+                            // split key tile x the split query, broadcast to every column
+                            const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
+                            const Split2 ks = key_split(kv, kt, lane);
+                            const floatx4 sc = mfma_x3(ks, split2(qv, 1.0f), floatx4{0.f, 0.f, 0.f, 0.f});
+                            float sv[4], mt = -INFINITY;
+    #pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                sv[r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * sl : -INFINITY;
+                                mt = fmaxf(mt, sv[r]);
                             }
-                            const floatx4 sc = mfma_x3(key_split(kv, kt, lane), qs, floatx4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) sv[4 * h + r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] : -INFINITY;
-                        }
-                        const float mt = max_cols(fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
-                                                        fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])))) *
-                                         sl;
-                        // P x 2^kPExp <= 2^kPExp (mt is the exact max): fp16 two-part as in attend
-                        const float bm = (float)kPExp - mt;
-                        float pr[8];
-#pragma unroll
-                        for (int r = 0; r < 8; ++r) pr[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], sl, bm));
-                        float lt = ((pr[0] + pr[1]) + (pr[2] + pr[3])) + ((pr[4] + pr[5]) + (pr[6] + pr[7]));
-                        lt = sum_cols(lt);
-                        const Split2 ps = split2(pr, 1.0f);
-                        const int pp = wave;
-                        const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-                        const int vlo = vt_lane_off(lane);
-                        const floatx4 o0 = mfma_x3(vt_split(kv, pp, 0, vlo), ps, zero);
-                        const floatx4 o1 = mfma_x3(vt_split(kv, pp, 1, vlo), ps, zero);
-                        if (c == 0) {
-                            *reinterpret_cast<floatx4*>(&S.part_o[wave][4 * g]) = o0;
-                            *reinterpret_cast<floatx4*>(&S.part_o[wave][16 + 4 * g]) = o1;
-                        }
-                        if (lane == 0) {
-                            S.part_m[wave] = mt;
-                            S.part_l[wave] = lt;
-                        }
-                    }
-                } else {
-                    const int lane = lane_id(), g = lane >> 4, c = lane & 15;
-                    const floatx4 qa = ld4(&S.ql[4 * g]), qc = ld4(&S.ql[16 + 4 * g]);
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int kt = wave + NW * h;
-                        if (kt > qlast) break;
-                        // split key tile x the split query, broadcast to every column
-                        const float qv[8] = {qa[0], qa[1], qa[2], qa[3], qc[0], qc[1], qc[2], qc[3]};
-                        const Split2 ks = key_split(kv, kt, lane);
-                        const floatx4 sc = mfma_x3(ks, split2(qv, 1.0f), floatx4{0.f, 0.f, 0.f, 0.f});
-                        float sv[4], mt = -INFINITY;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            sv[r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] * sl : -INFINITY;
-                            mt = fmaxf(mt, sv[r]);
-                        }
-                        mt = max_cols(mt);
-                        float pr[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) pr[r] = __builtin_amdgcn_exp2f(sv[r] - mt);
-                        float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
-                        lt = sum_cols(lt) * exp2i(kPExp);
-                        const floatx4 v0 = ld4(&kv.Vt[c][kt * 16 + 4 * g]);
-                        const floatx4 v1 = ld4(&kv.Vt[16 + c][kt * 16 + 4 * g]);
-                        floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) o0 = mfma4(v0[s4], pr[s4], o0);
-#pragma unroll
-                        for (int s4 = 0; s4 < 4; ++s4) o1 = mfma4(v1[s4], pr[s4], o1);
-                        o0 = o0 * exp2i(kPExp);  // the values are y x 2^attn_ey already
-                        o1 = o1 * exp2i(kPExp);
-                        if (c == 0) {
-                            *reinterpret_cast<floatx4*>(&S.part_o[kt][4 * g]) = o0;
-                            *reinterpret_cast<floatx4*>(&S.part_o[kt][16 + 4 * g]) = o1;
-                        }
-                        if (lane == 0) {
-                            S.part_m[kt] = mt;
-                            S.part_l[kt] = lt;
-                        }
-                    }
-                }
-                bar_lds();
-                DR_STAMP(2 * L - 1);
-                // (2) the tail wave: the rest of token T-1's last block (merge, c_proj, ln_2, MLP),
-                // ln_f and the head as fp32 matrix-vector products on the VALU (dr_tail), then
-                // selection and the env step
-                if (wave == kTailWave) {
-                    // the step's serial tail: issue ahead of the other workgroup's waves on this SIMD
-                    DPT_TAIL_PRIO(3);
-                    const int lane = lane_id();
-                    float lg[kDrA];
-                    dr_tail(S, P, W, pt, tw, nparts, M, lg);
-                    DR_STAMP(2 * L + 2);
-                    if (lane == 0) {
-                        float q[kDrA] = {0.f, 0.f, 0.f, 0.f, 0.f};
-                        if (p.sample) cdf_fast<kDrA>(lg, p.temp, q);
-                        if (p.memo) {
-                            const int sidx = sx * p.dim + sy;
-#pragma unroll
-                            for (int k = 0; k < kDrA; ++k) {
-                                S.memo[sidx][S.kMemoLg + k] = lg[k];
-                                S.memo[sidx][k] = q[k];
+                            mt = max_cols(mt);
+                            float pr[4];
+    #pragma unroll
+                            for (int r = 0; r < 4; ++r) pr[r] = __builtin_amdgcn_exp2f(sv[r] - mt);
+                            float lt = (pr[0] + pr[1]) + (pr[2] + pr[3]);
+                            lt = sum_cols(lt) * exp2i(kPExp);
+                            const floatx4 v0 = ld4(&kv.Vt[c][kt * 16 + 4 * g]);
+                            const floatx4 v1 = ld4(&kv.Vt[16 + c][kt * 16 + 4 * g]);
+                            floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+    #pragma unroll
+                            for (int s4 = 0; s4 < 4; ++s4) o0 = mfma4(v0[s4], pr[s4], o0);
+    #pragma unroll
+                            for (int s4 = 0; s4 < 4; ++s4) o1 = mfma4(v1[s4], pr[s4], o1);
+                            o0 = o0 * exp2i(kPExp);  // the values are y x 2^attn_ey already
+                            o1 = o1 * exp2i(kPExp);
+                            if (c == 0) {
+                                *reinterpret_cast<floatx4*>(&S.part_o[kt][4 * g]) = o0;
+                                *reinterpret_cast<floatx4*>(&S.part_o[kt][16 + 4 * g]) = o1;
+                            }
+                            if (lane == 0) {
+                                S.part_m[kt] = mt;
+                                S.part_l[kt] = lt;
                             }
                         }
-                        S.nfwd += 1;
-                        finish_step(lg, q, t, sx, sy, p.sample ? S.u_ep[t] : 0.0);
-                        S.sx = cur_x;
-                        S.sy = cur_y;
                     }
-                    DR_STAMP(2 * L + 3);
-                    DPT_TAIL_PRIO(0);
+                    bar_lds();
+                    DR_STAMP(2 * L - 1);
+                    // (2) the MLP waves: merge, c_proj, ln_2 and a quarter of the MLP of token T-1 as fp32
+                    // matrix-vector products (dr_tail_mlp); (3) after a barrier the tail wave: ln_f, head,
+                    // selection and the env step
+                    float x1 = 0.f;
+                    if (wave < kMlpWaves) {
+                        // the weights here, not before (1): live across the attention partials they push the
+                        // kernel past 256 VGPRs (spills); their latency runs under the merge
+                        dr_tail_ld_early(tw, wave, tlw);
+                        dr_tail_ld_late(tw, wave, tlw);
+    #ifndef DPT_DR_SKIP_TAIL
+                        x1 = dr_tail_mlp(S, W, tlw, wave, nparts, M);
+    #endif
+                    }
+                    bar_lds();
+                    DR_STAMP(2 * L);
+                    if (wave == kTailWave) {
+                        // the step's serial tail: issue ahead of the other workgroup's waves on this SIMD
+                        DPT_TAIL_PRIO(3);
+                        const int lane = lane_id();
+                        float lg[kDrA] = {};
+    #ifndef DPT_DR_SKIP_TAIL
+                        dr_tail_head(S, P, W, pt, x1, M, lg);
+    #endif
+                        DR_STAMP(2 * L + 2);
+                        if (lane == 0) {
+                            float q[kDrA] = {0.f, 0.f, 0.f, 0.f, 0.f};
+                            if (p.sample) cdf_fast<kDrA>(lg, p.temp, q);
+                            if (p.memo) {
+                                const int sidx = sx * p.dim + sy;
+    #pragma unroll
+                                for (int k = 0; k < kDrA; ++k) {
+                                    S.memo[sidx][S.kMemoLg + k] = lg[k];
+                                    S.memo[sidx][k] = q[k];
+                                }
+                            }
+                            S.nfwd += 1;
+                            finish_step(lg, q, t, sx, sy, p.sample ? S.u_ep[t] : 0.0);
+                            S.sx = cur_x;
+                            S.sy = cur_y;
+                        }
+                        DR_STAMP(2 * L + 3);
+                        DPT_TAIL_PRIO(0);
+                    }
                 }
+            };
+            // the workspace kernels (the product path) specialised on the block count; the
+            // workspace-free fallback dispatches per phase (its specialisation computed wrong
+            // logits at 101-token windows: not shipped)
+            if constexpr (kWs) {
+                if (nb == 2) forward(std::integral_constant<int, 2>{});
+                else if (nb == 1) forward(std::integral_constant<int, 1>{});
+                else forward(std::integral_constant<int, 0>{});
+            } else {
+                forward(std::integral_constant<int, -1>{});
             }
             // the end of the step (with the memo, the barrier after the memo-hit chain at the top of
             // the loop would order the state and the partials as well, but dropping this one was
