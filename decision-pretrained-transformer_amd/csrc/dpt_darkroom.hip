@@ -93,6 +93,16 @@ struct DrGeom {
     static constexpr int kWsPerTask = 3 * kBlk * 64 * 8;  // [x | u | layer-0 partial o] per task
 };
 
+// DPT_DR_WG3 (default): the 4-wave workspace kernel at three workgroups per CU (<= 168 VGPRs, and the
+// score product's keys read from the values' token-major rows so that three workgroups' LDS fit the
+// CU: 35.6 KB + the parameter block).  The rollout is latency-bound per workgroup, so a third task
+// per CU is nearly free: config 3 235.8 -> 202.4 ms, bit-identical (A/B in one process per library).
+#ifndef DPT_DR_WG3
+#define DPT_DR_WG3 1
+#endif
+#ifndef DPT_DR_WG3_N
+#define DPT_DR_WG3_N 3
+#endif
 // 16-B multiple: the dynamic parameter block P follows it and is read with 16-B loads.
 // kWs (a per-task workspace is given): the layer-0 partials live in the workspace and
 // the freed LDS holds the values as split pair tiles (P V on mfma_x3);
@@ -102,7 +112,7 @@ struct alignas(16) DrSmem {
     static constexpr int kFwdT = DrGeom<NW>::kT, kFwdBlocks = DrGeom<NW>::kBlk;
     // keys and values of the current layer (the 16-wave geometry reads the keys from the values'
     // rows: 512 tokens of both in LDS)
-    KVBuf<kFwdT, kSplitKeys, kSplitKeys && kWs, kWs && NW == 16> kv;
+    KVBuf<kFwdT, kSplitKeys, kSplitKeys && kWs, kWs && (NW == 16 || (NW == 4 && DPT_DR_WG3))> kv;
     int2 ctx[kFwdT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
     int2 cur[kFwdT];   // this episode's transitions
     // layer-0 episode cache: the causal softmax partial of every token over keys
@@ -459,7 +469,7 @@ __device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
 // kTab: token 0's layer-0 input and LN1 output come from the per-state table (the workspace kernels
 // on grids of <= kMemoStates cells); without it block 0 is re-embedded and normalised every step
 template <bool kWs, int NW, bool kTab = kWs>
-__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1)
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? (kWs && DPT_DR_WG3 ? DPT_DR_WG3_N : 2) : 1)
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     static_assert(kWs || !kTab, "the state table lives in the workspace");
     __shared__ DrSmem<kWs, NW> S;
