@@ -65,7 +65,10 @@ namespace dpt {
 
 constexpr int kDrA = 5;                     // DarkRoom actions
 constexpr int kDrF = 10;                    // token features 2*sd + A + 1
-constexpr int kMemoStates = 128;            // logits memo rows (grids up to 11 x 11)
+#ifndef DPT_DR_MEMO_STATES
+#define DPT_DR_MEMO_STATES 128
+#endif
+constexpr int kMemoStates = DPT_DR_MEMO_STATES;  // logits memo rows (grids up to 11 x 11)
 
 struct PTop {
     int lnf_g, lnf_b, head_w, head_b, emb_b, wpe0, emb_w, total;
@@ -100,6 +103,9 @@ struct DrGeom {
 #ifndef DPT_DR_WG3
 #define DPT_DR_WG3 1
 #endif
+#ifndef DPT_DR_NO_DIAG_BIAS
+#define DPT_DR_NO_DIAG_BIAS 0
+#endif
 #ifndef DPT_DR_WG3_N
 #define DPT_DR_WG3_N 3
 #endif
@@ -117,7 +123,7 @@ struct alignas(16) DrSmem {
     int2 cur[kFwdT];   // this episode's transitions
     // layer-0 episode cache: the causal softmax partial of every token over keys
     // 1..t, unnormalised o^T in C-layout per (block, lane), m and l per token
-    float l0o[kWs ? 1 : kFwdBlocks][64][8];
+    float l0o[kWs ? 0 : kFwdBlocks][64][8];  // (none with the workspace: zero-length, clang extension)
     float l0m[kFwdT], l0l[kFwdT];
     float k0[kE], v0[kE];             // layer 0: key / value of the query token
     float ql[kE], xl[kE];             // last layer: q and residual of token T-1
@@ -135,7 +141,9 @@ struct alignas(16) DrSmem {
     static_assert(kMemoLg >= kDrA && kMemoLg + kDrA <= kMemoRow, "memo row layout");
     alignas(16) float memo[kMemoStates][kMemoRow];
     double u_ep[kFwdT];                // this episode's selection uniforms, one per step
+#if !DPT_DR_NO_DIAG_BIAS
     alignas(16) float diag_bias[64 * 4];  // the diagonal score tile's causal mask (diag_bias_init)
+#endif
     int sx, sy, nfwd, tnext;
 };
 
@@ -500,7 +508,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         for (int i = tid; i < (int)(sizeof(S.kv.VT) / 16); i += blockDim.x) vs[i] = uint4{0u, 0u, 0u, 0u};
     }
     for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
+#if !DPT_DR_NO_DIAG_BIAS
     diag_bias_init(S.diag_bias, tid, blockDim.x);
+    const float* diag_bias = S.diag_bias;
+#else
+    const float* diag_bias = nullptr;
+#endif
 
     // the task's goal and action permutation, once (wave-uniform: scalar registers), not
     // reloaded from memory on thread 0's serial select chain every step
@@ -514,10 +527,12 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         const int nctx = min(ep, p.R) * p.horizon;
         const int T = 1 + nctx;
         const int nqb = (T + 15) >> 4;
-        const int qlast = (T - 1) >> 4, clast = (T - 1) & 15;
         int qb[2];
         const int nb = assign_blocks<NW>(wave, nqb, qb);
+#if !DPT_DR_OPAQUE
+        const int qlast = (T - 1) >> 4, clast = (T - 1) & 15;
         const bool own0 = nb > 0 && qb[0] == 0;
+#endif
         if (tid == 0) {
             S.sx = 0;
             S.sy = 0;
@@ -561,7 +576,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             for (int j = 0; j < 2; ++j) {
                 if (j >= nb) break;
                 float m, l, o[8];
-                attend(S.kv, q[j], qb[j], 1, scale, m, l, o, M, S.diag_bias);
+                attend(S.kv, q[j], qb[j], 1, scale, m, l, o, M, diag_bias);
                 // the partial at its true scale (attend's o, l carry 2^(attn_ey + kPExp), 2^kPExp)
                 l *= exp2i(-kPExp);
                 const float down = exp2i(-(M.attn_ey + kPExp));
@@ -821,7 +836,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         for (int j = 0; j < 2; ++j) {
                             if (j >= NBR) break;
                             float m;
-                            attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, S.diag_bias);
+                            attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, diag_bias);
                         }
                         DR_BLOCKS(attn_proj3_ol<NB>(W, split0.layer(layer), o, l, x, M));
                     }
@@ -841,7 +856,6 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 // column of these MFMAs carries the same token (B operands broadcast).
                 {
                     const float* W = P + (L - 1) * PL::size;
-                    const FragSrc3 f3 = split0.layer(L - 1);
                     const auto& kv = S.kv;
                     // the fp32 tail weights of the last block (pack_tail_kernel): each MLP wave's 48 per
                     // lane, in flight across the attention partials and their barrier

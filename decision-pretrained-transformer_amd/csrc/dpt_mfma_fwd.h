@@ -20,9 +20,10 @@ constexpr int kVStride = kFwdT + 4;          // Vt[feature][token] (128-token bu
 
 // Small parameters copied to LDS once per launch (offsets in floats): per block
 // [ln1_g ln1_b attn_b proj_b ln2_g ln2_b fc_b mp_b], then the model-level ones.
+// (attn_b holds only the folded attention's g0: the unfolded c_attn bias had 3E entries)
 struct PL {
-    static constexpr int ln1_g = 0, ln1_b = 32, attn_b = 64, proj_b = 160, ln2_g = 192, ln2_b = 224,
-                         fc_b = 256, mp_b = 384, size = 416;
+    static constexpr int ln1_g = 0, ln1_b = 32, attn_b = 64, proj_b = 96, ln2_g = 128, ln2_b = 160,
+                         fc_b = 192, mp_b = 320, size = 352;
 };
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 // This workgroup's keys and values of the current layer, for windows of up to TMAX
