@@ -555,18 +555,20 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         }
         __syncthreads();
 
-        // layer-0 episode cache: causal partial over keys 1..t of every token
-        {
+        // layer-0 episode cache: causal partial over keys 1..t of every token (specialised on the
+        // wave's block count in the workspace kernels, as the step's forward below)
+        auto prologue = [&](auto nb_c) {
+            constexpr int NBC = decltype(nb_c)::value;
+            const int NBR = NBC >= 0 ? NBC : nb;
             float x[2][8], xn[2][8], q[2][8];
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                if (j < nb) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
-            DPT_BLOCKS(nb, (ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                           u_proj_kv3_n<NB>(P, split0, xn, q, S.kv, qb, M)));
+                if (j < NBR) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
+            DR_BLOCKS((ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b), u_proj_kv3_n<NB>(P, split0, xn, q, S.kv, qb, M)));
             if constexpr (kWs) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    if (j >= nb) break;
+                    if (j >= NBR) break;
                     ws_store(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
                     ws_store(l0_cache<NW>(p, task, 1, qb[j]), q[j]);
                 }
@@ -574,7 +576,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             bar_lds();
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                if (j >= nb) break;
+                if (j >= NBR) break;
                 float m, l, o[8];
                 attend(S.kv, q[j], qb[j], 1, scale, m, l, o, M, diag_bias);
                 // the partial at its true scale (attend's o, l carry 2^(attn_ey + kPExp), 2^kPExp)
@@ -595,6 +597,13 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 }
             }
             __syncthreads();
+        };
+        if constexpr (kWs) {
+            if (nb == 2) prologue(std::integral_constant<int, 2>{});
+            else if (nb == 1) prologue(std::integral_constant<int, 1>{});
+            else prologue(std::integral_constant<int, 0>{});
+        } else {
+            prologue(std::integral_constant<int, -1>{});
         }
 
         // the policy's logits are a pure function of (window, query state) and the
