@@ -103,6 +103,9 @@ struct DrGeom {
 #ifndef DPT_DR_WG3
 #define DPT_DR_WG3 1
 #endif
+#ifndef DPT_DR_NW8_2
+#define DPT_DR_NW8_2 1
+#endif
 #ifndef DPT_DR_NO_DIAG_BIAS
 #define DPT_DR_NO_DIAG_BIAS 0
 #endif
@@ -118,7 +121,7 @@ struct alignas(16) DrSmem {
     static constexpr int kFwdT = DrGeom<NW>::kT, kFwdBlocks = DrGeom<NW>::kBlk;
     // keys and values of the current layer (the 16-wave geometry reads the keys from the values'
     // rows: 512 tokens of both in LDS)
-    KVBuf<kFwdT, kSplitKeys, kSplitKeys && kWs, kWs && (NW == 16 || (NW == 4 && DPT_DR_WG3))> kv;
+    KVBuf<kFwdT, kSplitKeys, kSplitKeys && kWs, kWs && (NW == 16 || (NW == 4 && DPT_DR_WG3) || (NW == 8 && DPT_DR_NW8_2))> kv;
     int2 ctx[kFwdT];   // context transitions, oldest first: .x = x|y<<8|a<<16|r<<24, .y = nx|ny<<8
     int2 cur[kFwdT];   // this episode's transitions
     // layer-0 episode cache: the causal softmax partial of every token over keys
@@ -477,7 +480,7 @@ __device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
 // kTab: token 0's layer-0 input and LN1 output come from the per-state table (the workspace kernels
 // on grids of <= kMemoStates cells); without it block 0 is re-embedded and normalised every step
 template <bool kWs, int NW, bool kTab = kWs>
-__global__ void __launch_bounds__(NW * 64, NW == 4 ? (kWs && DPT_DR_WG3 ? DPT_DR_WG3_N : 2) : 1)
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? (kWs && DPT_DR_WG3 ? DPT_DR_WG3_N : 2) : (NW == 8 && kWs && DPT_DR_NW8_2 ? 4 : 1))
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     static_assert(kWs || !kTab, "the state table lives in the workspace");
     __shared__ DrSmem<kWs, NW> S;

@@ -40,14 +40,16 @@ def child(lib):
     if ":" in lib:  # "libX.so:<bytes>": the same library at another DPT_TUNE_CACHE_BUDGET
         dpt_hip.set_cache_budget(int(lib.split(":")[1]))
     if os.environ.get("AB_WL") == "darkroom":  # config 3: 4096 tasks x 40 episodes x 100 steps
-        sd, _ = bench.synthetic_state_dict(4, 2, 5, 100)
-        m = dpt_hip.DeviceModel(sd, 4, 2, 5, 404)
+        # AB_DR_R: context episodes (window 1 + 100 R; 1 = config 3)
+        R = int(os.environ.get("AB_DR_R", "1"))
+        sd, _ = bench.synthetic_state_dict(4, 2, 5, 100 * R)
+        m = dpt_hip.DeviceModel(sd, 4, 2, 5, 4 * (1 + 100 * R))
         goals = np.stack(np.unravel_index(np.arange(N) % 100, (10, 10)), 1)
         ts = []
         for rnd in range(3):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            out = m.rollout_darkroom(goals, 40, 100, 1, seed=rnd)
+            out = m.rollout_darkroom(goals, 40, 100, R, seed=rnd)
             b.record()
             torch.cuda.synchronize()
             if rnd > 0:
@@ -56,7 +58,7 @@ def child(lib):
         digest = None
         if os.environ.get("AB_DIGEST", "1") == "1":
             import hashlib
-            o = m.rollout_darkroom(goals[:512], 6, 100, 1, seed=77, want_actions=True, want_logits=True)
+            o = m.rollout_darkroom(goals[:512], 6, 100, R, seed=77, want_actions=True, want_logits=True)
             h = hashlib.sha1(o["actions"].cpu().numpy().tobytes())
             h.update(o["logits"].cpu().numpy().tobytes())
             digest = h.hexdigest()[:16]
