@@ -310,6 +310,12 @@ __device__ inline int select_fixed_fast(const float (&lg)[NA], int sample, float
 struct TrDims {
     int L, E, F, A, B, T, npos;
     int fwd_only;  // DPT_TRAIN_FORWARD_ONLY: inference workspace (nothing saved for a backward)
+    // dropout (dpt_hip.h dpt_train_desc): element kept iff its Philox word >= drop_thr, then
+    // scaled by drop_scale; drop_thr == 0: no dropout
+    uint32_t drop_thr;
+    float drop_scale;
+    uint64_t drop_seed;
+    __host__ __device__ bool drop() const { return drop_thr != 0; }
     __host__ __device__ int R() const { return B * T; }
     __host__ __device__ int64_t layer_size() const { return 12ll * E * E + 13ll * E; }
 };

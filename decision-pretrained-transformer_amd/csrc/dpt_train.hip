@@ -145,6 +145,25 @@ __global__ void tr_embed(const float* __restrict__ tok, const float* __restrict_
     x[i] = acc + blob[b.wpe + (int64_t)t * d.E + e];
 }
 
+// dropout factor of element e of a site (dpt_hip.h dpt_train_desc): drop_scale when the element's
+// Philox word clears the threshold, else 0.  Regenerated in the backward -- no mask is stored.
+__device__ inline float tr_keep(const TrDims& d, int site, int64_t e) {
+    const U4 r = philox(d.drop_seed, (uint64_t)site, e >> 2, DPT_STREAM_DROPOUT);
+    const int k = (int)(e & 3);
+    const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : k == 2 ? r.z : r.w;
+    return w >= d.drop_thr ? d.drop_scale : 0.0f;
+}
+
+// out[i] = (add ? add[i] : 0) + x[i] keep(site, i) over n elements: the dropout of the embedding
+// (in place), the residual adds x + drop(y) after c_proj / mlp.c_proj, and the gradients through them
+__global__ void tr_dropout(const float* __restrict__ x, const float* __restrict__ add, int64_t n, TrDims d, int site,
+                           float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = x[i] * tr_keep(d, site, i);
+    out[i] = add ? add[i] + v : v;
+}
+
 // LayerNorm over E (eps 1e-5), one wave per row; saves (mean, rstd)
 __global__ void tr_layernorm(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ bb,
                              int R, int E, float* __restrict__ y, float* __restrict__ st) {
@@ -177,8 +196,10 @@ __global__ void tr_linear(const float* __restrict__ X, const float* __restrict__
 }
 
 // causal single-head attention, one wave per (task, query t): P[b][t][j] = softmax_j(q_t k_j / sqrt(E)),
-// j <= t, and o_t = sum_j P[b][t][j] v_j.  qkv rows [q | k | v] (c_attn output).
-__global__ void tr_attn_fwd(const float* __restrict__ qkv, TrDims d, float* __restrict__ P, float* __restrict__ O) {
+// j <= t, and o_t = sum_j P[b][t][j] keep(site, (b T + t) T + j) v_j (site < 0: no dropout; P is
+// saved undropped).  qkv rows [q | k | v] (c_attn output).
+__global__ void tr_attn_fwd(const float* __restrict__ qkv, TrDims d, int site, float* __restrict__ P,
+                            float* __restrict__ O) {
     extern __shared__ float sm[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * (blockDim.x / 64) + wave;
@@ -208,9 +229,10 @@ __global__ void tr_attn_fwd(const float* __restrict__ qkv, TrDims d, float* __re
     }
     const float inv = 1.0f / wave_sum(l);
     float* prow = P ? P + ((int64_t)b * T + t) * T : nullptr;  // saved for the backward unless forward-only
+    const int64_t mrow = ((int64_t)b * T + t) * T;
     for (int j = lane; j <= t; j += 64) {
         const float p = pr[j] * inv;
-        pr[j] = p;
+        pr[j] = site >= 0 ? p * tr_keep(d, site, mrow + j) : p;
         if (prow) prow[j] = p;
     }
     wave_lds_sync();
@@ -341,9 +363,10 @@ __global__ void tr_ln_param_part(const float* __restrict__ x, const float* __res
 }
 
 // attention backward, one wave per (task, query t): D_t = sum_e dO_t O_t,
-// dS[b][t][j] = P[b][t][j] (dO_t . v_j - D_t) for j <= t
+// dS[b][t][j] = P[b][t][j] (keep_tj dO_t . v_j - D_t) for j <= t (keep = 1 when site < 0; D_t stays
+// dO_t . O_t since O was formed from the dropped probabilities)
 __global__ void tr_attn_bwd_ds(const float* __restrict__ qkv, const float* __restrict__ P,
-                               const float* __restrict__ O, const float* __restrict__ dO, TrDims d,
+                               const float* __restrict__ O, const float* __restrict__ dO, TrDims d, int site,
                                float* __restrict__ dS) {
     extern __shared__ float sm[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -365,6 +388,7 @@ __global__ void tr_attn_bwd_ds(const float* __restrict__ qkv, const float* __res
         const float* v = base + (int64_t)j * 3 * E + 2 * E;
         float dp = 0.f;
         for (int e = 0; e < E; ++e) dp = fmaf(go[e], v[e], dp);
+        if (site >= 0) dp *= tr_keep(d, site, ((int64_t)b * T + t) * T + j);
         dS[pr + j] = P[pr + j] * (dp - dd);
     }
 }
@@ -382,9 +406,9 @@ __global__ void tr_attn_bwd_dq(const float* __restrict__ qkv, const float* __res
     dqkv[(int64_t)row * 3 * E + e] = acc / sqrtf((float)E);
 }
 
-// dk_j = sum_{t >= j} dS[t][j] q_t / sqrt(E), dv_j = sum_{t >= j} P[t][j] dO_t into dqkv[r][E:3E]
+// dk_j = sum_{t >= j} dS[t][j] q_t / sqrt(E), dv_j = sum_{t >= j} P[t][j] keep_tj dO_t into dqkv[r][E:3E]
 __global__ void tr_attn_bwd_dkv(const float* __restrict__ qkv, const float* __restrict__ P,
-                                const float* __restrict__ dS, const float* __restrict__ dO, TrDims d,
+                                const float* __restrict__ dS, const float* __restrict__ dO, TrDims d, int site,
                                 float* __restrict__ dqkv) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)d.R() * d.E) return;
@@ -395,7 +419,8 @@ __global__ void tr_attn_bwd_dkv(const float* __restrict__ qkv, const float* __re
     float ak = 0.f, av = 0.f;
     for (int t = j; t < T; ++t) {
         ak = fmaf(dS[col + (int64_t)t * T], q[(int64_t)t * 3 * E], ak);
-        av = fmaf(P[col + (int64_t)t * T], go[(int64_t)t * E], av);
+        const float pt = P[col + (int64_t)t * T];
+        av = fmaf(site >= 0 ? pt * tr_keep(d, site, ((int64_t)b * T + t) * T + j) : pt, go[(int64_t)t * E], av);
     }
     dqkv[(int64_t)row * 3 * E + E + e] = ak / sqrtf((float)E);
     dqkv[(int64_t)row * 3 * E + 2 * E + e] = av;
@@ -892,12 +917,18 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
     const int64_t RE = (int64_t)R * E, TT = (int64_t)d.B * d.T * TrWs::tpad(d.T);
     const int rows_per_block = kTrThreads / 64;
     const size_t attn_lds = sizeof(float) * rows_per_block * (size_t)(d.T + E);
-    if (!mm_fast(E) && attn_lds > 160 * 1024) {
+    if ((!mm_fast(E) || d.drop()) && attn_lds > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "train forward: window T=%d too long for the attention kernel", d.T);
         return DPT_EUNSUPPORTED;
     }
     if (attn_lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)tr_attn_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)attn_lds);
     hipLaunchKernelGGL(tr_embed, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, tok, blob, d, B, ws + W.x);
+    // dropout (GPT2Model in training mode): drop(x0) in place, the attention probabilities, and
+    // c_proj / mlp.c_proj outputs before their residual adds -- on the row kernels, which take the
+    // masks (the matrix-core forms fuse the residual add)
+    const bool drop = d.drop();
+    if (drop) hipLaunchKernelGGL(tr_dropout, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, ws + W.x, nullptr, RE, d, 0,
+                                 ws + W.x);
     // slot of layer l's arrays: l, or 0 (x: l & 1) in the forward-only workspace
     auto xs = [&](int l) -> int64_t { return d.fwd_only ? (l & 1) : l; };
     for (int l = 0; l < d.L; ++l) {
@@ -916,7 +947,7 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
         float* xn = ws + W.x + xs(l + 1) * RE;
         hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x,
                            blob + P.ln1_g, blob + P.ln1_b, R, E, y1, st1);
-        const bool fast = mm_fast(E);
+        const bool fast = mm_fast(E) && !drop;
         if (fast)
             mm(E, kMmQkv, y1, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, R, qkv, st);
         else
@@ -926,12 +957,14 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
             attn_fwd_fast(E, qkv, d, Pm, o, st);
         else
             hipLaunchKernelGGL(tr_attn_fwd, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), attn_lds,
-                               st, qkv, d, Pm, o);
+                               st, qkv, d, drop ? 1 + 3 * l : -1, Pm, o);
         if (fast)
             mm(E, kMmProj, o, blob + P.proj_w, blob + P.proj_b, x, nullptr, R, x2, st);
         else
             hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, o, blob + P.proj_w,
-                               blob + P.proj_b, x, R, E, E, 0, x2);
+                               blob + P.proj_b, drop ? nullptr : x, R, E, E, 0, x2);
+        if (drop)  // x2 = x + drop(o W_proj + b_proj)
+            hipLaunchKernelGGL(tr_dropout, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, x2, x, RE, d, 2 + 3 * l, x2);
         hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x2,
                            blob + P.ln2_g, blob + P.ln2_b, R, E, y2, st2);
         if (fast) {
@@ -941,7 +974,10 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
             hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, y2, blob + P.fc_w,
                                blob + P.fc_b, nullptr, R, E, 4 * E, 0, hpre);
             hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, hpre, blob + P.mp_w,
-                               blob + P.mp_b, x2, R, 4 * E, E, 1, xn);
+                               blob + P.mp_b, drop ? nullptr : x2, R, 4 * E, E, 1, xn);
+            if (drop)  // x_{l+1} = x2 + drop(gelu(hpre) W_mp + b_mp)
+                hipLaunchKernelGGL(tr_dropout, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, xn, x2, RE, d, 3 + 3 * l,
+                                   xn);
         }
         if (int rc = launched("train forward layer")) return rc;
     }
@@ -976,6 +1012,7 @@ int train_backward(const TrDims& d, const float* blob, const float* tok, float* 
     hipLaunchKernelGGL(tr_layernorm_bwd, dim3(row_blocks), dim3(kTrThreads), 0, st, ws + W.x + d.L * RE, ws + W.stf,
                        blob + B.lnf_g, dy, R, E, nullptr, dx);
     const size_t ds_lds = sizeof(float) * rows_per_block * (size_t)E;
+    const bool drop = d.drop();
     for (int l = d.L - 1; l >= 0; --l) {
         const TrLayer P = TrLayer::make(B.layers + l * d.layer_size(), E);
         const TrLayer G = TrLayer::make(B.layers + l * d.layer_size(), E);  // same offsets in dblob
@@ -993,16 +1030,23 @@ int train_backward(const TrDims& d, const float* blob, const float* tok, float* 
         float* dqkv = ws + W.dqkv;
         float* dout = ws + W.dout;
         float* dS = ws + W.dS;
-        const bool fast = mm_fast(E);
-        // MLP: x_{l+1} = x2 + gelu(hpre) W_mp + b_mp, hpre = y2 W_fc + b_fc
+        const bool fast = mm_fast(E) && !drop;
+        // MLP: x_{l+1} = x2 + drop(gelu(hpre) W_mp + b_mp), hpre = y2 W_fc + b_fc; with dropout the
+        // product's gradient dx keep (into dy, free until the LayerNorm input gradient below)
+        const float* dmp = dx;
+        if (drop) {
+            hipLaunchKernelGGL(tr_dropout, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dx, nullptr, RE, d, 3 + 3 * l,
+                               dy);
+            dmp = dy;
+        }
         if (fast) {
             if (int rc = wgrad_fast(E, kMmMp, hpre, dx, R, 4 * E, E, part, dblob + G.mp_w, dblob + G.mp_b, st)) return rc;
             mm(E, kMmBdMp, dx, blob + P.mp_w, nullptr, nullptr, hpre, R, dh, st);
             if (int rc = wgrad_fast(E, kMmFc, y2, dh, R, E, 4 * E, part, dblob + G.fc_w, dblob + G.fc_b, st)) return rc;
             mm(E, kMmBdFc, dh, blob + P.fc_w, nullptr, nullptr, nullptr, R, dy, st);
         } else {
-            if (int rc = wgrad(hpre, dx, R, 4 * E, E, 1, part, dblob + G.mp_w, dblob + G.mp_b, st)) return rc;
-            hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, dx, blob + P.mp_w,
+            if (int rc = wgrad(hpre, dmp, R, 4 * E, E, 1, part, dblob + G.mp_w, dblob + G.mp_b, st)) return rc;
+            hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE * 4)), dim3(kTrThreads), 0, st, dmp, blob + P.mp_w,
                                R, 4 * E, E, hpre, nullptr, dh);
             if (int rc = wgrad(y2, dh, R, E, 4 * E, 0, part, dblob + G.fc_w, dblob + G.fc_b, st)) return rc;
             hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dh, blob + P.fc_w, R,
@@ -1011,21 +1055,29 @@ int train_backward(const TrDims& d, const float* blob, const float* tok, float* 
         if (int rc = ln_param_grad(x2, st2, dy, R, E, part, dblob + G.ln2_g, dblob + G.ln2_b, st)) return rc;
         hipLaunchKernelGGL(tr_layernorm_bwd, dim3(row_blocks), dim3(kTrThreads), 0, st, x2, st2, blob + P.ln2_g, dy, R, E,
                            dx, dx2);
-        // attention: x2 = x + o W_proj + b_proj
+        // attention: x2 = x + drop(o W_proj + b_proj)
+        const float* dpj = dx2;
+        if (drop) {
+            hipLaunchKernelGGL(tr_dropout, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dx2, nullptr, RE, d, 2 + 3 * l,
+                               dy);
+            dpj = dy;
+        }
         if (fast) {
             if (int rc = wgrad_fast(E, kMmProj, o, dx2, R, E, E, part, dblob + G.proj_w, dblob + G.proj_b, st)) return rc;
             mm(E, kMmBdProj, dx2, blob + P.proj_w, nullptr, nullptr, nullptr, R, dout, st);
         } else {
-            if (int rc = wgrad(o, dx2, R, E, E, 0, part, dblob + G.proj_w, dblob + G.proj_b, st)) return rc;
-            hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dx2, blob + P.proj_w,
+            if (int rc = wgrad(o, dpj, R, E, E, 0, part, dblob + G.proj_w, dblob + G.proj_b, st)) return rc;
+            hipLaunchKernelGGL(tr_linear_bwd_data, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dpj, blob + P.proj_w,
                                R, E, E, nullptr, nullptr, dout);
         }
         if (fast) {
             attn_bwd_fast(E, qkv, Pm, o, dout, d, dS, dqkv, st);
         } else {
-            hipLaunchKernelGGL(tr_attn_bwd_ds, dim3(row_blocks), dim3(kTrThreads), ds_lds, st, qkv, Pm, o, dout, d, dS);
+            const int site = drop ? 1 + 3 * l : -1;
+            hipLaunchKernelGGL(tr_attn_bwd_ds, dim3(row_blocks), dim3(kTrThreads), ds_lds, st, qkv, Pm, o, dout, d, site,
+                               dS);
             hipLaunchKernelGGL(tr_attn_bwd_dq, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, dS, d, dqkv);
-            hipLaunchKernelGGL(tr_attn_bwd_dkv, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, Pm, dS, dout, d,
+            hipLaunchKernelGGL(tr_attn_bwd_dkv, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, qkv, Pm, dS, dout, d, site,
                                dqkv);
         }
         if (fast) {
@@ -1042,7 +1094,8 @@ int train_backward(const TrDims& d, const float* blob, const float* tok, float* 
                            dx2, dx);
         if (int rc = launched("train backward layer")) return rc;
     }
-    // embedding: x0 = tok emb_w + emb_b + wpe[t]
+    // embedding: x0 = drop(tok emb_w + emb_b + wpe[t])
+    if (drop) hipLaunchKernelGGL(tr_dropout, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, dx, nullptr, RE, d, 0, dx);
     if (int rc = wgrad(tok, dx, R, d.F, E, 0, part, dblob + B.emb_w, dblob + B.emb_b, st)) return rc;
     hipLaunchKernelGGL(tr_wpe_grad, dim3(blocks_for((int64_t)d.T * E)), dim3(kTrThreads), 0, st, dx, d, dblob + B.wpe);
     return launched("train backward embed");

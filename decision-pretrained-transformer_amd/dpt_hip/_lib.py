@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DPT_HIP_LIB: another build's file name in this directory (A/B runs of kernel variants)
 LIB_PATH = os.path.join(_HERE, os.environ.get("DPT_HIP_LIB", "libdpt_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 DPT_OK = 0
 DPT_EINVAL = -1
@@ -28,6 +28,7 @@ BANDIT_F32 = 16
 STREAM_SELECT = 0
 STREAM_REWARD = 1
 STREAM_ROLLIN = 2
+STREAM_DROPOUT = 3  # training dropout masks (dpt_train_desc)
 STREAM_POLICY = 16  # + arm index (baseline-policy draws)
 
 _c_void_p = ctypes.c_void_p
@@ -179,7 +180,8 @@ SIGNATURES["dpt_darkroom_workspace_numel_window"] = (_i32, [_i32, _i32, ctypes.P
 
 class TrainDesc(ctypes.Structure):
     _fields_ = [("n_layer", _i32), ("n_embd", _i32), ("state_dim", _i32), ("action_dim", _i32),
-                ("n_positions", _i32), ("batch", _i32), ("window", _i32), ("reserved", _i32)]
+                ("n_positions", _i32), ("batch", _i32), ("window", _i32), ("reserved", _i32),
+                ("dropout", ctypes.c_float), ("reserved2", _i32), ("dropout_seed", ctypes.c_uint64)]
 
 
 TRAIN_FORWARD_ONLY = 1  # dpt_train_desc.reserved flag (DPT_TRAIN_FORWARD_ONLY)

@@ -155,8 +155,11 @@ class Transformer(nn.Module):
         from dpt_hip import train as tr
         tok = self._tokens(x)
         grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        p, seed = 0.0, 0
+        if self.training and self.dropout > 0:  # fresh masks per call, from torch's (seedable) CPU generator
+            p, seed = float(self.dropout), int(torch.randint(0, 2 ** 62, (1,)).item())
         dims = (self.n_layer, self.n_embd, self.state_dim, self.action_dim, self.n_positions, tok.shape[0],
-                tok.shape[1], 0 if grad else tr.FORWARD_ONLY)
+                tok.shape[1], 0 if grad else tr.FORWARD_ONLY, p, seed)
         preds = tr.TransformerFunction.apply(tok, dims, *tr.param_list(self))
         return preds[:, -1, :] if self.test else preds[:, 1:, :]
 
@@ -172,13 +175,12 @@ class Transformer(nn.Module):
         takes the fused kernels at width 32 and the generic kernels at other widths.
 
         Dropout: the reference's GPT2Config applies embd/attn/resid dropout with p = ``dropout``
-        (models/net.py:30-32) in training mode; the HIP kernels have no dropout, so a
-        training-mode forward with ``dropout > 0`` raises instead of silently skipping it
-        (``dropout = 0``, the common_args.py default, and eval mode are exact)."""
-        if self.training and self.dropout > 0:
-            raise NotImplementedError(f"dropout={self.dropout} in training mode: the HIP training kernels "
-                                      "implement dropout 0 only (set --dropout 0 or call model.eval())")
-        if (self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())) \
+        (models/net.py:30-32) in training mode -- with or without grad (train.py:265-278's test
+        loss runs in training mode).  Such calls take the training kernels with dropout: masks
+        from Philox keyed by a seed drawn from torch's CPU generator per call (include/dpt_hip.h
+        dpt_train_desc), the same distribution as torch's dropout, not its random stream."""
+        if (self.training and (self.dropout > 0 or (torch.is_grad_enabled()
+                                                    and any(p.requires_grad for p in self.parameters())))) \
                 or self.n_embd != dpt_hip.E:
             return self._forward_generic(x)
         dm = self.device_model()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 5
+#define DPT_ABI_VERSION 6
 
 /* error codes (mapped to the reference's Python exceptions by dpt_hip/_lib.py) */
 #define DPT_OK 0
@@ -58,6 +58,7 @@ extern "C" {
 #define DPT_STREAM_SELECT 0
 #define DPT_STREAM_REWARD 1
 #define DPT_STREAM_ROLLIN 2
+#define DPT_STREAM_DROPOUT 3 /* training dropout masks: counter (site, element / 4), word element % 4 */
 #define DPT_STREAM_POLICY 16 /* + arm index: baseline-policy draws (Thompson posterior samples) */
 
 int dpt_abi_version(void);
@@ -395,7 +396,18 @@ typedef struct dpt_train_desc {
     int32_t n_layer, n_embd, state_dim, action_dim, n_positions;
     int32_t batch, window;        /* sequences and tokens per sequence (1 + context length) */
     int32_t reserved;             /* flags: DPT_TRAIN_FORWARD_ONLY or 0 */
+    float dropout;                /* GPT2Config embd/attn/resid_pdrop (net.py:30-32), 0 <= p < 1 */
+    int32_t reserved2;            /* 0 */
+    uint64_t dropout_seed;        /* Philox key of this forward's masks (a fresh one per step) */
 } dpt_train_desc;
+/* Dropout (GPT2Model in training mode, p = dropout > 0): element e of a site is kept iff
+ * word_e >= thr, thr = min(ceil(p 2^32), 2^32 - 1), word_e = component e % 4 of
+ * Philox(dropout_seed, (site, e / 4, DPT_STREAM_DROPOUT)), and kept elements are scaled by
+ * float(1 / (1 - p)).  Sites: 0 = the embedding sum x0 (B, T, E); per layer l, 1 + 3 l = the
+ * attention probabilities (B, T, T) [element (b t + i) T + j], 2 + 3 l = c_proj's output,
+ * 3 + 3 l = mlp.c_proj's output (B, T, E), each dropped before its residual add.  The backward
+ * regenerates the same masks from the desc: pass the forward's desc unchanged.  p > 0 runs the
+ * row kernels (no matrix-core forms).                                                       */
 /* Inference through the training forward (no backward will follow): the workspace holds one
  * layer's activations and no attention probabilities or backward scratch
  * (dpt_train_workspace_numel sizes it by the flag); dpt_train_backward rejects the desc. */

@@ -529,6 +529,94 @@ def train_grads():
     print("train grads")
 
 
+def train_dropout():
+    """train.py:286-331 with --dropout > 0: the reference model built with dropout p (GPT2Config
+    embd/attn/resid_pdrop, models/net.py:30-32) in training mode, its every dropout call fed the
+    mask the HIP kernels draw (include/dpt_hip.h dpt_train_desc: Philox(seed, (site, e / 4,
+    DPT_STREAM_DROPOUT)) word e % 4 >= ceil(p 2^32), kept elements times float32(1 / (1 - p))).
+    torch.nn.functional.dropout is replaced for the call and each call's site is checked by order
+    and shape: 0 the embedding sum, then per layer the attention probabilities, c_proj's output
+    and mlp.c_proj's output -- this pins WHERE GPT-2 drops, which is what the restatement must
+    match (torch's own mask stream is not reproducible on the device, and is not the point).
+    Attention runs "eager" for the recording: sdpa draws its probability mask inside the fused
+    op, where no mask can be injected; eager applies the same dropout to the same softmax
+    probabilities.  Float64, the bandit5 weights, two (p, seed) pairs."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.dirname(OUT))
+    from philox_np import philox
+    from net import Transformer
+    g = dict(np.load(os.path.join(OUT, "forward_bandit5.npz")))
+    H, sd_, ad, L, E = (int(x) for x in g["cfg"])
+    C, B = 20, 3
+    out = {}
+    real = torch.nn.functional.dropout
+    for case, (p, seed) in enumerate(((0.1, 77), (0.3, 2 ** 40 + 5))):
+        m = Transformer(dict(horizon=H, state_dim=sd_, action_dim=ad, n_layer=L, n_embd=E, n_head=4, dropout=p,
+                             test=False))
+        state = m.state_dict()
+        for k, v in g.items():
+            if k.startswith("w/"):
+                state[k[2:]] = torch.from_numpy(v)
+        m.load_state_dict(state)
+        m.transformer.set_attn_implementation("eager")
+        m = m.double()
+        m.train()
+        rs = np.random.RandomState(900 + case)
+        batch = {"query_states": np.ones((B, 1)), "context_states": np.ones((B, C, 1)),
+                 "context_actions": np.eye(ad)[rs.randint(0, ad, (B, C))],
+                 "context_next_states": np.ones((B, C, 1)), "context_rewards": rs.normal(0.5, 0.5, (B, C, 1))}
+        batch["zeros"] = np.zeros((B, sd_ ** 2 + ad + 1))
+        opt = np.eye(ad)[rs.randint(0, ad, B)]
+        p32 = np.float32(p)
+        thr = min(int(np.ceil(np.float64(p32) * 2.0 ** 32)), 2 ** 32 - 1)
+        scale = np.float64(np.float32(1.0) / (np.float32(1.0) - p32))
+        T = C + 1
+        shapes = [(B, T, E)]
+        for _ in range(L):
+            shapes += [(B, 1, T, T), (B, T, E), (B, T, E)]
+        calls = []
+
+        def fake(x, p=0.5, training=True, inplace=False, _p=p):
+            p_, p = p, _p
+            site = len(calls)
+            assert training and abs(p_ - p) < 1e-12, (site, p_, training)
+            assert tuple(x.shape) == shapes[site], (site, tuple(x.shape), shapes[site])
+            n = x.numel()
+            w = np.stack(philox(seed, site, np.arange((n + 3) // 4), 3), 1).reshape(-1)[:n]
+            k = torch.from_numpy(np.where(w >= thr, scale, 0.0).reshape(x.shape))
+            calls.append(site)
+            return x * k
+        torch.nn.functional.dropout = fake
+        try:
+            tb = {k: torch.tensor(v, dtype=torch.float64) for k, v in batch.items()}
+            m.zero_grad()
+            pred = m(tb)                                             # train.py:302
+            true = torch.tensor(opt, dtype=torch.float64).unsqueeze(1).repeat(1, pred.shape[1], 1)
+            loss = torch.nn.CrossEntropyLoss(reduction="sum")(pred.reshape(-1, ad), true.reshape(-1, ad))
+            loss.backward()                                          # train.py:309
+        finally:
+            torch.nn.functional.dropout = real
+        assert calls == list(range(len(shapes))), calls
+        pre = f"c{case}/"
+        for k, v in batch.items():
+            out[pre + k] = np.asarray(v, np.float64)
+        out[pre + "optimal_actions"] = opt
+        out[pre + "p"] = np.float64(p)
+        out[pre + "seed"] = np.uint64(seed)
+        out[pre + "loss"] = np.float64(loss.item())
+        out[pre + "preds"] = pred.detach().numpy()
+        for k, prm in m.named_parameters():
+            if prm.grad is not None and not k.endswith("wte.weight"):
+                gv = prm.grad.detach().numpy()
+                if k.endswith("wpe.weight"):
+                    assert not gv[T:].any()
+                    gv = gv[:T]
+                out[pre + "grad/" + k] = gv
+    np.savez_compressed(os.path.join(OUT, "train_dropout.npz"), **out)
+    print("train dropout")
+
+
 def linucb_d4():
     """LinUCB (ctrls/ctrl_bandit.py:447-528) on 12-arm linear bandits with lin_d = 4 (the --lin_d
     flag, common_args.py:15-16), through eval_linear_bandit.deploy_online_vec with every draw

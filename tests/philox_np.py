@@ -41,3 +41,15 @@ def normal(seed, step, task, stream):
     u1 = 1.0 - u53(x[0], x[1])
     u2 = u53(x[2], x[3])
     return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+
+def dropout_keep(seed, p, site, shape):
+    """The training kernels' dropout factors of one site (include/dpt_hip.h dpt_train_desc):
+    element e kept iff word e % 4 of Philox(seed, (site, e / 4, DPT_STREAM_DROPOUT = 3)) >=
+    ceil(p 2^32) (p as float32), kept elements times float32(1 / (1 - p)); float64 array."""
+    p32 = np.float32(p)
+    thr = min(int(np.ceil(np.float64(p32) * 2.0 ** 32)), 2 ** 32 - 1)
+    scale = np.float64(np.float32(1.0) / (np.float32(1.0) - p32))
+    n = int(np.prod(shape))
+    w = np.stack(philox(seed, site, np.arange((n + 3) // 4), 3), 1).reshape(-1)[:n]
+    return np.where(w >= np.uint64(thr), scale, 0.0).reshape(shape)

@@ -59,7 +59,7 @@ def test_struct_layout_matches_header(tmp_path):
     from dpt_hip import _lib
     structs = {"dpt_model_desc": _lib.ModelDesc, "dpt_bandit_rollout_args": _lib.BanditRolloutArgs,
                "dpt_policy_rollout_args": _lib.PolicyRolloutArgs,
-               "dpt_darkroom_rollout_args": _lib.DarkroomRolloutArgs}
+               "dpt_darkroom_rollout_args": _lib.DarkroomRolloutArgs, "dpt_train_desc": _lib.TrainDesc}
     cc = shutil.which("gcc") or shutil.which("cc")
     if cc is None:
         pytest.skip("no C compiler")

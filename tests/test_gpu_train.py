@@ -319,3 +319,118 @@ def test_forward_only_workspace_and_second_backward():
     loss.backward(retain_graph=True)
     with pytest.raises(RuntimeError, match="retain_graph"):
         loss.backward()
+
+
+def _dropout_step(m, batch, opt, A, p, seed, grad=True):
+    """One train.py:296-310 step of m in training mode with dropout p through
+    TransformerFunction with an explicit mask seed -> (loss, preds[:, 1:])."""
+    from dpt_hip import train as tr
+    tok = m._tokens(batch)
+    dims = (m.n_layer, m.n_embd, m.state_dim, m.action_dim, m.n_positions, tok.shape[0], tok.shape[1],
+            0 if grad else tr.FORWARD_ONLY, p, seed)
+    pred = tr.TransformerFunction.apply(tok, dims, *tr.param_list(m))[:, 1:, :]
+    true = opt.unsqueeze(1).repeat(1, pred.shape[1], 1).reshape(-1, A)
+    loss = torch.nn.CrossEntropyLoss(reduction="sum")(pred.reshape(-1, A), true)
+    if grad:
+        m.zero_grad()
+        loss.backward()
+    return loss, pred
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_train_dropout_matches_reference(case):
+    """Training-mode dropout (models/net.py:30-32, p = 0.1 and 0.3): loss, preds and every
+    gradient against the reference model run with the same masks injected
+    (tests/golden/train_dropout.npz, float64); the forward-only call (no_grad in training mode,
+    train.py:265-278) gives the same preds from the same seed."""
+    g = golden("train_dropout.npz")
+    fw, m = model_from_fixture("bandit5")
+    A = int(fw["cfg"][2])
+    pre = f"c{case}/"
+    batch = {k: torch.from_numpy(g[pre + k]).float().cuda() for k in KEYS}
+    batch["zeros"] = torch.from_numpy(g[pre + "zeros"]).float().cuda()
+    opt = torch.from_numpy(g[pre + "optimal_actions"]).float().cuda()
+    p, seed = float(g[pre + "p"]), int(g[pre + "seed"])
+    m.train()
+    loss, pred = _dropout_step(m, batch, opt, A, p, seed)
+    ref_loss = float(g[pre + "loss"])
+    assert abs(loss.item() - ref_loss) <= 1e-5 * abs(ref_loss)
+    ref = g[pre + "preds"]
+    assert (np.abs(pred.detach().cpu().numpy() - ref) <= 1e-5 * np.maximum(1, np.abs(ref))).all()
+    for k, prm in m.named_parameters():
+        if k.endswith("wte.weight"):
+            continue
+        r = g[pre + "grad/" + k]
+        got = prm.grad.detach().cpu().numpy()
+        got = got[:r.shape[0]] if k.endswith("wpe.weight") else got
+        assert rel_err(got, r) <= 5 * GRAD_TOL, k
+    with torch.no_grad():
+        _, pred2 = _dropout_step(m, batch, opt, A, p, seed, grad=False)
+    assert torch.equal(pred2, pred.detach())
+    with torch.no_grad():
+        _, pred3 = _dropout_step(m, batch, opt, A, p, seed + 1, grad=False)
+    assert not torch.equal(pred3, pred.detach())   # another seed, other masks
+
+
+@pytest.mark.parametrize("E,T", [(16, 38), (64, 103)])
+def test_train_dropout_other_widths_vs_oracle(E, T):
+    """Dropout at widths 16 / 64 (the widths whose p = 0 path runs the matrix-core kernels; with
+    dropout the row kernels) against the float64 oracle with the same masks; windows with
+    T % 4 != 0."""
+    from models.net import Transformer
+    from oracle import dpt_oracle_torch as OT
+    from philox_np import dropout_keep
+    A, L, B, C, sd, p, seed = 5, 2, 4, T - 1, 2, 0.2, 12345
+    torch.manual_seed(E + T + 1)
+    m = Transformer(dict(horizon=C, state_dim=sd, action_dim=A, n_layer=L, n_embd=E, n_head=1, dropout=p,
+                         test=False))
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.add_(0.05 * torch.randn_like(prm))
+    w = {k: v.detach().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    m = m.cuda()
+    rs = np.random.RandomState(E * 5 + T)
+    hb = {"query_states": rs.randint(0, 10, (B, sd)).astype(np.float64),
+          "context_states": rs.randint(0, 10, (B, C, sd)).astype(np.float64),
+          "context_actions": np.eye(A)[rs.randint(0, A, (B, C))],
+          "context_next_states": rs.randint(0, 10, (B, C, sd)).astype(np.float64),
+          "context_rewards": rs.normal(0.5, 0.5, (B, C, 1)), "optimal_actions": np.eye(A)[rs.randint(0, A, B)]}
+
+    def drop(site):
+        return torch.from_numpy(dropout_keep(seed, p, site, (B, T, T) if site % 3 == 1 else (B, T, E)))
+    loss_ref, preds_ref, grads_ref = OT.grads(w, hb, L, sd, A, drop=drop)
+    batch = {k: torch.tensor(hb[k], dtype=torch.float32, device="cuda") for k in KEYS}
+    batch["zeros"] = torch.zeros((B, sd * sd + A + 1), device="cuda")
+    opt = torch.tensor(hb["optimal_actions"], dtype=torch.float32, device="cuda")
+    m.train()
+    loss, pred = _dropout_step(m, batch, opt, A, p, seed)
+    assert abs(loss.item() - loss_ref) <= 1e-5 * abs(loss_ref)
+    assert (np.abs(pred.detach().cpu().numpy() - preds_ref) <= 1e-5 * np.maximum(1, np.abs(preds_ref))).all()
+    for k, prm in m.named_parameters():
+        if k.endswith("wte.weight"):
+            continue
+        assert rel_err(prm.grad.detach().cpu().numpy(), grads_ref[k]) <= 5 * GRAD_TOL, k
+
+
+def test_train_dropout_through_the_model_forward():
+    """Transformer.forward in training mode with dropout > 0 (the reference's --dropout flag):
+    seeds come from torch's generator -- the same manual_seed, the same preds; a second call, new
+    masks -- and eval mode applies none (equal to the p = 0 model's preds)."""
+    g = golden("train_grads.npz")
+    _, m = model_from_fixture("bandit5")
+    batch, _ = batch_from(g, "bandit5")
+    m.dropout = 0.3
+    m.train()
+    torch.manual_seed(3)
+    a = m(batch).detach()
+    b = m(batch).detach()
+    torch.manual_seed(3)
+    c = m(batch).detach()
+    assert torch.equal(a, c) and not torch.equal(a, b)
+    m.eval()
+    with torch.no_grad():
+        e = m(batch)
+    m.dropout = 0.0
+    with torch.no_grad():
+        f = m(batch)
+    assert torch.equal(e, f)

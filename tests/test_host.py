@@ -86,19 +86,52 @@ def test_train_blob_order_matches_pack_weights():
     assert all(torch.equal(a, b) for a, b in zip(back, ps))
 
 
-def test_training_mode_dropout_is_rejected():
-    """GPT2Config applies dropout in training mode (models/net.py:30-32); the HIP kernels have none,
-    so a training-mode forward with dropout > 0 raises (with or without grad) instead of training
-    or evaluating without it.  Eval mode ignores dropout, as the reference does."""
-    import pytest
+def test_training_mode_dropout_takes_the_training_kernels(monkeypatch):
+    """GPT2Config applies dropout in training mode (models/net.py:30-32), with or without grad
+    (train.py:265-278's test loss): such calls go to the training kernels (which implement it)
+    with a fresh Philox seed drawn from torch's generator per call; eval mode ignores dropout."""
     import torch
+    from dpt_hip import train as tr
     from models.net import Transformer
     m = Transformer(dict(horizon=4, state_dim=1, action_dim=5, n_layer=2, n_embd=32, n_head=1, dropout=0.1,
                          test=False))
-    with pytest.raises(NotImplementedError, match="dropout"):
+    seen = []
+
+    def fake_apply(tok, dims, *params):
+        seen.append(dims)
+        return torch.zeros((tok.shape[0], tok.shape[1], 5))
+    monkeypatch.setattr(tr.TransformerFunction, "apply", fake_apply)
+    monkeypatch.setattr(m, "_tokens", lambda x: torch.zeros((3, 9, 8)))
+    torch.manual_seed(5)
+    m(_tiny_batch())
+    with torch.no_grad():
         m(_tiny_batch())
-    with torch.no_grad(), pytest.raises(NotImplementedError, match="dropout"):
-        m(_tiny_batch())
+    torch.manual_seed(5)
+    m(_tiny_batch())
+    assert [d[7] for d in seen] == [0, tr.FORWARD_ONLY, 0]
+    assert all(abs(d[8] - 0.1) < 1e-12 for d in seen)
+    assert seen[0][9] != seen[1][9] and seen[0][9] == seen[2][9]   # fresh per call, seedable
     m.eval()
-    with pytest.raises(RuntimeError, match="ROCm GPU"):  # eval mode goes on to the (absent) GPU
+    m.dropout = 0.1
+    seen.clear()
+    import pytest
+    with pytest.raises(RuntimeError, match="ROCm GPU"):  # eval mode: the fused inference path
         m(_tiny_batch())
+    assert not seen
+
+
+def test_train_desc_rejects_bad_dropout():
+    """dpt_train_desc.dropout outside [0, 1) is an argument error (host-side check, no GPU)."""
+    import ctypes
+    import pytest
+    from dpt_hip import _lib
+    from dpt_hip import train as tr
+    lib = _lib.load()
+    n = ctypes.c_int64()
+    for p in (1.0, -0.1, 1.5):
+        d = tr.desc(2, 32, 1, 5, 40, 3, 9, dropout=p, seed=1)
+        with pytest.raises(ValueError, match="dropout"):
+            _lib.check(lib.dpt_train_blob_numel(ctypes.byref(d), ctypes.byref(n)))
+    d = tr.desc(2, 32, 1, 5, 40, 3, 9, dropout=0.5, seed=1)
+    _lib.check(lib.dpt_train_blob_numel(ctypes.byref(d), ctypes.byref(n)))
+    assert n.value > 0

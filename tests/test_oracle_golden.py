@@ -314,3 +314,39 @@ def test_linucb_matches_reference(fix):
                                   first_u_idx=g["first_action"])
     assert np.array_equal(out["actions"], g["actions"])
     assert np.array_equal(out["cum_means"], g["cum_means"])
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_torch_oracle_dropout_matches_reference(case):
+    """Training-mode dropout (GPT2Config embd/attn/resid_pdrop, models/net.py:30-32): the
+    float64 oracle with the kernels' Philox masks (tests/philox_np.dropout_keep) against the
+    reference model run with the same masks injected at its dropout calls
+    (tests/golden/train_dropout.npz; gen_golden.py train_dropout checks each call's site by order
+    and shape) -- pins the placement of every mask: embedding sum, attention probabilities,
+    c_proj and mlp.c_proj outputs."""
+    import torch
+    from oracle import dpt_oracle_torch as OT
+    from philox_np import dropout_keep
+    g = golden("train_dropout.npz")
+    fw = golden("forward_bandit5.npz")
+    H, sd, A, L, E = (int(x) for x in fw["cfg"])
+    w = {k[2:]: v for k, v in fw.items() if k.startswith("w/")}
+    pre = f"c{case}/"
+    batch = {k: g[pre + k] for k in ("query_states", "context_states", "context_actions", "context_next_states",
+                                     "context_rewards", "optimal_actions")}
+    B, T = batch["context_states"].shape[0], batch["context_states"].shape[1] + 1
+    p, seed = float(g[pre + "p"]), int(g[pre + "seed"])
+
+    def drop(site):
+        shape = (B, T, T) if site % 3 == 1 else (B, T, E)
+        return torch.from_numpy(dropout_keep(seed, p, site, shape))
+    loss, preds, gr = OT.grads(w, batch, L, sd, A, drop=drop)
+    assert abs(loss - float(g[pre + "loss"])) <= 1e-10 * abs(loss)
+    assert np.abs(preds - g[pre + "preds"]).max() <= 1e-12
+    for k, v in gr.items():
+        ref = g[pre + "grad/" + k]
+        got = v[:ref.shape[0]] if k.endswith("wpe.weight") else v
+        assert np.abs(got - ref).max() <= 1e-10 * max(1e-30, np.abs(ref).max()), k
+    # the masks drop about p of the elements (a loose sanity bar on the threshold)
+    k0 = dropout_keep(seed, p, 0, (64, 1024))
+    assert abs((k0 == 0).mean() - p) < 0.01
