@@ -76,6 +76,8 @@ int train_backward(const TrDims&, const float*, const float*, float*, const floa
 int64_t train_workspace_numel(const TrDims&);
 int64_t train_blob_numel(const TrDims&);
 int train_dims_check(const TrDims&);
+int64_t gen_rollout_workspace_numel(const TrDims&, int, int);
+int rollout_bandit_generic(const TrDims&, const float*, const dpt_bandit_rollout_args&, hipStream_t);
 
 }  // namespace dpt
 
@@ -556,6 +558,25 @@ int dpt_train_backward(const dpt_train_desc* d, const float* blob, const float* 
     REQUIRE(blob && tokens && ws && dpreds && dblob, "null pointer");
     REQUIRE(!t.fwd_only, "train backward: the description is forward-only (DPT_TRAIN_FORWARD_ONLY)");
     return train_backward(t, blob, tokens, ws, dpreds, dblob, S(stream));
+}
+
+int dpt_rollout_bandit_generic_workspace_numel(const dpt_train_desc* d, int32_t N, int32_t H, int64_t* numel) {
+    TrDims t;
+    if (int rc = train_dims(d, t)) return rc;
+    REQUIRE(numel, "null numel");
+    REQUIRE(N >= 0 && H >= 0, "N=%d H=%d", N, H);
+    *numel = gen_rollout_workspace_numel(t, N, H);
+    return DPT_OK;
+}
+
+int dpt_rollout_bandit_generic(const dpt_train_desc* d, const float* blob, const dpt_bandit_rollout_args* a,
+                               void* stream) {
+    TrDims t;
+    if (int rc = train_dims(d, t)) return rc;
+    REQUIRE(blob && a, "null pointer");
+    REQUIRE(!t.drop(), "generic bandit rollout: dropout must be 0 (an eval-mode forward)");
+    if (a->N == 0 || a->H == 0) return DPT_OK;
+    return rollout_bandit_generic(t, blob, *a, S(stream));
 }
 
 }  // extern "C"

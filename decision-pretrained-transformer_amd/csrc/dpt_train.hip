@@ -1101,4 +1101,226 @@ int train_backward(const TrDims& d, const float* blob, const float* tok, float* 
     return launched("train backward embed");
 }
 
+// ------------------------------------------------------------------------------ generic-width rollout
+// The bandit online loop (evals/eval_bandit.py:56-103: decode -> select -> env step -> append the
+// transition) at ANY width, for models the fused E = 32 kernel (dpt_decode.hip) is not built for.
+// Exact K/V-cache decode: the bandit's query token sits at position 0 and never changes, and the
+// prediction is read at the last position, so every earlier position's keys and values stay
+// valid (causal attention) and a step computes the new token only.  One pass per step over all N
+// tasks: embed, then per layer the training forward's row kernels (or their matrix-core forms at
+// widths 16 / 32 / 64) on N rows, the attention of the new token over the task's cache, ln_f and
+// the head; then selection and the env step with the draws and arithmetic of the fused kernel.
+// Workspace (floats): K and V caches [L][N][H][E], then per-step rows.
+struct GenWs {
+    int64_t K, V, x, x2, y, st, qkv, o, h, lg, tok, total;
+    static GenWs make(const TrDims& d, int N, int H) {
+        GenWs w;
+        const int64_t E = d.E, n = N, cache = (int64_t)d.L * n * H * E;
+        int64_t p = 0;
+        auto take = [&](int64_t k) { const int64_t at = p; p += k; p = (p + 3) & ~3ll; return at; };
+        w.K = take(cache);
+        w.V = take(cache);
+        w.x = take(n * E);
+        w.x2 = take(n * E);
+        w.y = take(n * E);
+        w.st = take(n * 2);
+        w.qkv = take(n * 3 * E);
+        w.o = take(n * E);
+        w.h = take(n * 4 * E);
+        w.lg = take(n * d.A);
+        w.tok = take(n * d.F);
+        w.total = p;
+        return w;
+    }
+};
+
+// x[n][e] = tok[n] emb_w + emb_b + wpe[pos]: the new token of every task (tr_embed's order)
+__global__ void gen_embed(const float* __restrict__ tok, const float* __restrict__ blob, TrDims d, TrBlob b, int N,
+                          int pos, float* __restrict__ x) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)N * d.E) return;
+    const int n = (int)(i / d.E), e = (int)(i % d.E);
+    float acc = blob[b.emb_b + e];
+    for (int f = 0; f < d.F; ++f) acc = fmaf(tok[(int64_t)n * d.F + f], blob[b.emb_w + (int64_t)f * d.E + e], acc);
+    x[i] = acc + blob[b.wpe + (int64_t)pos * d.E + e];
+}
+
+// One wave per task: store the new token's key and value at position pos of the task's cache
+// (rows [pos][E] of [N][H][E]) and attend over positions 0..pos -- tr_attn_fwd's arithmetic for the
+// causal row of the new token (the new key and value are read from the qkv row itself).
+__global__ void gen_attn_decode(const float* __restrict__ qkv, float* __restrict__ Kc, float* __restrict__ Vc, int E,
+                                int N, int H, int pos, float* __restrict__ O) {
+    extern __shared__ float sm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int task = blockIdx.x * (blockDim.x / 64) + wave;
+    if (task >= N) return;
+    float* pr = sm + (size_t)wave * (H + E);
+    float* q = pr + H;
+    const float* row = qkv + (int64_t)task * 3 * E;
+    float* K = Kc + (int64_t)task * H * E;
+    float* V = Vc + (int64_t)task * H * E;
+    for (int e = lane; e < E; e += 64) {
+        q[e] = row[e];
+        K[(int64_t)pos * E + e] = row[E + e];
+        V[(int64_t)pos * E + e] = row[2 * E + e];
+    }
+    wave_lds_sync();
+    const float scale = 1.0f / sqrtf((float)E);
+    float m = -INFINITY;
+    for (int j = lane; j <= pos; j += 64) {
+        const float* k = j == pos ? row + E : K + (int64_t)j * E;
+        float s = 0.f;
+        for (int e = 0; e < E; ++e) s = fmaf(q[e], k[e], s);
+        s *= scale;
+        pr[j] = s;
+        m = fmaxf(m, s);
+    }
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = lane; j <= pos; j += 64) {
+        const float p = expf(pr[j] - m);
+        pr[j] = p;
+        l += p;
+    }
+    const float inv = 1.0f / wave_sum(l);
+    for (int j = lane; j <= pos; j += 64) pr[j] *= inv;
+    wave_lds_sync();
+    for (int e = lane; e < E; e += 64) {
+        float acc = 0.f;
+        for (int j = 0; j < pos; ++j) acc = fmaf(pr[j], V[(int64_t)j * E + e], acc);
+        acc = fmaf(pr[pos], row[2 * E + e], acc);
+        O[(int64_t)task * E + e] = acc;
+    }
+}
+
+struct GenEnv {
+    int N, H, A, sd, type, sample;
+    int64_t first_task;
+    double var;
+    uint64_t seed, counter;
+    const double* means;
+    const double* uniforms;
+    const double* noise;
+    int32_t* actions_out;
+    double* rewards_out;
+    double* arm_value_out;
+    float* logits_out;
+};
+
+// the token rows: the query [1_sd, 0_A, 0_sd, 0] at step 0 (eval_bandit.py: query state ones)
+__global__ void gen_query_token(int N, int F, int sd, float* __restrict__ tok) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)N * F) return;
+    tok[i] = (int)(i % F) < sd ? 1.f : 0.f;
+}
+
+// selection and env step of step h for every task (the fused kernel's draws, select_from_logits
+// and reward arithmetic), the outputs, and the next token [1_sd, onehot(a), 1_sd, float(r)]
+// (eval_bandit.py:83-86)
+__global__ void gen_select_env(const float* __restrict__ lg, GenEnv g, int h, float* __restrict__ tok) {
+    const int task = blockIdx.x * blockDim.x + threadIdx.x;
+    if (task >= g.N) return;
+    const int64_t gtask = g.first_task + task;
+    const uint64_t ctr = g.counter + (uint64_t)h;
+    double u = 0.0;
+    if (g.sample) u = g.uniforms ? g.uniforms[(size_t)h * g.N + task] : philox_uniform(g.seed, ctr, gtask, DPT_STREAM_SELECT);
+    const float* l = lg + (int64_t)task * g.A;
+    const int a = select_from_logits(l, g.A, g.sample, 1.0f, u);
+    const double mean = g.means[(int64_t)task * g.A + a];
+    double dr;
+    if (g.noise) dr = g.noise[(size_t)h * g.N + task];
+    else if (g.type == DPT_BANDIT_BERNOULLI) dr = philox_uniform(g.seed, ctr, gtask, DPT_STREAM_REWARD);
+    else dr = philox_normal(g.seed, ctr, gtask, DPT_STREAM_REWARD);
+    const double r = g.type == DPT_BANDIT_BERNOULLI ? (dr < mean ? 1.0 : 0.0) : gaussian_reward(mean, g.var, dr);
+    const size_t o = (size_t)task * g.H + h;
+    g.actions_out[o] = a;
+    g.rewards_out[o] = r;
+    g.arm_value_out[o] = mean;
+    if (g.logits_out)
+        for (int k = 0; k < g.A; ++k) g.logits_out[((size_t)h * g.N + task) * g.A + k] = l[k];
+    const int F = 2 * g.sd + g.A + 1;
+    float* t = tok + (int64_t)task * F;
+    for (int k = 0; k < g.sd; ++k) t[k] = 1.f;
+    for (int k = 0; k < g.A; ++k) t[g.sd + k] = k == a ? 1.f : 0.f;
+    for (int k = 0; k < g.sd; ++k) t[g.sd + g.A + k] = 1.f;
+    t[F - 1] = (float)r;
+}
+
+int64_t gen_rollout_workspace_numel(const TrDims& d, int N, int H) { return GenWs::make(d, N, H).total; }
+
+int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_rollout_args& a, hipStream_t st) {
+    if (int rc = train_dims_check(d)) return rc;
+    if (a.A != d.A || d.F != 2 + a.A + 1 || a.H > d.npos || a.N < 1 || a.H < 1 ||
+        (a.type != DPT_BANDIT_GAUSSIAN && a.type != DPT_BANDIT_BERNOULLI) || a.kvcache == nullptr || a.means == nullptr ||
+        a.actions_out == nullptr || a.rewards_out == nullptr || a.arm_value_out == nullptr) {
+        set_error(DPT_EINVAL, "generic bandit rollout: A=%d (model %d), state_dim must be 1, H=%d (n_positions %d), type=%d",
+                  a.A, d.A, a.H, d.npos, a.type);
+        return DPT_EINVAL;
+    }
+    const int N = a.N, H = a.H, E = d.E, L = d.L;
+    const TrBlob B = TrBlob::make(d);
+    const GenWs W = GenWs::make(d, N, H);
+    float* ws = a.kvcache;
+    const int rows_per_block = kTrThreads / 64;
+    const unsigned row_blocks = (N + rows_per_block - 1) / rows_per_block;
+    const size_t attn_lds = sizeof(float) * rows_per_block * (size_t)(H + E);
+    if (attn_lds > 160 * 1024) {
+        set_error(DPT_EUNSUPPORTED, "generic bandit rollout: H=%d too long for the attention kernel", H);
+        return DPT_EUNSUPPORTED;
+    }
+    if (attn_lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)gen_attn_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)attn_lds);
+    GenEnv g{N, H, a.A, 1, a.type, a.sample, a.first_task, a.var, a.seed, a.counter, a.means, a.uniforms, a.noise,
+             a.actions_out, a.rewards_out, a.arm_value_out, a.logits_out};
+    const bool fast = mm_fast(E);
+    float* x = ws + W.x;
+    float* x2 = ws + W.x2;
+    float* y = ws + W.y;
+    float* stt = ws + W.st;
+    float* qkv = ws + W.qkv;
+    float* o = ws + W.o;
+    float* hb = ws + W.h;
+    const int64_t NE = (int64_t)N * E, cache = (int64_t)N * H * E;
+    hipLaunchKernelGGL(gen_query_token, dim3(blocks_for((int64_t)N * d.F)), dim3(kTrThreads), 0, st, N, d.F, 1,
+                       ws + W.tok);
+    for (int h = 0; h < H; ++h) {
+        hipLaunchKernelGGL(gen_embed, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, ws + W.tok, blob, d, B, N, h, x);
+        for (int l = 0; l < L; ++l) {
+            const TrLayer P = TrLayer::make(B.layers + l * d.layer_size(), E);
+            hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x, blob + P.ln1_g, blob + P.ln1_b,
+                               N, E, y, stt);
+            if (fast)
+                mm(E, kMmQkv, y, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, N, qkv, st);
+            else
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE * 3)), dim3(kTrThreads), 0, st, y, blob + P.attn_w,
+                                   blob + P.attn_b, nullptr, N, E, 3 * E, 0, qkv);
+            hipLaunchKernelGGL(gen_attn_decode, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv,
+                               ws + W.K + l * cache, ws + W.V + l * cache, E, N, H, h, o);
+            if (fast)
+                mm(E, kMmProj, o, blob + P.proj_w, blob + P.proj_b, x, nullptr, N, x2, st);
+            else
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, o, blob + P.proj_w,
+                                   blob + P.proj_b, x, N, E, E, 0, x2);
+            hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x2, blob + P.ln2_g, blob + P.ln2_b,
+                               N, E, y, stt);
+            if (fast) {
+                mm(E, kMmFc, y, blob + P.fc_w, blob + P.fc_b, nullptr, nullptr, N, hb, st);
+                mm(E, kMmMp, hb, blob + P.mp_w, blob + P.mp_b, x2, nullptr, N, x, st);
+            } else {
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE * 4)), dim3(kTrThreads), 0, st, y, blob + P.fc_w,
+                                   blob + P.fc_b, nullptr, N, E, 4 * E, 0, hb);
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, hb, blob + P.mp_w,
+                                   blob + P.mp_b, x2, N, 4 * E, E, 1, x);
+            }
+        }
+        hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x, blob + B.lnf_g, blob + B.lnf_b, N,
+                           E, y, stt);
+        hipLaunchKernelGGL(tr_linear, dim3(blocks_for((int64_t)N * d.A)), dim3(kTrThreads), 0, st, y, blob + B.head_w,
+                           blob + B.head_b, nullptr, N, E, d.A, 0, ws + W.lg);
+        hipLaunchKernelGGL(gen_select_env, dim3((N + 255) / 256), dim3(256), 0, st, ws + W.lg, g, h, ws + W.tok);
+        if (int rc = launched("generic bandit rollout step")) return rc;
+    }
+    return DPT_OK;
+}
+
 }  // namespace dpt

@@ -95,7 +95,11 @@ def load():
                               "the DPT hot path has no CPU fallback")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            # (tests/test_abi.py requires every header symbol; an older build loaded for an A/B may
+            # lack newer entry points, which then fail when called)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
             fn.restype = res
             fn.argtypes = args
         v = lib.dpt_abi_version()
@@ -193,3 +197,7 @@ SIGNATURES["dpt_train_forward"] = (_i32, [ctypes.POINTER(TrainDesc), _c_void_p, 
                                           _c_void_p])
 SIGNATURES["dpt_train_backward"] = (_i32, [ctypes.POINTER(TrainDesc), _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                            _c_void_p, _c_void_p])
+SIGNATURES["dpt_rollout_bandit_generic_workspace_numel"] = (_i32, [ctypes.POINTER(TrainDesc), _i32, _i32,
+                                                                   ctypes.POINTER(_i64)])
+SIGNATURES["dpt_rollout_bandit_generic"] = (_i32, [ctypes.POINTER(TrainDesc), _c_void_p,
+                                                   ctypes.POINTER(BanditRolloutArgs), _c_void_p])

@@ -45,7 +45,6 @@ def _fused_ok(vec_env, controller, horizon):
     from models.net import Transformer
     return (isinstance(controller, BanditTransformerController) and isinstance(vec_env, BanditEnvVec)
             and isinstance(controller.model, Transformer) and controller.model.state_dim == 1
-            and controller.model.n_embd == dpt_hip.E
             and controller.batch_size == vec_env.num_envs and horizon <= controller.model.n_positions)
 
 
@@ -59,7 +58,6 @@ def rollout_fused(vec_env, controller, horizon, uniforms=None, noise=None, seed=
     are used unless ``uniforms`` is given explicitly.  Draws are keyed by the
     global task id (``vec_env.first_task`` for a shard).
     """
-    dm = controller.model.device_model()
     s0, ctr0 = controller._stream.next()
     controller._stream.counter = ctr0 + horizon
     seed = s0 if seed is None else seed
@@ -68,8 +66,14 @@ def rollout_fused(vec_env, controller, horizon, uniforms=None, noise=None, seed=
                              for h in range(horizon)])
     if first_task is None:
         first_task = getattr(vec_env, "first_task", 0)
-    return dm.rollout_bandit(vec_env.means_device, horizon, vec_env.var, controller.sample, vec_env.type_code,
-                             seed=seed, first_task=first_task, uniforms=uniforms, noise=noise, counter=ctr0)
+    kw = dict(seed=seed, first_task=first_task, uniforms=uniforms, noise=noise, counter=ctr0)
+    model = controller.model
+    if model.n_embd != dpt_hip.E:  # widths the fused kernel is not built for: the generic-width rollout
+        from dpt_hip import train as tr
+        return tr.rollout_bandit_generic(model, vec_env.means_device, horizon, vec_env.var, controller.sample,
+                                         vec_env.type_code, **kw)
+    return model.device_model().rollout_bandit(vec_env.means_device, horizon, vec_env.var, controller.sample,
+                                               vec_env.type_code, **kw)
 
 
 def _policy_ok(vec_env, controller):

@@ -419,6 +419,20 @@ int dpt_train_forward(const dpt_train_desc* desc_host, const float* blob, const 
 int dpt_train_backward(const dpt_train_desc* desc_host, const float* blob, const float* tokens, float* workspace,
                        const float* dpreds, float* dblob, void* stream);
 
+/* The bandit online loop (evals/eval_bandit.py:56-103, as dpt_rollout_bandit) for models of ANY
+ * width (state_dim 1, blob in the dpt_train_desc layout; desc batch / window unused, set 1, and
+ * dropout 0): an exact K/V-cache decode, one step for all N tasks at a time (the training
+ * forward's row kernels, or their matrix-core forms at widths 16 / 32 / 64, on N rows; the new
+ * token's attention over the task's cache), then the fused kernel's selection, draws and env
+ * step.  args->kvcache = dpt_rollout_bandit_generic_workspace_numel floats (K and V caches
+ * [n_layer][N][H][n_embd] plus per-step rows); the other fields as for dpt_rollout_bandit.
+ * Replaces the per-step path (Transformer.forward over the whole window every step) at widths
+ * the fused kernel is not built for.                                                        */
+int dpt_rollout_bandit_generic_workspace_numel(const dpt_train_desc* desc_host, int32_t N, int32_t H,
+                                               int64_t* numel_out_host);
+int dpt_rollout_bandit_generic(const dpt_train_desc* desc_host, const float* blob,
+                               const dpt_bandit_rollout_args* args_host, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

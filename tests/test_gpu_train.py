@@ -434,3 +434,106 @@ def test_train_dropout_through_the_model_forward():
     with torch.no_grad():
         f = m(batch)
     assert torch.equal(e, f)
+
+
+def _width_model(E, L, H, seed):
+    from models.net import Transformer
+    torch.manual_seed(seed)
+    m = Transformer(dict(horizon=H, state_dim=1, action_dim=5, n_layer=L, n_embd=E, n_head=1, dropout=0.0,
+                         test=True)).cuda().eval()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    return m
+
+
+@pytest.mark.parametrize("E,L,bern,sample", [(16, 3, False, True), (48, 2, False, True), (64, 4, True, True),
+                                             (64, 2, False, False), (32, 2, False, True)])
+def test_generic_width_rollout_vs_oracle(E, L, bern, sample):
+    """dpt_rollout_bandit_generic (the bandit online loop at any width: exact K/V-cache decode, one
+    step for all tasks at a time) against the float64 oracle's re-forward-every-step rollout fed the
+    same draws: logits within 1e-5 at every step, actions / rewards / arm values exactly.  Widths on
+    the row kernels (48) and on the matrix-core forms (16, 32, 64), Gaussian and Bernoulli rewards,
+    sampling and greedy; 37 tasks (a partial row block)."""
+    from dpt_hip import train as tr
+    from oracle import dpt_oracle as O
+    N, H = 37, 40
+    m = _width_model(E, L, H, E + L)
+    W = O.split_weights({k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}, L)
+    rs = np.random.RandomState(E * 3 + L)
+    means = rs.uniform(0, 1, (N, 5))
+    u = rs.uniform(size=(H, N))
+    g = rs.uniform(size=(H, N)) if bern else rs.normal(size=(H, N))
+    out = tr.rollout_bandit_generic(m, means, H, 0.3, sample, 1 if bern else 0, uniforms=u, noise=g,
+                                    want_logits=True)
+    ref = O.bandit_online_rollout(W, means, H, 0.3, u, g, sample=sample, bernoulli=bern)
+    lg = out["logits"].cpu().numpy()
+    assert (np.abs(lg - ref["logits"]) <= 1e-5 * np.maximum(1, np.abs(ref["logits"]))).all()
+    assert np.array_equal(out["actions"].cpu().numpy(), ref["actions"])
+    assert np.array_equal(out["rewards"].cpu().numpy(), ref["rewards"])
+    assert np.array_equal(out["arm_value"].cpu().numpy().T, ref["cum_means"])
+
+
+def test_generic_width_rollout_equals_fused_kernel_at_width_32():
+    """At width 32 the generic-width rollout and the fused kernel (dpt_rollout_bandit) run the same
+    loop: with the same Philox draws (seed, counter, global task ids) the actions agree; with
+    injected draws over 300 tasks x 80 steps every task agrees up to its first step whose uniform
+    lies within 1e-5 of a cdf edge (where the two fp32 summation orders may choose differently),
+    with logits within 1e-5 of each other up to that step."""
+    from dpt_hip import train as tr
+    N, H, L = 300, 80, 4
+    m = _width_model(32, L, H, 7)
+    rs = np.random.RandomState(3)
+    means = rs.uniform(0, 1, (N, 5))
+    a = tr.rollout_bandit_generic(m, means[:16], 12, 0.3, True, seed=99, first_task=1000, counter=5)
+    b = m.device_model().rollout_bandit(means[:16], 12, 0.3, True, seed=99, first_task=1000, counter=5)
+    assert np.array_equal(a["rewards"].cpu().numpy(), b["rewards"].cpu().numpy())   # same Philox draws
+    u, g = rs.uniform(size=(H, N)), rs.normal(size=(H, N))
+    a = tr.rollout_bandit_generic(m, means, H, 0.3, True, uniforms=u, noise=g, want_logits=True)
+    b = m.device_model().rollout_bandit(means, H, 0.3, True, uniforms=u, noise=g, want_logits=True)
+    la, lb = a["logits"].cpu().numpy(), b["logits"].cpu().numpy()
+    aa, ab = a["actions"].cpu().numpy(), b["actions"].cpu().numpy()
+    ra, rb = a["rewards"].cpu().numpy(), b["rewards"].cpu().numpy()
+    for i in range(N):
+        diff = np.nonzero(aa[i] != ab[i])[0]
+        n = int(diff[0]) if diff.size else H
+        if n < H:  # the first disagreement must be a near-tie of the draw with the cdf
+            p = np.exp(lb[n, i].astype(np.float64) - lb[n, i].max())
+            cdf = np.cumsum(p / p.sum())
+            assert np.abs(cdf[:-1] - u[n, i]).min() < 1e-5, (i, n)
+        k = min(n + 1, H)
+        assert (np.abs(la[:k, i] - lb[:k, i]) <= 1e-5 * np.maximum(1, np.abs(lb[:k, i]))).all(), i
+        assert np.array_equal(ra[i, :n], rb[i, :n]), i
+
+
+def test_generic_width_rollout_through_eval_bandit():
+    """eval_bandit.deploy_online_vec with a width-64 controller takes the generic-width rollout
+    (one call) and returns the per-step loop's cum_means (fused=False: the reference's loop, the
+    whole window re-forwarded every step) for the same draws."""
+    from ctrls.ctrl_bandit import BanditTransformerController
+    from envs.bandit_env import BanditEnv, BanditEnvVec
+    from evals import eval_bandit
+    from dpt_hip import train as tr
+    n, H = 9, 24
+    m = _width_model(64, 3, H, 5)
+    rs = np.random.RandomState(8)
+    means = rs.uniform(0, 1, (n, 5))
+    u, g = rs.uniform(size=(H, n)), rs.normal(size=(H, n))
+    calls = []
+    real = tr.rollout_bandit_generic
+
+    def spy(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+    tr.rollout_bandit_generic = spy
+    try:
+        vec = BanditEnvVec([BanditEnv(mu, H, var=0.3) for mu in means])
+        cm = eval_bandit.deploy_online_vec(vec, BanditTransformerController(m, sample=True, batch_size=n), H,
+                                           uniforms=u, noise=g)
+    finally:
+        tr.rollout_bandit_generic = real
+    vec = BanditEnvVec([BanditEnv(mu, H, var=0.3) for mu in means])
+    cm_ref = eval_bandit.deploy_online_vec(vec, BanditTransformerController(m, sample=True, batch_size=n), H,
+                                           uniforms=u, noise=g, fused=False)
+    assert calls == [1]
+    assert np.array_equal(cm, cm_ref)
