@@ -902,9 +902,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     #pragma unroll
                                 for (int r = 0; r < 4; ++r) sv[4 * h + r] = (kt * 16 + 4 * g + r <= T - 1) ? sc[r] : -INFINITY;
                             }
-                            const float mt = max_cols(fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
-                                                            fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])))) *
-                                             sl;
+                            const float mt = max_cols(vmax8(sv)) * sl;
                             // P x 2^kPExp <= 2^kPExp (mt is the exact max): fp16 two-part as in attend
                             const float bm = (float)kPExp - mt;
                             float pr[8];

@@ -202,13 +202,24 @@ __device__ inline float sum_x32(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// max of scores without fmaxf's NaN quieting: the compiler cannot see that an MFMA result is
+// canonical, so every fmaxf operand got a canonicalising v_max_f32 x, x (184 of the C3 kernel's 281
+// v_max).  llvm.maximum (IEEE 754-2019 maximum, NaN-propagating) needs no canonical inputs and
+// lowers to gfx950's v_maximum3_f32; scores are finite or -inf, never NaN, so the value is the
+// same.  (Inline-asm v_max3 is not an option: the hazard recognizer does not pad an asm read of
+// an MFMA result, which read stale accumulators.)
+__device__ inline float vmax2(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ inline float vmax3(float a, float b, float c) { return vmax2(vmax2(a, b), c); }
+__device__ inline float vmax8(const float (&v)[8]) {
+    return vmax2(vmax2(vmax2(v[0], v[1]), vmax2(v[2], v[3])), vmax2(vmax2(v[4], v[5]), vmax2(v[6], v[7])));
+}
 __device__ inline float max_x16(float v) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    return vmax2(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 __device__ inline float max_x32(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    return vmax2(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 // sum / max over the 4 lane groups (the 4 feature slices of a token column)
 __device__ inline float sum_cols(float v) { return sum_x32(sum_x16(v)); }
@@ -601,10 +612,9 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
                     }
                 }
             }
-            const float mt = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
-                                   fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
+            const float mt = vmax8(sv);
             if (__builtin_amdgcn_ballot_w64(mt > thr)) {  // wave-uniform
-                const float mn = fmaxf(m, max_cols(mt * scale));
+                const float mn = vmax2(m, max_cols(mt * scale));
                 const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
                 lsum *= corr;
 #pragma unroll
