@@ -350,7 +350,7 @@ __device__ inline float dr_tail_mlp(Smem& S, const float* W, const DrTailW& t, i
     // merge the key-tile partials (attend's convention: o / l is the output x 2^attn_ey); this lane's
     // 16 features 16 half .. 16 half + 15
     float mx = -INFINITY;
-    for (int k = 0; k < nparts; ++k) mx = fmaxf(mx, S.part_m[k]);
+    for (int k = 0; k < nparts; ++k) mx = vmax2(mx, S.part_m[k]);
     float lsum = 0.f;
     floatx4 o[4] = {};
     for (int k = 0; k < nparts; ++k) {
@@ -768,7 +768,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             // exp2 domain, as attend's m (q is at 2^attn_eq: u_proj3_w)
                             const float s0 = sdot * ((scale * 1.4426950408889634f) * exp2i(-M.attn_eq));
                             const float mt = S.l0m[tok], lt = S.l0l[tok];
-                            const float mn = fmaxf(mt, s0);
+                            const float mn = vmax2(mt, s0);
                             const float ea = __builtin_amdgcn_exp2f(mt - mn), eb = __builtin_amdgcn_exp2f(s0 - mn);
                             // 1 / l by v_rcp_f32 (1 ulp, attn_proj3_ol), with c_proj's split scale 2^attn_ey
                             const float inv = __builtin_amdgcn_rcpf(lt * ea + eb) * exp2i(M.attn_ey);

@@ -461,12 +461,21 @@ __global__ __launch_bounds__(256) void tr_mm_rows(const float* __restrict__ X, c
     constexpr int KS = K / 4;  // k-steps
     constexpr int LDB = mm_ldb(K, N);
     extern __shared__ float Bs[];  // [K][LDB]
-    for (int i = threadIdx.x; i < K * N; i += 256) {
-        const int k = i / N, n = i % N;
-        Bs[k * LDB + n] = TRANS ? W[(int64_t)n * K + k] : W[i];
+    if constexpr (TRANS) {
+        for (int i = threadIdx.x; i < K * N; i += blockDim.x) {
+            const int k = i / N, n = i % N;
+            Bs[k * LDB + n] = W[(int64_t)n * K + k];
+        }
+    } else {  // 16-B loads (N % 16 == 0: a float4 never crosses a row)
+        for (int i = threadIdx.x; i < K * N / 4; i += blockDim.x) {
+            const floatx4 v = reinterpret_cast<const floatx4*>(W)[i];
+            const int k = 4 * i / N, n = 4 * i % N;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Bs[k * LDB + n + r] = v[r];
+        }
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, kq = lane >> 4;
-    const int row0 = (blockIdx.x * 4 + wave) * 16;
+    const int row0 = (blockIdx.x * (blockDim.x >> 6) + wave) * 16;
     const int row = min(row0 + i16, R - 1);  // rows past R compute garbage that is never stored
     float a[KS];
     const floatx4* xr = reinterpret_cast<const floatx4*>(X + (int64_t)row * K + kq * KS);
@@ -832,6 +841,8 @@ static void launch_mm(const float* X, const float* W, const float* bias, const f
                       float* Y, hipStream_t st) {
     const size_t lds = sizeof(float) * K * mm_ldb(K, N);
     allow_lds(tr_mm_rows<K, N, TRANS, ACT, EPI>, lds);
+    // 4 waves (64 rows) per workgroup (1-wave workgroups for the decode rows of the generic-width
+    // rollout were measured 2x slower: each stages the whole weight matrix for 16 rows)
     hipLaunchKernelGGL((tr_mm_rows<K, N, TRANS, ACT, EPI>), dim3((R + 63) / 64), dim3(256), lds, st, X, W, bias, res,
                        aux, R, Y);
 }
@@ -1193,6 +1204,75 @@ __global__ void gen_attn_decode(const float* __restrict__ qkv, float* __restrict
     }
 }
 
+// The same for E % 4 == 0, E <= 256, with the rows read as float4: LPK lanes per key (a power of
+// two >= E / 4), 64 / LPK keys per wave-instruction, so every key row is one coalesced read.  Scores
+// are 4-term partial dots summed over the key's lanes by xor shuffles; the values accumulate per
+// lane group (keys kq, kq + KPW, ...) and the groups are summed at the end: a different fp32
+// order than gen_attn_decode (and tr_attn_fwd), the same softmax.
+template <int LPK>
+__global__ void gen_attn_decode4(const float* __restrict__ qkv, float* __restrict__ Kc, float* __restrict__ Vc, int E,
+                                 int N, int H, int pos, float* __restrict__ O) {
+    constexpr int KPW = 64 / LPK;
+    extern __shared__ float sm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int task = blockIdx.x * (blockDim.x / 64) + wave;
+    if (task >= N) return;
+    float* pr = sm + (size_t)wave * H;
+    const int E4 = E >> 2, c = lane % LPK, kq = lane / LPK;
+    const bool act = c < E4;
+    const float* row = qkv + (int64_t)task * 3 * E;
+    const floatx4* K4 = reinterpret_cast<const floatx4*>(Kc + (int64_t)task * H * E);
+    const floatx4* V4 = reinterpret_cast<const floatx4*>(Vc + (int64_t)task * H * E);
+    const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+    const floatx4 q = act ? reinterpret_cast<const floatx4*>(row)[c] : zero;
+    const floatx4 kn = act ? reinterpret_cast<const floatx4*>(row + E)[c] : zero;
+    const floatx4 vn = act ? reinterpret_cast<const floatx4*>(row + 2 * E)[c] : zero;
+    if (kq == 0 && act) {
+        reinterpret_cast<floatx4*>(Kc + (int64_t)task * H * E)[(int64_t)pos * E4 + c] = kn;
+        reinterpret_cast<floatx4*>(Vc + (int64_t)task * H * E)[(int64_t)pos * E4 + c] = vn;
+    }
+    const float scale = 1.0f / sqrtf((float)E);
+    float m = -INFINITY;
+    for (int jb = 0; jb <= pos; jb += KPW) {
+        const int j = jb + kq;
+        floatx4 k = zero;
+        if (act && j < pos) k = K4[(int64_t)j * E4 + c];
+        else if (act && j == pos) k = kn;
+        float d = fmaf(q[0], k[0], fmaf(q[1], k[1], fmaf(q[2], k[2], q[3] * k[3])));
+#pragma unroll
+        for (int x = 1; x < LPK; x <<= 1) d += __shfl_xor(d, x, 64);
+        if (j <= pos) {
+            d *= scale;
+            if (c == 0) pr[j] = d;
+            m = fmaxf(m, d);
+        }
+    }
+    m = wave_max(m);
+    wave_lds_sync();
+    float l = 0.f;
+    for (int j = lane; j <= pos; j += 64) {
+        const float p = expf(pr[j] - m);
+        pr[j] = p;
+        l += p;
+    }
+    const float inv = 1.0f / wave_sum(l);
+    wave_lds_sync();
+    floatx4 acc = zero;
+    for (int jb = 0; jb <= pos; jb += KPW) {
+        const int j = jb + kq;
+        if (!act || j > pos) continue;
+        const floatx4 v = j == pos ? vn : V4[(int64_t)j * E4 + c];
+        const float p = pr[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = fmaf(p, v[r], acc[r]);
+    }
+#pragma unroll
+    for (int x = LPK; x < 64; x <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] += __shfl_xor(acc[r], x, 64);
+    if (kq == 0 && act) reinterpret_cast<floatx4*>(O + (int64_t)task * E)[c] = acc * inv;
+}
+
 struct GenEnv {
     int N, H, A, sd, type, sample;
     int64_t first_task;
@@ -1263,13 +1343,20 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
     float* ws = a.kvcache;
     const int rows_per_block = kTrThreads / 64;
     const unsigned row_blocks = (N + rows_per_block - 1) / rows_per_block;
-    const size_t attn_lds = sizeof(float) * rows_per_block * (size_t)(H + E);
+    // the float4 attention for E % 4 == 0 up to 256 (LPK lanes per key), else the scalar one
+    const int lpk = E % 4 ? 0 : E <= 16 ? 4 : E <= 32 ? 8 : E <= 64 ? 16 : E <= 128 ? 32 : E <= 256 ? 64 : 0;
+    const void* attn_k = lpk == 4    ? (const void*)gen_attn_decode4<4>
+                         : lpk == 8  ? (const void*)gen_attn_decode4<8>
+                         : lpk == 16 ? (const void*)gen_attn_decode4<16>
+                         : lpk == 32 ? (const void*)gen_attn_decode4<32>
+                         : lpk == 64 ? (const void*)gen_attn_decode4<64>
+                                     : (const void*)gen_attn_decode;
+    const size_t attn_lds = sizeof(float) * rows_per_block * (size_t)(lpk ? H : H + E);
     if (attn_lds > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "generic bandit rollout: H=%d too long for the attention kernel", H);
         return DPT_EUNSUPPORTED;
     }
-    if (attn_lds > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)gen_attn_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)attn_lds);
+    if (attn_lds > 64 * 1024) (void)hipFuncSetAttribute(attn_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)attn_lds);
     GenEnv g{N, H, a.A, 1, a.type, a.sample, a.first_task, a.var, a.seed, a.counter, a.means, a.uniforms, a.noise,
              a.actions_out, a.rewards_out, a.arm_value_out, a.logits_out};
     const bool fast = mm_fast(E);
@@ -1294,8 +1381,16 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
             else
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE * 3)), dim3(kTrThreads), 0, st, y, blob + P.attn_w,
                                    blob + P.attn_b, nullptr, N, E, 3 * E, 0, qkv);
-            hipLaunchKernelGGL(gen_attn_decode, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv,
-                               ws + W.K + l * cache, ws + W.V + l * cache, E, N, H, h, o);
+            float* Kc = ws + W.K + l * cache;
+            float* Vc = ws + W.V + l * cache;
+            switch (lpk) {
+                case 4: hipLaunchKernelGGL(gen_attn_decode4<4>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
+                case 8: hipLaunchKernelGGL(gen_attn_decode4<8>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
+                case 16: hipLaunchKernelGGL(gen_attn_decode4<16>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
+                case 32: hipLaunchKernelGGL(gen_attn_decode4<32>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
+                case 64: hipLaunchKernelGGL(gen_attn_decode4<64>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
+                default: hipLaunchKernelGGL(gen_attn_decode, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o);
+            }
             if (fast)
                 mm(E, kMmProj, o, blob + P.proj_w, blob + P.proj_b, x, nullptr, N, x2, st);
             else

@@ -39,7 +39,8 @@ def main():
     N, H, L = int(os.environ.get("GT_N", 4096)), int(os.environ.get("GT_H", 500)), 4
     means = np.random.RandomState(0).uniform(0, 1, (N, 5))
     out = {"N": N, "H": H, "L": L}
-    for E in (16, 32, 48, 64, 128):
+    widths = [int(w) for w in os.environ.get("GT_E", "16,32,48,64,128").split(",")]
+    for E in widths:
         m = model(E, L, H)
         t = timed(lambda: tr.rollout_bandit_generic(m, means, H, 0.3, True, seed=1))
         out[f"generic_E{E}"] = {"s": t, "env_steps_per_s": N * H / t}
@@ -48,6 +49,9 @@ def main():
             t = timed(lambda: dm.rollout_bandit(means, H, 0.3, True, seed=1))
             out["fused_E32"] = {"s": t, "env_steps_per_s": N * H / t}
         print(json.dumps({k: v for k, v in out.items() if k.endswith(f"E{E}")}), file=sys.stderr, flush=True)
+    if os.environ.get("GT_PER_STEP", "1") != "1":
+        print(json.dumps(out))
+        return
     # the per-step path at width 64 (what the generic rollout replaces), short horizon
     from ctrls.ctrl_bandit import BanditTransformerController
     from envs.bandit_env import BanditEnv, BanditEnvVec

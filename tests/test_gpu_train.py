@@ -448,13 +448,15 @@ def _width_model(E, L, H, seed):
 
 
 @pytest.mark.parametrize("E,L,bern,sample", [(16, 3, False, True), (48, 2, False, True), (64, 4, True, True),
-                                             (64, 2, False, False), (32, 2, False, True)])
+                                             (64, 2, False, False), (32, 2, False, True), (18, 2, False, True),
+                                             (128, 2, False, True)])
 def test_generic_width_rollout_vs_oracle(E, L, bern, sample):
     """dpt_rollout_bandit_generic (the bandit online loop at any width: exact K/V-cache decode, one
     step for all tasks at a time) against the float64 oracle's re-forward-every-step rollout fed the
     same draws: logits within 1e-5 at every step, actions / rewards / arm values exactly.  Widths on
-    the row kernels (48) and on the matrix-core forms (16, 32, 64), Gaussian and Bernoulli rewards,
-    sampling and greedy; 37 tasks (a partial row block)."""
+    the row kernels (18, 48, 128) and on the matrix-core forms (16, 32, 64); the float4 attention
+    (E % 4 == 0) and the scalar one (18); Gaussian and Bernoulli rewards, sampling and greedy; 37
+    tasks (a partial row block)."""
     from dpt_hip import train as tr
     from oracle import dpt_oracle as O
     N, H = 37, 40
