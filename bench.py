@@ -291,10 +291,19 @@ def darkroom_workload(L, H, Heps, N, first, count, n_total, dist, memo):
         dense = int(fw[0]) * parts[0][0] + int(fw[1:].sum()) * parts[1][0]
         peak = flops / (dense / X3_PEAK_TF + (flops - dense) / FP32_MFMA_PEAK_TF)
         traffic = None  # HBM bytes read per launch (rocprofv3 FETCH_SIZE x2, scripts/profile_darkroom.sh)
+        issue = None  # the issue roofline from the same PMC pass (scripts/pmc_darkroom.py)
         pmc = os.path.join(ROOT, "profiles", "pmc_rollout_darkroom.json")
         if os.path.exists(pmc) and count == 4096 and H == 100:
-            traffic = json.load(open(pmc)).get("hbm_fetch_bytes_corrected")
-        return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+            pj = json.load(open(pmc))
+            traffic = pj.get("hbm_fetch_bytes_corrected")
+            if "simd_valu_or_mfma_busy_frac" in pj:
+                issue = {k: pj[k] for k in ("simd_valu_issue_frac", "mfma_pipe_busy_frac", "valu_mfma_coexec_frac",
+                                            "simd_valu_or_mfma_busy_frac", "avg_waves_per_simd")}
+                issue["note"] = ("fractions of SIMD cycles from the committed PMC pass of this kernel at this "
+                                 "config (profiles/pmc_rollout_darkroom.json): VALU issue, MFMA pipe busy, both, "
+                                 "either -- the kernel is issue-bound, so this, not the MFMA-only peak, is its "
+                                 "binding roofline")
+        return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "issue": issue,
                 "frac": achieved / peak, "traffic": traffic,
                 "peak_fp32_mfma": FP32_MFMA_PEAK_TF, "frac_of_fp32_mfma": achieved / FP32_MFMA_PEAK_TF,
                 "matrix_flops_per_launch": dense,

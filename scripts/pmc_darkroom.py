@@ -46,6 +46,15 @@ def main(prof, out):
         res["lds_bank_conflict_frac_of_lds_cycles"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
     if "SQ_VALU_MFMA_COEXEC_CYCLES" in c:
         res["valu_mfma_coexec_frac"] = c["SQ_VALU_MFMA_COEXEC_CYCLES"] / simd_cycles
+    if "SQ_ACTIVE_INST_VALU" in c:
+        # the issue roofline: SIMD cycles with VALU issue (quad-cycles x 4, summed over the waves of
+        # a SIMD, which issue one VALU instruction at a time), with the MFMA pipe busy, and with
+        # either (the co-executed cycles counted once)
+        valu = 4 * c["SQ_ACTIVE_INST_VALU"] / simd_cycles
+        res["simd_valu_issue_frac"] = valu
+        res["simd_valu_or_mfma_busy_frac"] = valu + res["mfma_pipe_busy_frac"] - res.get("valu_mfma_coexec_frac", 0)
+    if wc:
+        res["avg_waves_per_simd"] = 4 * wc / simd_cycles
     res["note"] = ("SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles (guide, cycle constants); "
                    "SQ_VALU_MFMA_BUSY_CYCLES counts cycles, summed over the 1024 SIMDs (16 per "
                    "v_mfma_f32_16x16x32_f16); GRBM_GUI_ACTIVE is summed over the 8 XCDs")

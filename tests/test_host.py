@@ -135,3 +135,28 @@ def test_train_desc_rejects_bad_dropout():
     d = tr.desc(2, 32, 1, 5, 40, 3, 9, dropout=0.5, seed=1)
     _lib.check(lib.dpt_train_blob_numel(ctypes.byref(d), ctypes.byref(n)))
     assert n.value > 0
+
+
+def test_generic_rollout_workspace_and_argument_checks():
+    """dpt_rollout_bandit_generic_workspace_numel: K and V caches [L][N][H][E] plus the per-step
+    rows (host-side, no GPU); a desc with dropout is rejected before any device work, and N = 0
+    is a no-op."""
+    import ctypes
+    import pytest
+    from dpt_hip import _lib
+    from dpt_hip import train as tr
+    lib = _lib.load()
+    L, E, A, N, H = 3, 48, 5, 10, 7
+    d = tr.desc(L, E, 1, A, 4 * (1 + H), 1, 1)
+    n = ctypes.c_int64()
+    _lib.check(lib.dpt_rollout_bandit_generic_workspace_numel(ctypes.byref(d), N, H, ctypes.byref(n)))
+    cache = 2 * L * N * H * E
+    rows = N * (4 * E + 2 + 3 * E + 4 * E + A + (2 + A + 1))  # x x2 y o, st, qkv, h, logits, token
+    assert cache + rows <= n.value <= cache + rows + 4 * 12
+    args = _lib.BanditRolloutArgs()
+    args.N, args.H, args.A = 0, H, A
+    _lib.check(lib.dpt_rollout_bandit_generic(ctypes.byref(d), ctypes.c_void_p(8), ctypes.byref(args), None))
+    dd = tr.desc(L, E, 1, A, 4 * (1 + H), 1, 1, dropout=0.1, seed=3)
+    args.N = N
+    with pytest.raises(ValueError, match="dropout"):
+        _lib.check(lib.dpt_rollout_bandit_generic(ctypes.byref(dd), ctypes.c_void_p(8), ctypes.byref(args), None))
