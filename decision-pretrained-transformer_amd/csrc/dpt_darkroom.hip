@@ -753,18 +753,28 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             va = ld4(&S.v0[4 * g]);
                             vb = ld4(&S.v0[16 + 4 * g]);
                         }
-                        float o[2][8];
+                        float o[2][8], sd[2] = {0.f, 0.f};
+    #pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            if (j >= NBR) break;
+    #pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                sd[j] = fmaf(q[j][r], ka[r], sd[j]);
+                                sd[j] = fmaf(q[j][4 + r], kc[r], sd[j]);
+                            }
+                        }
+                        if constexpr (NBC == 2) {
+                            sum_cols2(sd[0], sd[1]);
+                        } else {
+    #pragma unroll
+                            for (int j = 0; j < 2; ++j)
+                                if (j < NBR) sd[j] = sum_cols(sd[j]);
+                        }
     #pragma unroll
                         for (int j = 0; j < 2; ++j) {
                             if (j >= NBR) break;
                             const int tok = qb[j] * 16 + (lane & 15);
-                            float sdot = 0.f;
-    #pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                sdot = fmaf(q[j][r], ka[r], sdot);
-                                sdot = fmaf(q[j][4 + r], kc[r], sdot);
-                            }
-                            sdot = sum_cols(sdot);
+                            const float sdot = sd[j];
                             // exp2 domain, as attend's m (q is at 2^attn_eq: u_proj3_w)
                             const float s0 = sdot * ((scale * 1.4426950408889634f) * exp2i(-M.attn_eq));
                             const float mt = S.l0m[tok], lt = S.l0l[tok];
@@ -844,11 +854,20 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     #ifndef DPT_DR_SKIP_ATTN
                     if (NBR > 0) {
                         float o[2][8], l[2];
+                        if constexpr (NBC == 2 && kSplitV) {  // the two blocks' l reduced together (sum_cols2)
     #pragma unroll
-                        for (int j = 0; j < 2; ++j) {
-                            if (j >= NBR) break;
-                            float m;
-                            attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, diag_bias);
+                            for (int j = 0; j < 2; ++j) {
+                                float m;
+                                attend<decltype(S.kv), false>(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, diag_bias);
+                            }
+                            sum_cols2(l[0], l[1]);
+                        } else {
+    #pragma unroll
+                            for (int j = 0; j < 2; ++j) {
+                                if (j >= NBR) break;
+                                float m;
+                                attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, diag_bias);
+                            }
                         }
                         DR_BLOCKS(attn_proj3_ol<NB>(W, split0.layer(layer), o, l, x, M));
                     }

@@ -223,6 +223,20 @@ __device__ inline float max_x32(float v) {
 }
 // sum / max over the 4 lane groups (the 4 feature slices of a token column)
 __device__ inline float sum_cols(float v) { return sum_x32(sum_x16(v)); }
+// sum_cols of two values at once (a wave's two blocks): the first swap exchanges a's odd rows with
+// b's even rows, so one add leaves a's row-pair sums in rows 0 / 2 and b's in rows 1 / 3; the
+// xor-32 exchange completes both totals (a's in rows 0 / 2, b's in 1 / 3) and a last xor-16
+// exchange hands every lane both.  Three permlanes and two adds instead of four and four, and
+// the same sums in the same order as sum_cols: bit-identical.
+__device__ inline void sum_cols2(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    const float s = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    const float u = __uint_as_float(t[0]) + __uint_as_float(t[1]);
+    const auto w = __builtin_amdgcn_permlane16_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+    a = __uint_as_float(w[0]);
+    b = __uint_as_float(w[1]);
+}
 __device__ inline float max_cols(float v) { return max_x32(max_x16(v)); }
 
 __device__ inline void bar_lds() {
@@ -254,6 +268,48 @@ __device__ inline void ln_cols(const float (&v)[8], float (&out)[8], const float
     const fx2 o3 = __builtin_elementwise_fma(d3 * rr, fx2{g1[2], g1[3]}, fx2{b1[2], b1[3]});
     out[0] = o0.x; out[1] = o0.y; out[2] = o1.x; out[3] = o1.y;
     out[4] = o2.x; out[5] = o2.y; out[6] = o3.x; out[7] = o3.y;
+}
+
+// ln_cols of a wave's two blocks with their column reductions paired (sum_cols2): the same
+// arithmetic, bit-identical, three permlanes per statistic for both blocks instead of four
+__device__ inline void ln_cols2(const float (&v)[2][8], float (&out)[2][8], const float* __restrict__ gam,
+                                const float* __restrict__ bet) {
+    typedef float fx2 __attribute__((ext_vector_type(2)));
+    const int g = lane_id() >> 4;
+    fx2 d[2][4];
+    float mean[2], var[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const fx2 v0 = {v[j][0], v[j][1]}, v1 = {v[j][2], v[j][3]}, v2 = {v[j][4], v[j][5]}, v3 = {v[j][6], v[j][7]};
+        const fx2 sa = (v0 + v1) + (v2 + v3);
+        mean[j] = sa.x + sa.y;
+    }
+    sum_cols2(mean[0], mean[1]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const float mj = mean[j] * (1.0f / kE);
+        const fx2 mm = {mj, mj};
+        d[j][0] = fx2{v[j][0], v[j][1]} - mm;
+        d[j][1] = fx2{v[j][2], v[j][3]} - mm;
+        d[j][2] = fx2{v[j][4], v[j][5]} - mm;
+        d[j][3] = fx2{v[j][6], v[j][7]} - mm;
+        const fx2 qa = (d[j][0] * d[j][0] + d[j][1] * d[j][1]) + (d[j][2] * d[j][2] + d[j][3] * d[j][3]);
+        var[j] = qa.x + qa.y;
+    }
+    sum_cols2(var[0], var[1]);
+    const floatx4 g0 = ld4(gam + 4 * g), g1 = ld4(gam + 16 + 4 * g);
+    const floatx4 b0 = ld4(bet + 4 * g), b1 = ld4(bet + 16 + 4 * g);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const float rstd = __builtin_amdgcn_rsqf(var[j] * (1.0f / kE) + 1e-5f);
+        const fx2 rr = {rstd, rstd};
+        const fx2 o0 = __builtin_elementwise_fma(d[j][0] * rr, fx2{g0[0], g0[1]}, fx2{b0[0], b0[1]});
+        const fx2 o1 = __builtin_elementwise_fma(d[j][1] * rr, fx2{g0[2], g0[3]}, fx2{b0[2], b0[3]});
+        const fx2 o2 = __builtin_elementwise_fma(d[j][2] * rr, fx2{g1[0], g1[1]}, fx2{b1[0], b1[1]});
+        const fx2 o3 = __builtin_elementwise_fma(d[j][3] * rr, fx2{g1[2], g1[3]}, fx2{b1[2], b1[3]});
+        out[j][0] = o0.x; out[j][1] = o0.y; out[j][2] = o1.x; out[j][3] = o1.y;
+        out[j][4] = o2.x; out[j][5] = o2.y; out[j][6] = o3.x; out[j][7] = o3.y;
+    }
 }
 
 // gelu_fast on a pair: the same operations in the same order on v_pk_{mul,fma,add}_f32 (each
@@ -318,8 +374,12 @@ __device__ inline Split2 gelu_split(const floatx4& a, const floatx4& b, const Ge
 
 template <int NB>
 __device__ inline void ln_n(const float (&x)[2][8], float (&xn)[2][8], const float* gam, const float* bet) {
+    if constexpr (NB == 2) {
+        ln_cols2(x, xn, gam, bet);
+    } else {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) ln_cols(x[j], xn[j], gam, bet);
+        for (int j = 0; j < NB; ++j) ln_cols(x[j], xn[j], gam, bet);
+    }
 }
 
 // x += (a | b) x down, down an exact power of two: one packed fma per pair (the product is exact,
@@ -536,7 +596,9 @@ __device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const fl
 // 2^(attn_ey + kPExp) sum_s 2^(s-m) v_s (C-layout), all in the exp2 domain: s and m are the
 // scores times log2(e) (folded into the scale), so each probability is one v_exp_f32.  o / l is
 // the attention output at the scale of the c_proj product's B operand (attn_proj3_ol).
-template <class KV>
+// kReduceL = false (split-value form): lsum is returned as this lane's partial, for a caller that
+// reduces two blocks' columns at once (sum_cols2)
+template <class KV, bool kReduceL = true>
 __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
                               float& lsum, float (&o)[8], const ModelView& M, const float* diag_bias = nullptr) {
     // The running reference m of a token column moves only when a key tile holds a
@@ -650,7 +712,7 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
         }
         for (; kb < kb_last; kb += 2) pair(kb, std::false_type{});
         pair(kb_last, std::true_type{});
-        lsum = sum_cols(lsum);
+        if constexpr (kReduceL) lsum = sum_cols(lsum);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             o[r] = o0[r];
