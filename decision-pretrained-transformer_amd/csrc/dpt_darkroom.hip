@@ -180,7 +180,18 @@ struct DarkroomParams {
 // o is the layer-0 episode partial (the prologue's attention over keys 1..t).
 // The workspace starts with the per-state table (kDrTab floats), then the task caches, at the
 // stride of the launch's geometry (dpt_darkroom_workspace_numel_window).
-constexpr int kDrTabPerState = 2 * 4 * 8;
+// DPT_DR_L0LIN (default): layer 0's attention output enters c_proj linearly.  Per token t the
+// merged output is o_t = (1 - a_t) o'_t + a_t v0 (o'_t: the episode's normalised partial over keys
+// 1..t, v0: the query token's value, a_t = 1 / (1 + l_t 2^(m_t - s0_t)), s0_t = q_t . k0), so
+//   x_t + c_proj(o_t) = A_t + a_t (V0 - C_t),  C_t = Wvp o'_t + bvp,  A_t = x_t + C_t,  V0 = Wvp v0 + bvp.
+// The episode prologue stores A and C in the workspace (slots x and o), the state table holds V0, and a
+// step's layer 0 is the score, one exp and one rcp per token and a packed sub + fma per value instead of
+// the merge, the split of o and c_proj's six MFMAs.  Same algebra, other fp32 rounding.
+#ifndef DPT_DR_L0LIN
+#define DPT_DR_L0LIN 1
+#endif
+// per state: [x | y | V0][g][8] (the query token's layer-0 input, its LN1 output, Wvp y + bvp)
+constexpr int kDrTabPerState = (DPT_DR_L0LIN ? 3 : 2) * 4 * 8;
 constexpr int kDrTab = kMemoStates * kDrTabPerState;
 constexpr int kDrMaxWaves = 16;
 template <int NW>
@@ -198,6 +209,31 @@ __device__ inline void ws_load(const float* d, float (&v)[8]) {
     for (int r = 0; r < 4; ++r) {
         v[r] = a[r];
         v[4 + r] = b[r];
+    }
+}
+
+// DPT_DR_L0LIN episode prologue: c = Wvp o' + bvp from attend's (o, l) (o / l = o' x 2^attn_ey), at true
+// scale, and x += c (A); the token-0 column (no key in 1..0: l = 0) gets c = 0
+template <int NB>
+__device__ inline void l0_cproj(const float* W, const FragSrc3& f3, float (&o)[2][8], const float (&l)[2],
+                                float (&x)[2][8], const int (&qb)[2], const ModelView& M) {
+    const int lane = lane_id(), g = lane >> 4;
+    const int vo = FragSrc3::lane_off();
+    const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
+    const floatx4 b0 = ld4(W + PL::proj_b + 4 * g), b1 = ld4(W + PL::proj_b + 16 + 4 * g);  // scaled (PL)
+    const float down = exp2i(-(M.attn_ew + M.attn_ey));
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const Split2 os = split2(o[j], l[j] > 0.f ? __builtin_amdgcn_rcpf(l[j]) : 0.f);
+        const floatx4 c0 = mfma_x3(w0, os, b0), c1 = mfma_x3(w1, os, b1);
+        const bool tok0 = qb[j] == 0 && (lane & 15) == 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            o[j][r] = tok0 ? 0.f : c0[r] * down;
+            o[j][4 + r] = tok0 ? 0.f : c1[r] * down;
+            x[j][r] += o[j][r];
+            x[j][4 + r] += o[j][4 + r];
+        }
     }
 }
 
@@ -277,6 +313,22 @@ __global__ void __launch_bounds__(64) state_tables_kernel(ModelView M, int dim, 
         ws_store(d, x);
         ws_store(d + 32, y);
     }
+#if DPT_DR_L0LIN
+    // V0 = Wvp y + bvp (fp32 fma chain per feature), stored in the same [g][8] lane order
+    __shared__ float ys[kE];
+    if ((lane & 15) == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ys[16 * (k >> 2) + 4 * g + (k & 3)] = y[k];
+    }
+    __syncthreads();
+    if (lane < kE) {
+        const float* F = M.l0;  // layer 0's folded attention
+        float v = F[L0Off::bvp + lane];
+        for (int k = 0; k < kE; ++k) v = fmaf(F[L0Off::Wvp + k * kE + lane], ys[k], v);
+        const int gf = (lane & 15) >> 2, kk = 4 * (lane >> 4) + (lane & 3);
+        tab[(size_t)s * kDrTabPerState + 64 + gf * 8 + kk] = v;
+    }
+#endif
 }
 
 // LDS stores of this wave visible to its own later loads (waits for them: no barrier, one wave)
@@ -572,11 +624,38 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     if (j >= NBR) break;
-                    ws_store(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
+                    if (!(DPT_DR_L0LIN && kTab)) ws_store(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
                     ws_store(l0_cache<NW>(p, task, 1, qb[j]), q[j]);
                 }
             }
             bar_lds();
+#if DPT_DR_L0LIN
+            if constexpr (kTab) {
+                // the partials through c_proj once per episode: C = Wvp o' + bvp, A = x + C (the token-0
+                // column has no partial: C = 0 there, and its A comes from the state table)
+                float o[2][8], l[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (j >= NBR) break;
+                    float m;
+                    attend(S.kv, q[j], qb[j], 1, scale, m, l[j], o[j], M, diag_bias);
+                    const int lane = lane_id();
+                    if (lane < 16) {
+                        S.l0m[qb[j] * 16 + lane] = m;
+                        S.l0l[qb[j] * 16 + lane] = l[j] * exp2i(-kPExp);
+                    }
+                }
+                DR_BLOCKS(l0_cproj<NB>(P, split0, o, l, x, qb, M));
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (j >= NBR) break;
+                    ws_store(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
+                    ws_store(l0_cache<NW>(p, task, 2, qb[j]), o[j]);
+                }
+                __syncthreads();
+                return;
+            }
+#endif
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 if (j >= NBR) break;
@@ -737,6 +816,58 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         bar_lds();
                     }
                     DR_STAMP(0);
+#if DPT_DR_L0LIN
+                    if (kTab && NBR > 0) {
+                        // x = A + a (V0 - C) per token column (DPT_DR_L0LIN): x holds A, the workspace's o slot C
+                        const int lane = lane_id(), g = lane >> 4;
+                        const float* tr = p.tab + (size_t)(sx * p.dim + sy) * kDrTabPerState + 8 * g;
+                        const floatx4 ka = ld4(tr + 32), kc = ld4(tr + 36);
+                        const floatx4 va = ld4(tr + 64), vb = ld4(tr + 68);
+                        float sd[2] = {0.f, 0.f};
+    #pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            if (j >= NBR) break;
+    #pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                sd[j] = fmaf(q[j][r], ka[r], sd[j]);
+                                sd[j] = fmaf(q[j][4 + r], kc[r], sd[j]);
+                            }
+                        }
+                        if constexpr (NBC == 2) {
+                            sum_cols2(sd[0], sd[1]);
+                        } else {
+    #pragma unroll
+                            for (int j = 0; j < 2; ++j)
+                                if (j < NBR) sd[j] = sum_cols(sd[j]);
+                        }
+    #pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            if (j >= NBR) break;
+                            const int tok = qb[j] * 16 + (lane & 15);
+                            const float s0 = sd[j] * ((scale * 1.4426950408889634f) * exp2i(-M.attn_eq));
+                            const float mt = S.l0m[tok], lt = S.l0l[tok];
+                            // a = 1 / (1 + l 2^(m - s0)): 1 for the token-0 column (l = 0, m = -inf)
+                            const float a = __builtin_amdgcn_rcpf(fmaf(lt, __builtin_amdgcn_exp2f(mt - s0), 1.0f));
+                            const float* pc = l0_cache<NW>(p, task, 2, qb[j]);
+                            const floatx4 ca = ld4(pc), cb = ld4(pc + 4);
+                            const floatx2 a2 = {a, a};
+    #pragma unroll
+                            for (int r = 0; r < 4; r += 2) {
+                                const floatx2 t0 = __builtin_elementwise_fma(
+                                    a2, floatx2{va[r], va[r + 1]} - floatx2{ca[r], ca[r + 1]}, floatx2{x[j][r], x[j][r + 1]});
+                                const floatx2 t1 = __builtin_elementwise_fma(
+                                    a2, floatx2{vb[r], vb[r + 1]} - floatx2{cb[r], cb[r + 1]}, floatx2{x[j][4 + r], x[j][5 + r]});
+                                x[j][r] = t0.x;
+                                x[j][r + 1] = t0.y;
+                                x[j][4 + r] = t1.x;
+                                x[j][5 + r] = t1.y;
+                            }
+                        }
+                        float xn[2][8];
+                        DR_BLOCKS((ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                                   mlp3_n<NB>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
+                    } else
+#endif
                     if (NBR > 0) {
                         // merge key 0 into the cached partial of every token column
                         const int lane = lane_id(), g = lane >> 4;
