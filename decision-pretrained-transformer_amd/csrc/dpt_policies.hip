@@ -11,6 +11,7 @@
 // pairwise order each step: means, bounds and therefore action indices are
 // bit-identical to the reference for the same draws (LinUCB: see linucb_choose).
 #include "dpt_common.h"
+#include "dpt_linucb.h"
 
 namespace dpt {
 
@@ -67,196 +68,6 @@ __device__ double pw_sum(const double* x, size_t stride, int n) {
     return lvl2(x, a) + lvl2(x + (size_t)a * stride, n - a);
 }
 
-constexpr int kMaxD = 8;  // LinUCB feature dimension (lin_d) supported
-
-// ----------------------------------------------------------------------------- LinUCB
-// LinUCBPolicy.act_numpy_vec (ctrls/ctrl_bandit.py:503-526) rebuilds its estimate from the
-// whole context every step with numpy:
-//   X = arms[argmax(actions)]; cov = I + X^T X; cov_inv = np.linalg.inv(cov)
-//   theta = (cov_inv @ X^T) @ r; value_k = theta @ arm_k + c * sqrt(arm_k @ cov_inv @ arm_k)
-// numpy hands each product to its BLAS (OpenBLAS, scipy-openblas 0.3.29 in the image the
-// fixtures were recorded in) and each of those kernels has its own, fixed rounding order.  The
-// lane restates those orders (established against numpy on the recording host:
-// tests/golden/gen_golden.py linucb fixtures), so at lin_d = 2 every value -- and so every arm
-// index -- is bit-identical to the reference's:
-//   X^T X  dsyrk: per entry one fma chain over the context, K-blocked like the level-3 driver
-//          (blocks of GEMM_Q = 384, a remainder between Q and 2Q split in halves), C += block;
-//   inv    dgesv(cov, I): getf2 (partial pivot by first max |.|, l = a10 * (1/a00), u11 =
-//          a11 - l u01 unfused) then getrs (unit-lower forward step, upper back step with the
-//          reciprocal diagonal, the off-diagonal term fused);
-//   cov_inv @ X^T  dgemm with K = d: per entry an fma chain from 0;
-//   (.) @ r  dgemv_t: 2048-row blocks of the first n - n%4 rows, two interleaved unfused
-//          accumulators per block summed into y, then the n%4 tail rows contracted into y;
-//   theta @ arm, arm @ cov_inv, (.) @ arm  ddot / dgemv_n with d rows: fma chains from 0.
-// For lin_d > 2 the inverse is a plain partial-pivot LU and the d-column kernels are not
-// restated (OpenBLAS switches to its 4-column microkernels), so indices there are equal up to
-// near-ties of the arm values.
-constexpr int kSyrkQ = 384;
-__host__ __device__ inline int syrk_block(int ls, int n) {
-    const int ml = n - ls;
-    if (ml >= 2 * kSyrkQ) return kSyrkQ;
-    if (ml > kSyrkQ) return (ml + 1) / 2;
-    return ml;
-}
-
-// dgemv_t row reduction y = sum_k m(k) r(k) over k < n in OpenBLAS's order (see above)
-template <class Mk, class Rk>
-__host__ __device__ inline double gemv_t_sum(Mk m, Rk r, int n) {
-    const int m3 = n & 3, m1 = n - m3;
-    double y = 0.0;
-    for (int s0 = 0; s0 < m1; s0 += 2048) {
-        const int nb = min(2048, m1 - s0);
-        double l0 = 0.0, l1 = 0.0;
-        int k = s0;
-        // the products of 8 rows first (independent loads in flight), then the two chains in order
-        for (; k + 8 <= s0 + nb; k += 8) {
-            double pr[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) pr[t] = m(k + t) * r(k + t);
-#pragma unroll
-            for (int t = 0; t < 8; t += 2) {
-                l0 = l0 + pr[t];
-                l1 = l1 + pr[t + 1];
-            }
-        }
-        for (; k < s0 + nb; k += 2) {
-            l0 = l0 + m(k) * r(k);
-            l1 = l1 + m(k + 1) * r(k + 1);
-        }
-        y = y + (l0 + l1);
-    }
-    if (m3 == 1) {
-        y = fma(m(m1), r(m1), y);
-    } else if (m3 == 2) {
-        y = y + fma(m(m1), r(m1), m(m1 + 1) * r(m1 + 1));
-    } else if (m3 == 3) {
-        y = y + fma(m(m1 + 2), r(m1 + 2), fma(m(m1), r(m1), m(m1 + 1) * r(m1 + 1)));
-    }
-    return y;
-}
-
-// One LinUCB decision from the n-transition context (arm indices act(k), rewards rew(k), time
-// order).  arms (A, d) row-major.
-template <class Act, class Rew>
-__host__ __device__ int linucb_choose(Act act, Rew rew, int n, const double* arms, int A, int d, double c) {
-    // cov = I + X^T X (upper triangle, mirrored like numpy's syrk result)
-    double cov[kMaxD * kMaxD];
-    for (int p = 0; p < d; ++p)
-        for (int q = p; q < d; ++q) cov[p * kMaxD + q] = 0.0;
-    for (int ls = 0; ls < n;) {
-        const int ml = syrk_block(ls, n);
-        double acc[kMaxD * kMaxD];
-        for (int p = 0; p < d; ++p)
-            for (int q = p; q < d; ++q) acc[p * kMaxD + q] = 0.0;
-        for (int k0 = ls; k0 < ls + ml; k0 += 8) {
-            // the arm indices of 8 transitions loaded together, then the fma chains in order
-            const int kn = min(8, ls + ml - k0);
-            int ak[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) ak[t] = t < kn ? act(k0 + t) : 0;
-            for (int t = 0; t < kn; ++t) {
-                const double* x = arms + (size_t)ak[t] * d;
-                for (int p = 0; p < d; ++p)
-                    for (int q = p; q < d; ++q) acc[p * kMaxD + q] = fma(x[p], x[q], acc[p * kMaxD + q]);
-            }
-        }
-        for (int p = 0; p < d; ++p)
-            for (int q = p; q < d; ++q) cov[p * kMaxD + q] = cov[p * kMaxD + q] + acc[p * kMaxD + q];
-        ls += ml;
-    }
-    for (int p = 0; p < d; ++p) {
-        cov[p * kMaxD + p] = 1.0 + cov[p * kMaxD + p];
-        for (int q = p + 1; q < d; ++q) {
-            cov[p * kMaxD + q] = 0.0 + cov[p * kMaxD + q];
-            cov[q * kMaxD + p] = cov[p * kMaxD + q];
-        }
-    }
-    double ci[kMaxD * kMaxD];
-    if (d == 2) {
-        const bool sw = fabs(cov[kMaxD]) > fabs(cov[0]);  // idamax: the first max
-        const double a00 = sw ? cov[kMaxD] : cov[0], a01 = sw ? cov[kMaxD + 1] : cov[1];
-        const double a10 = sw ? cov[0] : cov[kMaxD], a11 = sw ? cov[1] : cov[kMaxD + 1];
-        const double l = a10 * (1.0 / a00);
-        const double u11 = a11 - l * a01;
-        const double r00 = 1.0 / a00, r11 = 1.0 / u11;
-        for (int col = 0; col < 2; ++col) {
-            const double b0 = (sw ? 1 : 0) == col ? 1.0 : 0.0, b1 = (sw ? 0 : 1) == col ? 1.0 : 0.0;
-            const double y1 = b1 - l * b0;
-            const double x1 = y1 * r11;
-            const double x0 = fma(-a01, x1, b0) * r00;
-            ci[col] = x0;
-            ci[kMaxD + col] = x1;
-        }
-    } else {
-        // LU with partial pivoting (reciprocal pivots, LAPACK style), then the d unit columns
-        double lu[kMaxD * kMaxD];
-        int piv[kMaxD];
-        for (int k = 0; k < d * kMaxD; ++k) lu[k] = cov[k];
-        for (int j = 0; j < d; ++j) {
-            int pr = j;
-            for (int p = j + 1; p < d; ++p)
-                if (fabs(lu[p * kMaxD + j]) > fabs(lu[pr * kMaxD + j])) pr = p;
-            piv[j] = pr;
-            if (pr != j)
-                for (int q = 0; q < d; ++q) {
-                    const double t = lu[j * kMaxD + q];
-                    lu[j * kMaxD + q] = lu[pr * kMaxD + q];
-                    lu[pr * kMaxD + q] = t;
-                }
-            const double rp = 1.0 / lu[j * kMaxD + j];
-            for (int p = j + 1; p < d; ++p) {
-                const double lf = lu[p * kMaxD + j] * rp;
-                lu[p * kMaxD + j] = lf;
-                for (int q = j + 1; q < d; ++q) lu[p * kMaxD + q] = lu[p * kMaxD + q] - lf * lu[j * kMaxD + q];
-            }
-        }
-        for (int col = 0; col < d; ++col) {
-            double b[kMaxD];
-            for (int p = 0; p < d; ++p) b[p] = p == col ? 1.0 : 0.0;
-            for (int j = 0; j < d; ++j) {
-                const double t = b[j];
-                b[j] = b[piv[j]];
-                b[piv[j]] = t;
-            }
-            for (int p = 1; p < d; ++p)
-                for (int q = 0; q < p; ++q) b[p] = fma(-lu[p * kMaxD + q], b[q], b[p]);
-            for (int p = d - 1; p >= 0; --p) {
-                double t = b[p];
-                for (int q = p + 1; q < d; ++q) t = fma(-lu[p * kMaxD + q], b[q], t);
-                b[p] = t * (1.0 / lu[p * kMaxD + p]);
-            }
-            for (int p = 0; p < d; ++p) ci[p * kMaxD + col] = b[p];
-        }
-    }
-    // theta = (cov_inv @ X^T) @ r
-    double theta[kMaxD];
-    for (int p = 0; p < d; ++p) {
-        const double* cp = ci + p * kMaxD;
-        auto mk = [&](int k) {
-            const double* x = arms + (size_t)act(k) * d;
-            double acc = cp[0] * x[0];
-            for (int j = 1; j < d; ++j) acc = fma(cp[j], x[j], acc);
-            return acc;
-        };
-        theta[p] = gemv_t_sum(mk, rew, n);
-    }
-    int best_k = 0;
-    double best = -INFINITY;
-    for (int k = 0; k < A; ++k) {
-        const double* x = arms + (size_t)k * d;
-        double tv = theta[0] * x[0];
-        for (int p = 1; p < d; ++p) tv = fma(theta[p], x[p], tv);
-        double qv = 0.0;
-        for (int j = 0; j < d; ++j) {
-            double w = ci[j] * x[0];
-            for (int p = 1; p < d; ++p) w = fma(ci[p * kMaxD + j], x[p], w);
-            qv = j == 0 ? w * x[0] : fma(w, x[j], qv);
-        }
-        const double v = tv + c * sqrt(qv);
-        if (v > best) { best = v; best_k = k; }
-    }
-    return best_k;
-}
 
 struct PolicyParams {
     int N, H, A, policy, online, type, sample, d, C, step0;
@@ -597,78 +408,22 @@ __global__ __launch_bounds__(64) void rollout_policy_wave_kernel(PolicyParams P)
                     if (p != q) cov[q * kMaxD + p] = 0.0 + cv;
                 }
                 __syncthreads();
-                if (lane == 0) {  // np.linalg.inv (linucb_choose's orders)
-                    if (d == 2) {
-                        const bool sw = fabs(cov[kMaxD]) > fabs(cov[0]);  // idamax: the first max
-                        const double a00 = sw ? cov[kMaxD] : cov[0], a01 = sw ? cov[kMaxD + 1] : cov[1];
-                        const double a10 = sw ? cov[0] : cov[kMaxD], a11 = sw ? cov[1] : cov[kMaxD + 1];
-                        const double l = a10 * (1.0 / a00);
-                        const double u11 = a11 - l * a01;
-                        const double r00 = 1.0 / a00, r11 = 1.0 / u11;
-                        for (int col = 0; col < 2; ++col) {
-                            const double b0 = (sw ? 1 : 0) == col ? 1.0 : 0.0, b1 = (sw ? 0 : 1) == col ? 1.0 : 0.0;
-                            const double y1 = b1 - l * b0;
-                            const double x1 = y1 * r11;
-                            const double x0 = fma(-a01, x1, b0) * r00;
-                            ci[col] = x0;
-                            ci[kMaxD + col] = x1;
-                        }
-                    } else {
-                        // LU in place in cov (no longer needed), pivots and the solve vector in the
-                        // LDS words LinUCB does not use otherwise (no private arrays: no scratch)
-                        double* lu = cov;
-                        int* piv = freq;
-                        double* b = pm_s;
-                        for (int j = 0; j < d; ++j) {
-                            int pr = j;
-                            for (int p = j + 1; p < d; ++p)
-                                if (fabs(lu[p * kMaxD + j]) > fabs(lu[pr * kMaxD + j])) pr = p;
-                            piv[j] = pr;
-                            if (pr != j)
-                                for (int q = 0; q < d; ++q) {
-                                    const double t = lu[j * kMaxD + q];
-                                    lu[j * kMaxD + q] = lu[pr * kMaxD + q];
-                                    lu[pr * kMaxD + q] = t;
-                                }
-                            const double rp = 1.0 / lu[j * kMaxD + j];
-                            for (int p = j + 1; p < d; ++p) {
-                                const double lf = lu[p * kMaxD + j] * rp;
-                                lu[p * kMaxD + j] = lf;
-                                for (int q = j + 1; q < d; ++q) lu[p * kMaxD + q] = lu[p * kMaxD + q] - lf * lu[j * kMaxD + q];
-                            }
-                        }
-                        for (int col = 0; col < d; ++col) {
-                            for (int p = 0; p < d; ++p) b[p] = p == col ? 1.0 : 0.0;
-                            for (int j = 0; j < d; ++j) {
-                                const double t = b[j];
-                                b[j] = b[piv[j]];
-                                b[piv[j]] = t;
-                            }
-                            for (int p = 1; p < d; ++p)
-                                for (int q = 0; q < p; ++q) b[p] = fma(-lu[p * kMaxD + q], b[q], b[p]);
-                            for (int p = d - 1; p >= 0; --p) {
-                                double t = b[p];
-                                for (int q = p + 1; q < d; ++q) t = fma(-lu[p * kMaxD + q], b[q], t);
-                                b[p] = t * (1.0 / lu[p * kMaxD + p]);
-                            }
-                            for (int p = 0; p < d; ++p) ci[p * kMaxD + col] = b[p];
-                        }
-                    }
+                if (lane == 0) {  // np.linalg.inv (linucb_inverse): the LU in place in cov (no longer
+                    // needed), pivots and the solve vector in LDS words LinUCB does not use otherwise
+                    // (no private arrays: no scratch)
+                    linucb_inverse(cov, freq, pm_s, ci, d);
                 }
                 __syncthreads();
                 // m_p(arm) = ci[p] . x_arm (the dgemm entry of cov_inv @ X^T for a row of that arm)
                 for (int t = lane; t < d * A; t += 64) {
                     const int p = t / A, k = t - p * A;
-                    const double* cp = ci + p * kMaxD;
-                    const double* x = arms + k * d;
-                    double acc = cp[0] * x[0];
-                    for (int j = 1; j < d; ++j) acc = fma(cp[j], x[j], acc);
-                    mv[t] = acc;
+                    mv[t] = linucb_m(ci + p * kMaxD, arms + k * d, d, n, p);
                 }
                 __syncthreads();
                 if (lane < d) {  // theta[p] = (cov_inv @ X^T)[p] @ r  (dgemv_t order)
                     const double* mp = mv + lane * A;
-                    theta[lane] = gemv_t_sum([&](int k) { return mp[lact[k]]; }, [&](int k) { return lr[k]; }, n);
+                    theta[lane] = gemv_t_sum([&](int k) { return mp[lact[k]]; }, [&](int k) { return lr[k]; }, n,
+                                             gemv_t_cols(lane, d));
                 }
                 __syncthreads();
                 for (int k = lane; k < A; k += 64) {
@@ -677,8 +432,7 @@ __global__ __launch_bounds__(64) void rollout_policy_wave_kernel(PolicyParams P)
                     for (int p = 1; p < d; ++p) tv = fma(theta[p], x[p], tv);
                     double qv = 0.0;
                     for (int j = 0; j < d; ++j) {
-                        double w = ci[j] * x[0];
-                        for (int p = 1; p < d; ++p) w = fma(ci[p * kMaxD + j], x[p], w);
+                        const double w = linucb_w(ci, x, d, j);
                         qv = j == 0 ? w * x[0] : fma(w, x[j], qv);
                     }
                     vals[k] = tv + P.c * sqrt(qv);

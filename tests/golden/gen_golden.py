@@ -665,6 +665,33 @@ def linucb_long():
     print("LinUCB long")
 
 
+def linucb_dims():
+    """LinUCB (ctrls/ctrl_bandit.py:447-528) at lin_d 3, 5, 6 and 8 (every width the policy kernel
+    takes besides 2 and 4, which linucb_long / linucb_d4 hold): 12-arm linear bandits over 100 steps
+    through eval_linear_bandit.deploy_online_vec, every draw recorded."""
+    import numpy as np
+    from envs import bandit_env
+    from ctrls import ctrl_bandit as cb
+    from evals import eval_linear_bandit
+    out = {}
+    for d in (3, 5, 6, 8):
+        N, H, A, var = 32, 100, 12, 0.3
+        arms = np.random.RandomState(1234 + d).normal(size=(A, d)) / np.sqrt(d)
+        thetas = np.random.RandomState(40 + d).normal(0, 1, (N, d)) / np.sqrt(d)
+        envs = [bandit_env.LinearBanditEnv(t, arms, H, var=var) for t in thetas]
+        vec = bandit_env.BanditEnvVec(envs)
+        np.random.seed(50 + d)
+        with DrawRecorder(np) as rec:
+            cm, meta = eval_linear_bandit.deploy_online_vec(vec, cb.LinUCBPolicy(envs[0], const=1.0, batch_size=N),
+                                                            H, include_meta=True)
+        pre = f"d{d}/"
+        out.update({pre + "means": np.stack([e.means for e in envs]), pre + "arms": arms, pre + "theta": thetas,
+                    pre + "cum_means": cm, pre + "actions": meta["context_actions"].argmax(-1).astype(np.int8),
+                    pre + "g": np.array(rec.g).reshape(H, N), pre + "first_action": np.asarray(rec.plain[0])})
+    np.savez_compressed(os.path.join(OUT, "linucb_dims.npz"), **out)
+    print("LinUCB dims")
+
+
 def linear_offline():
     """evals/eval_linear_bandit.py:202-286 (offline: Opt, the DPT greedy leg, Thompson with the
     100-draw vote and prior 0/1, LinUCB with const 0 'linreg') on fixed contexts of 20-arm linear

@@ -201,18 +201,25 @@ def test_baseline_offline_prefix_and_linucb():
     assert np.array_equal(out["arm_value"].cpu().numpy().T, g["lin/cum_means"])
 
 
-@pytest.mark.parametrize("fix", ["linucb_d4", "linucb_long"])
+@pytest.mark.parametrize("fix", ["linucb_d4", "linucb_long", "linucb_dims:3", "linucb_dims:5", "linucb_dims:6",
+                                 "linucb_dims:8"])
 def test_linucb_kernel_and_drop_in(fix):
     """LinUCB (ctrls/ctrl_bandit.py:447-528) against the reference's recorded online runs: lin_d = 4
-    (12 arms, 20 steps) and lin_d = 2 on the C4 arm table over 800 steps (the context crosses the
-    BLAS blocking of X^T X at 384 and 768 rows).  Every arm index and arm value exactly, through
-    the kernel and through eval_linear_bandit.deploy_online_vec with the reference's draws
-    injected."""
+    (12 arms, 20 steps), lin_d = 2 on the C4 arm table over 800 steps (the context crosses the
+    BLAS blocking of X^T X at 384 and 768 rows), and lin_d 3 / 5 / 6 / 8 over 100 steps (the
+    numpy orders of dpt_linucb.h at every width the kernel takes).  Every arm index and arm value
+    exactly, through the kernel and through eval_linear_bandit.deploy_online_vec with the
+    reference's draws injected."""
     import dpt_hip
     from ctrls.ctrl_bandit import LinUCBPolicy
     from envs.bandit_env import BanditEnvVec, LinearBanditEnv
     from evals import eval_linear_bandit
-    g = golden(f"{fix}.npz")
+    if ":" in fix:
+        name, d = fix.split(":")
+        gz = golden(f"{name}.npz")
+        g = {k.split("/", 1)[1]: gz[k] for k in gz if k.startswith(f"d{d}/")}
+    else:
+        g = golden(f"{fix}.npz")
     A = g["arms"].shape[0]
     H = g["g"].shape[0]
     u = (g["first_action"] + 0.5) / A

@@ -304,16 +304,26 @@ def test_torch_oracle_gradients_match_reference(name):
         assert np.abs(got - ref).max() <= 1e-10 * max(1e-30, np.abs(ref).max()), k
 
 
-@pytest.mark.parametrize("fix", ["linucb_d4", "linucb_long"])
+@pytest.mark.parametrize("fix", ["linucb_d4", "linucb_long", "linucb_dims:3", "linucb_dims:5", "linucb_dims:6",
+                                 "linucb_dims:8"])
 def test_linucb_matches_reference(fix):
-    """LinUCB with lin_d = 4, and lin_d = 2 over 800 steps (np.linalg.inv in the oracle, as in
-    the reference)."""
-    g = golden(f"{fix}.npz")
+    """LinUCB with lin_d = 4, lin_d = 2 over 800 steps, and lin_d 3 / 5 / 6 / 8 over 100 steps
+    (np.linalg.inv in the oracle, as in the reference)."""
+    g = golden_lin(fix)
     H = g["g"].shape[0]
     out = O.bandit_policy_rollout("linucb", g["means"], H, 0.3, g["g"], c=1.0, arms=g["arms"],
                                   first_u_idx=g["first_action"])
     assert np.array_equal(out["actions"], g["actions"])
     assert np.array_equal(out["cum_means"], g["cum_means"])
+
+
+def golden_lin(fix):
+    """a LinUCB fixture: "name" or "linucb_dims:<lin_d>" (one width of the multi-width file)"""
+    if ":" not in fix:
+        return golden(f"{fix}.npz")
+    name, d = fix.split(":")
+    g = golden(f"{name}.npz")
+    return {k.split("/", 1)[1]: g[k] for k in g if k.startswith(f"d{d}/")}
 
 
 @pytest.mark.parametrize("case", [0, 1])
