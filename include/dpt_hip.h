@@ -283,7 +283,7 @@ int dpt_rollout_bandit(const dpt_model* model, const dpt_bandit_rollout_args* ar
  * Per-arm statistics are recomputed each step from the per-arm reward lists in
  * numpy's fp64 pairwise-summation order, as the reference does, so action
  * indices match it bit for bit given the same draws (LinUCB: numpy's BLAS/LAPACK
- * rounding order restated at lin_d = 2; equal up to near-ties above).  policy_noise:
+ * rounding order restated at every lin_d, csrc/dpt_linucb.h).  policy_noise:
  * Thompson (H,N,A) posterior normals (sample = 1) or (H,100,N,A) for the 100-draw vote
  * (sample = 0); LinUCB (N) uniforms for the empty-context arm.  */
 #define DPT_POLICY_OPT 0
