@@ -3,7 +3,8 @@
 ``deploy_online_vec`` (evals/eval_darkroom.py:20-84): with the DPT controller
 over this package's ``Transformer`` and a ``DarkroomEnvVec`` the whole loop is
 one fused kernel launch (dpt_rollout_darkroom) when the window fits (1 + H <=
-dpt_hip.darkroom_max_window(): 512 tokens); otherwise it stays on the device step by step — per step one window forward (gfx950 kernel) over the fixed
+dpt_hip.darkroom_max_window(): 512 tokens) at width 32; otherwise it stays on the device step by
+step (any width) — per step one window forward (gfx950 kernels) over the fixed
 in-context episodes with the current state as query, device sampling, the
 integer grid step kernel, and an on-device append into the episode buffers;
 returns are summed on device and copied once at the end.  Other controllers
@@ -21,10 +22,33 @@ device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
 
 
 def _device_ok(vec_env, controller):
+    """The per-step device loop: our controller, env and model.  Width 32 forwards through the packed
+    device model; other widths through the generic kernels (_GenericWindow), for an inference-mode
+    model (test: the last position's logits; no dropout in play)."""
     from models.net import Transformer
+    m = controller.model
     return (isinstance(controller, DarkroomTransformerController) and isinstance(vec_env, DarkroomEnvVec)
-            and isinstance(controller.model, Transformer) and controller.model.n_embd == dpt_hip.E
-            and controller.batch_size == vec_env.num_envs)
+            and isinstance(m, Transformer) and controller.batch_size == vec_env.num_envs
+            and (m.n_embd == dpt_hip.E or (m.test and not (m.training and m.dropout > 0))))
+
+
+class _GenericWindow:
+    """forward_window for a model of another width: Transformer.forward's generic kernels
+    (dpt_train_forward on the forward-only workspace) over [query | context], last position."""
+
+    def __init__(self, model):
+        self.model = model
+
+    def forward_window(self, query, cs=None, ca=None, cn=None, cr=None):
+        x = {"query_states": query}
+        if cs is not None:
+            x.update(context_states=cs, context_actions=ca, context_next_states=cn, context_rewards=cr)
+        with torch.no_grad():
+            return self.model._forward_generic(x)
+
+
+def _window_model(model):
+    return model.device_model() if model.n_embd == dpt_hip.E else _GenericWindow(model)
 
 
 def _episode_device(dm, ctrl, vec_env, ctx, horizon):
@@ -69,7 +93,8 @@ def _episode_device(dm, ctrl, vec_env, ctx, horizon):
 
 def _fused_ok(vec_env, controller, H):
     # dpt_rollout_darkroom: 1 + H tokens per forward
-    return (_device_ok(vec_env, controller) and vec_env.state_dim == 2 and vec_env.action_dim == 5
+    return (_device_ok(vec_env, controller) and controller.model.n_embd == dpt_hip.E
+            and vec_env.state_dim == 2 and vec_env.action_dim == 5
             and 1 + H <= dpt_hip.darkroom_max_window() and vec_env.dim <= 255)
 
 
@@ -115,7 +140,7 @@ def deploy_online_vec(vec_env, controller, Heps, H, horizon, fused=True):
     cn = torch.zeros((num_envs, ctx_rollouts, horizon, sd), device=dev)
     cr = torch.zeros((num_envs, ctx_rollouts, horizon, 1), device=dev)
     fast = _device_ok(vec_env, controller)
-    dm = controller.model.device_model() if fast else None
+    dm = _window_model(controller.model) if fast else None
     cum_means = []
     for ep in range(Heps):
         if ep < ctx_rollouts:
@@ -194,7 +219,7 @@ def offline(eval_trajs, model, n_eval, H, dim, permuted=False, uniforms=None):
         if _device_ok(vec_env, ctrl):
             c = (batch["context_states"], batch["context_actions"], batch["context_next_states"],
                  batch["context_rewards"][..., 0])
-            _, _, _, er = _episode_device(model.device_model(), ctrl, vec_env, c, H)
+            _, _, _, er = _episode_device(_window_model(model), ctrl, vec_env, c, H)
             res[name] = er.sum(-1).cpu().numpy()
         else:  # other widths / model classes: the controller's own per-step forward
             _, _, _, rs = vec_env.deploy_eval(ctrl)

@@ -289,6 +289,43 @@ def test_other_widths_darkroom_offline(E):
                           O.darkroom_offline_episode(W, goals, ctx, H, None, sample=False).sum(-1))
 
 
+@pytest.mark.parametrize("E,memo", [(16, True), (64, True), (16, False)])
+def test_other_widths_darkroom_online(E, memo):
+    """evals/eval_darkroom.py deploy_online_vec (:20-84) with a model of width != 32: the per-step
+    device loop (generic kernels, the per-episode logits memo, device selection and grid step)
+    against the float64 oracle's rollout fed the same uniforms: returns and actions exactly, with
+    the memo and without it."""
+    import dpt_hip
+    from ctrls.ctrl_darkroom import DarkroomTransformerController
+    from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec
+    from evals import eval_darkroom
+    from models.net import Transformer
+    from oracle import dpt_oracle as O
+    torch.manual_seed(E + 7)
+    horizon, R, Heps, n = 10, 2, 5, 24
+    m = Transformer(dict(horizon=R * horizon, state_dim=2, action_dim=5, n_layer=2, n_embd=E, n_head=1,
+                         dropout=0.0, test=True)).cuda().eval()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.3 * torch.randn_like(p))
+    W = O.split_weights({k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}, 2)
+    rs = np.random.RandomState(E)
+    goals = rs.randint(0, 10, (n, 2))
+    u = rs.uniform(size=(Heps, horizon, n))
+    ref = O.darkroom_online_rollout(W, goals, Heps, R * horizon, horizon, u)
+    vec = DarkroomEnvVec([DarkroomEnv(10, g, horizon) for g in goals])
+    ctrl = DarkroomTransformerController(m, batch_size=n, sample=True)
+    uf = u.reshape(-1, n)
+    ctrl.uniforms = lambda k: uf[k]
+    assert eval_darkroom._device_ok(vec, ctrl) and not eval_darkroom._fused_ok(vec, ctrl, R * horizon)
+    try:
+        dpt_hip.set_darkroom_memo(memo)
+        ret = eval_darkroom.deploy_online_vec(vec, ctrl, Heps, R * horizon, horizon)
+    finally:
+        dpt_hip.set_darkroom_memo(True)
+    assert np.array_equal(ret, ref["returns"])
+
+
 def test_forward_only_workspace_and_second_backward():
     """Without autograd the generic forward runs on the forward-only workspace (DPT_TRAIN_FORWARD_ONLY:
     one layer's activations, no attention probabilities): same preds bit for bit as the training
