@@ -1,0 +1,46 @@
+"""DarkRoom online eval (evals/eval_darkroom.py deploy_online_vec) with models of width != 32: the
+per-step device loop (generic kernels + the per-episode logits memo) against the controller's own
+per-step loop (every task forwarded every step, actions copied to the host), same draws.
+Prints one JSON object: ms per eval and env-steps/s for each width and path."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "decision-pretrained-transformer_amd"), ROOT]
+from ctrls.ctrl_darkroom import DarkroomTransformerController  # noqa: E402
+from envs.darkroom_env import DarkroomEnv, DarkroomEnvVec  # noqa: E402
+from evals import eval_darkroom  # noqa: E402
+from models.net import Transformer  # noqa: E402
+
+N, Heps, horizon = int(os.environ.get("DR_N", "4096")), int(os.environ.get("DR_HEPS", "4")), 100
+goals = np.stack(np.unravel_index(np.arange(N) % 100, (10, 10)), 1)
+out = {}
+device_ok = eval_darkroom._device_ok
+for E in (16, 64):
+    torch.manual_seed(E)
+    m = Transformer(dict(horizon=horizon, state_dim=2, action_dim=5, n_layer=4, n_embd=E, n_head=1, dropout=0.0,
+                         test=True)).cuda().eval()
+    res = {}
+    for path in ("device_loop", "controller_loop"):
+        eval_darkroom._device_ok = device_ok if path == "device_loop" else (lambda *a: False)
+        ts, rets = [], None
+        for rnd in range(2):
+            np.random.seed(rnd)
+            ctrl = DarkroomTransformerController(m, batch_size=N, sample=True)
+            vec = DarkroomEnvVec([DarkroomEnv(10, g, horizon) for g in goals])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rets = eval_darkroom.deploy_online_vec(vec, ctrl, Heps, horizon, horizon)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        res[path] = {"ms": ts[-1] * 1e3, "env_steps_per_s": N * Heps * horizon / ts[-1],
+                     "return_total": int(np.asarray(rets).sum())}
+    eval_darkroom._device_ok = device_ok
+    res["speedup"] = res["controller_loop"]["ms"] / res["device_loop"]["ms"]
+    out[f"E{E}"] = res
+print(json.dumps({"tasks": N, "episodes": Heps, "horizon": horizon, "window": 1 + horizon, "n_layer": 4, **out}))
