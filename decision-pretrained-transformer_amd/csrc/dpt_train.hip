@@ -829,7 +829,7 @@ static int ln_param_grad(const float* x, const float* stt, const float* dy, int 
 
 // ---- matrix-core dispatch (widths 16, 32, 64; other widths keep the row kernels)
 static bool mm_fast(int E) { return E == 16 || E == 32 || E == 64; }
-enum MmKind { kMmQkv, kMmProj, kMmFc, kMmMp, kMmBdMp, kMmBdFc, kMmBdProj, kMmBdQkv };
+enum MmKind { kMmQkv, kMmProj, kMmFc, kMmMp, kMmBdMp, kMmBdFc, kMmBdProj, kMmBdQkv, kMmU };
 
 template <class Kern>
 static void allow_lds(Kern k, size_t bytes) {
@@ -861,6 +861,7 @@ static void mm_kind(int kind, const float* X, const float* W, const float* bias,
         case kMmBdFc: launch_mm<4 * E, E, true, false, 0>(X, W, bias, res, aux, R, Y, st); break;
         case kMmBdProj: launch_mm<E, E, true, false, 0>(X, W, bias, res, aux, R, Y, st); break;
         case kMmBdQkv: launch_mm<3 * E, E, true, false, 0>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmU: launch_mm<E, E, false, false, kMmBias>(X, W, bias, res, aux, R, Y, st); break;
     }
 }
 static void mm(int E, int kind, const float* X, const float* W, const float* bias, const float* res, const float* aux,
@@ -1117,20 +1118,60 @@ int train_backward(const TrDims& d, const float* blob, const float* tok, float* 
 // transition) at ANY width, for models the fused E = 32 kernel (dpt_decode.hip) is not built for.
 // Exact K/V-cache decode: the bandit's query token sits at position 0 and never changes, and the
 // prediction is read at the last position, so every earlier position's keys and values stay
-// valid (causal attention) and a step computes the new token only.  One pass per step over all N
+// valid (causal attention) and a step computes the new token only.  The cache holds each block's
+// LayerNorm output y instead of K and V (the folded attention, GenFold): half the bytes.  One pass per step over all N
 // tasks: embed, then per layer the training forward's row kernels (or their matrix-core forms at
 // widths 16 / 32 / 64) on N rows, the attention of the new token over the task's cache, ln_f and
 // the head; then selection and the env step with the draws and arithmetic of the fused kernel.
-// Workspace (floats): K and V caches [L][N][H][E], then per-step rows.
+// Folded attention (the fused kernels' algebra, dpt_decode.hip): with y_p = LN1(x_p) a block's keys
+// and values are affine in y_p, so q . k_p = u . y_p + const (u = q W_k^T = y G + g0, G = W_q W_k^T,
+// g0 = b_q W_k^T; the constant shifts every score of the row equally and cancels in the softmax) and
+// sum_p P_p v_p = (sum_p P_p y_p) W_v + b_v, so c_proj takes the attention-weighted y on
+// Wvp = W_v W_proj with bvp = b_v W_proj + b_proj.  The cache holds y alone: E floats per position
+// and layer instead of K and V's 2E.  Per layer [G | Wvp | g0 | bvp], [in][out], fp64 sums.
+struct GenFold {
+    __host__ __device__ static int64_t size(int E) { return 2ll * E * E + 2 * E; }
+};
+__global__ void gen_fold_kernel(const float* __restrict__ blob, TrDims d, TrBlob b, float* __restrict__ fold) {
+    const int E = d.E;
+    const int64_t per = GenFold::size(E), total = (int64_t)d.L * per;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int l = (int)(i / per);
+        const int64_t o = i % per;
+        const TrLayer P = TrLayer::make(b.layers + l * d.layer_size(), E);
+        const float* Wa = blob + P.attn_w;  // [E][3E]: columns q | k | v
+        const float* ba = blob + P.attn_b;
+        const float* Wp = blob + P.proj_w;  // [E][E]
+        double acc = 0.0;
+        if (o < (int64_t)E * E) {  // G[r][c] = sum_k Wq[r][k] Wk[c][k]
+            const int r = (int)(o / E), c = (int)(o % E);
+            for (int k = 0; k < E; ++k) acc += (double)Wa[(int64_t)r * 3 * E + k] * Wa[(int64_t)c * 3 * E + E + k];
+        } else if (o < 2ll * E * E) {  // Wvp[r][c] = sum_k Wv[r][k] Wp[k][c]
+            const int64_t oo = o - (int64_t)E * E;
+            const int r = (int)(oo / E), c = (int)(oo % E);
+            for (int k = 0; k < E; ++k) acc += (double)Wa[(int64_t)r * 3 * E + 2 * E + k] * Wp[(int64_t)k * E + c];
+        } else if (o < 2ll * E * E + E) {  // g0[c] = sum_k bq[k] Wk[c][k]
+            const int c = (int)(o - 2ll * E * E);
+            for (int k = 0; k < E; ++k) acc += (double)ba[k] * Wa[(int64_t)c * 3 * E + E + k];
+        } else {  // bvp[c] = sum_k bv[k] Wp[k][c] + bp[c]
+            const int c = (int)(o - 2ll * E * E - E);
+            for (int k = 0; k < E; ++k) acc += (double)ba[2 * E + k] * Wp[(int64_t)k * E + c];
+            acc += blob[P.proj_b + c];
+        }
+        fold[i] = (float)acc;
+    }
+}
+
+// Workspace (floats): the y cache [L][N][H][E], the folded weights, then per-step rows.
 struct GenWs {
-    int64_t K, V, x, x2, y, st, qkv, o, h, lg, tok, total;
+    int64_t Y, fold, x, x2, y, st, qkv, o, h, lg, tok, total;
     static GenWs make(const TrDims& d, int N, int H) {
         GenWs w;
         const int64_t E = d.E, n = N, cache = (int64_t)d.L * n * H * E;
         int64_t p = 0;
         auto take = [&](int64_t k) { const int64_t at = p; p += k; p = (p + 3) & ~3ll; return at; };
-        w.K = take(cache);
-        w.V = take(cache);
+        w.Y = take(cache);
+        w.fold = take((int64_t)d.L * GenFold::size(d.E));
         w.x = take(n * E);
         w.x2 = take(n * E);
         w.y = take(n * E);
@@ -1204,6 +1245,51 @@ __global__ void gen_attn_decode(const float* __restrict__ qkv, float* __restrict
     }
 }
 
+// gen_attn_decode in the folded-attention form (GenFold): u scores the cached y rows (and the new
+// position's own y, at yn), the output is the attention-weighted y (c_proj runs on Wvp)
+__global__ void gen_attn_ydecode(const float* __restrict__ u, const float* __restrict__ yn, float* __restrict__ Yc,
+                                 int E, int N, int H, int pos, float* __restrict__ O) {
+    extern __shared__ float sm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int task = blockIdx.x * (blockDim.x / 64) + wave;
+    if (task >= N) return;
+    float* pr = sm + (size_t)wave * (H + E);
+    float* q = pr + H;
+    const float* row = yn + (int64_t)task * E;
+    float* Y = Yc + (int64_t)task * H * E;
+    for (int e = lane; e < E; e += 64) {
+        q[e] = u[(int64_t)task * E + e];
+        Y[(int64_t)pos * E + e] = row[e];
+    }
+    wave_lds_sync();
+    const float scale = 1.0f / sqrtf((float)E);
+    float m = -INFINITY;
+    for (int j = lane; j <= pos; j += 64) {
+        const float* k = j == pos ? row : Y + (int64_t)j * E;
+        float s = 0.f;
+        for (int e = 0; e < E; ++e) s = fmaf(q[e], k[e], s);
+        s *= scale;
+        pr[j] = s;
+        m = fmaxf(m, s);
+    }
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = lane; j <= pos; j += 64) {
+        const float p = expf(pr[j] - m);
+        pr[j] = p;
+        l += p;
+    }
+    const float inv = 1.0f / wave_sum(l);
+    for (int j = lane; j <= pos; j += 64) pr[j] *= inv;
+    wave_lds_sync();
+    for (int e = lane; e < E; e += 64) {
+        float acc = 0.f;
+        for (int j = 0; j < pos; ++j) acc = fmaf(pr[j], Y[(int64_t)j * E + e], acc);
+        acc = fmaf(pr[pos], row[e], acc);
+        O[(int64_t)task * E + e] = acc;
+    }
+}
+
 // The same for E % 4 == 0, E <= 256, with the rows read as float4: LPK lanes per key (a power of
 // two >= E / 4), 64 / LPK keys per wave-instruction, so every key row is one coalesced read.  Scores
 // are 4-term partial dots summed over the key's lanes by xor shuffles; the values accumulate per
@@ -1262,6 +1348,65 @@ __global__ void gen_attn_decode4(const float* __restrict__ qkv, float* __restric
         const int j = jb + kq;
         if (!act || j > pos) continue;
         const floatx4 v = j == pos ? vn : V4[(int64_t)j * E4 + c];
+        const float p = pr[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = fmaf(p, v[r], acc[r]);
+    }
+#pragma unroll
+    for (int x = LPK; x < 64; x <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] += __shfl_xor(acc[r], x, 64);
+    if (kq == 0 && act) reinterpret_cast<floatx4*>(O + (int64_t)task * E)[c] = acc * inv;
+}
+
+// The folded-attention form of gen_attn_decode4 (GenFold): one y row per position, half the reads
+template <int LPK>
+__global__ void gen_attn_ydecode4(const float* __restrict__ u, const float* __restrict__ yn, float* __restrict__ Yc,
+                                  int E, int N, int H, int pos, float* __restrict__ O) {
+    constexpr int KPW = 64 / LPK;
+    extern __shared__ float sm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int task = blockIdx.x * (blockDim.x / 64) + wave;
+    if (task >= N) return;
+    float* pr = sm + (size_t)wave * H;
+    const int E4 = E >> 2, c = lane % LPK, kq = lane / LPK;
+    const bool act = c < E4;
+    const floatx4* Y4 = reinterpret_cast<const floatx4*>(Yc + (int64_t)task * H * E);
+    const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+    const floatx4 q = act ? reinterpret_cast<const floatx4*>(u + (int64_t)task * E)[c] : zero;
+    const floatx4 yv = act ? reinterpret_cast<const floatx4*>(yn + (int64_t)task * E)[c] : zero;
+    if (kq == 0 && act) reinterpret_cast<floatx4*>(Yc + (int64_t)task * H * E)[(int64_t)pos * E4 + c] = yv;
+    const float scale = 1.0f / sqrtf((float)E);
+    float m = -INFINITY;
+    for (int jb = 0; jb <= pos; jb += KPW) {
+        const int j = jb + kq;
+        floatx4 k = zero;
+        if (act && j < pos) k = Y4[(int64_t)j * E4 + c];
+        else if (act && j == pos) k = yv;
+        float d = fmaf(q[0], k[0], fmaf(q[1], k[1], fmaf(q[2], k[2], q[3] * k[3])));
+#pragma unroll
+        for (int x = 1; x < LPK; x <<= 1) d += __shfl_xor(d, x, 64);
+        if (j <= pos) {
+            d *= scale;
+            if (c == 0) pr[j] = d;
+            m = fmaxf(m, d);
+        }
+    }
+    m = wave_max(m);
+    wave_lds_sync();
+    float l = 0.f;
+    for (int j = lane; j <= pos; j += 64) {
+        const float p = expf(pr[j] - m);
+        pr[j] = p;
+        l += p;
+    }
+    const float inv = 1.0f / wave_sum(l);
+    wave_lds_sync();
+    floatx4 acc = zero;
+    for (int jb = 0; jb <= pos; jb += KPW) {
+        const int j = jb + kq;
+        if (!act || j > pos) continue;
+        const floatx4 v = j == pos ? yv : Y4[(int64_t)j * E4 + c];
         const float p = pr[j];
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[r] = fmaf(p, v[r], acc[r]);
@@ -1345,12 +1490,12 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
     const unsigned row_blocks = (N + rows_per_block - 1) / rows_per_block;
     // the float4 attention for E % 4 == 0 up to 256 (LPK lanes per key), else the scalar one
     const int lpk = E % 4 ? 0 : E <= 16 ? 4 : E <= 32 ? 8 : E <= 64 ? 16 : E <= 128 ? 32 : E <= 256 ? 64 : 0;
-    const void* attn_k = lpk == 4    ? (const void*)gen_attn_decode4<4>
-                         : lpk == 8  ? (const void*)gen_attn_decode4<8>
-                         : lpk == 16 ? (const void*)gen_attn_decode4<16>
-                         : lpk == 32 ? (const void*)gen_attn_decode4<32>
-                         : lpk == 64 ? (const void*)gen_attn_decode4<64>
-                                     : (const void*)gen_attn_decode;
+    const void* attn_k = lpk == 4    ? (const void*)gen_attn_ydecode4<4>
+                         : lpk == 8  ? (const void*)gen_attn_ydecode4<8>
+                         : lpk == 16 ? (const void*)gen_attn_ydecode4<16>
+                         : lpk == 32 ? (const void*)gen_attn_ydecode4<32>
+                         : lpk == 64 ? (const void*)gen_attn_ydecode4<64>
+                                     : (const void*)gen_attn_ydecode;
     const size_t attn_lds = sizeof(float) * rows_per_block * (size_t)(lpk ? H : H + E);
     if (attn_lds > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "generic bandit rollout: H=%d too long for the attention kernel", H);
@@ -1370,32 +1515,36 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
     const int64_t NE = (int64_t)N * E, cache = (int64_t)N * H * E;
     hipLaunchKernelGGL(gen_query_token, dim3(blocks_for((int64_t)N * d.F)), dim3(kTrThreads), 0, st, N, d.F, 1,
                        ws + W.tok);
+    hipLaunchKernelGGL(gen_fold_kernel, dim3(blocks_for((int64_t)L * GenFold::size(E))), dim3(kTrThreads), 0, st, blob, d,
+                       B, ws + W.fold);
     for (int h = 0; h < H; ++h) {
         hipLaunchKernelGGL(gen_embed, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, ws + W.tok, blob, d, B, N, h, x);
         for (int l = 0; l < L; ++l) {
             const TrLayer P = TrLayer::make(B.layers + l * d.layer_size(), E);
             hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x, blob + P.ln1_g, blob + P.ln1_b,
                                N, E, y, stt);
+            // u = y G + g0, the folded attention over the y cache, c_proj on Wvp (GenFold)
+            const float* F = ws + W.fold + l * GenFold::size(E);
+            const float *G = F, *Wvp = F + (int64_t)E * E, *g0 = F + 2ll * E * E, *bvp = g0 + E;
+            float* uq = qkv;
             if (fast)
-                mm(E, kMmQkv, y, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, N, qkv, st);
+                mm(E, kMmU, y, G, g0, nullptr, nullptr, N, uq, st);
             else
-                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE * 3)), dim3(kTrThreads), 0, st, y, blob + P.attn_w,
-                                   blob + P.attn_b, nullptr, N, E, 3 * E, 0, qkv);
-            float* Kc = ws + W.K + l * cache;
-            float* Vc = ws + W.V + l * cache;
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, y, G, g0, nullptr, N, E, E, 0,
+                                   uq);
+            float* Yc = ws + W.Y + l * cache;
             switch (lpk) {
-                case 4: hipLaunchKernelGGL(gen_attn_decode4<4>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
-                case 8: hipLaunchKernelGGL(gen_attn_decode4<8>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
-                case 16: hipLaunchKernelGGL(gen_attn_decode4<16>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
-                case 32: hipLaunchKernelGGL(gen_attn_decode4<32>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
-                case 64: hipLaunchKernelGGL(gen_attn_decode4<64>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o); break;
-                default: hipLaunchKernelGGL(gen_attn_decode, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, qkv, Kc, Vc, E, N, H, h, o);
+                case 4: hipLaunchKernelGGL(gen_attn_ydecode4<4>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, uq, y, Yc, E, N, H, h, o); break;
+                case 8: hipLaunchKernelGGL(gen_attn_ydecode4<8>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, uq, y, Yc, E, N, H, h, o); break;
+                case 16: hipLaunchKernelGGL(gen_attn_ydecode4<16>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, uq, y, Yc, E, N, H, h, o); break;
+                case 32: hipLaunchKernelGGL(gen_attn_ydecode4<32>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, uq, y, Yc, E, N, H, h, o); break;
+                case 64: hipLaunchKernelGGL(gen_attn_ydecode4<64>, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, uq, y, Yc, E, N, H, h, o); break;
+                default: hipLaunchKernelGGL(gen_attn_ydecode, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, uq, y, Yc, E, N, H, h, o);
             }
             if (fast)
-                mm(E, kMmProj, o, blob + P.proj_w, blob + P.proj_b, x, nullptr, N, x2, st);
+                mm(E, kMmProj, o, Wvp, bvp, x, nullptr, N, x2, st);
             else
-                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, o, blob + P.proj_w,
-                                   blob + P.proj_b, x, N, E, E, 0, x2);
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, o, Wvp, bvp, x, N, E, E, 0, x2);
             hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x2, blob + P.ln2_g, blob + P.ln2_b,
                                N, E, y, stt);
             if (fast) {
