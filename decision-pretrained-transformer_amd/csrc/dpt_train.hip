@@ -1359,16 +1359,18 @@ __global__ void gen_attn_decode4(const float* __restrict__ qkv, float* __restric
     if (kq == 0 && act) reinterpret_cast<floatx4*>(O + (int64_t)task * E)[c] = acc * inv;
 }
 
-// The folded-attention form of gen_attn_decode4 (GenFold): one y row per position, half the reads
+// The folded-attention form of gen_attn_decode4 (GenFold), one pass over the y cache (flash decoding):
+// lane group kq takes keys kq, kq + KPW, ... (LPK lanes per key, one float4 of the row each), kU keys
+// of the group per iteration (kU rows in flight per lane), and keeps its own softmax state (m, l, acc)
+// in the exp2 domain; the KPW groups are merged at the end by xor shuffles.  Each y row is read once
+// (the two-pass form read it for the scores and again for the weighted sum).  No LDS.
 template <int LPK>
 __global__ void gen_attn_ydecode4(const float* __restrict__ u, const float* __restrict__ yn, float* __restrict__ Yc,
                                   int E, int N, int H, int pos, float* __restrict__ O) {
-    constexpr int KPW = 64 / LPK;
-    extern __shared__ float sm[];
+    constexpr int KPW = 64 / LPK, kU = 4;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int task = blockIdx.x * (blockDim.x / 64) + wave;
     if (task >= N) return;
-    float* pr = sm + (size_t)wave * H;
     const int E4 = E >> 2, c = lane % LPK, kq = lane / LPK;
     const bool act = c < E4;
     const floatx4* Y4 = reinterpret_cast<const floatx4*>(Yc + (int64_t)task * H * E);
@@ -1376,46 +1378,58 @@ __global__ void gen_attn_ydecode4(const float* __restrict__ u, const float* __re
     const floatx4 q = act ? reinterpret_cast<const floatx4*>(u + (int64_t)task * E)[c] : zero;
     const floatx4 yv = act ? reinterpret_cast<const floatx4*>(yn + (int64_t)task * E)[c] : zero;
     if (kq == 0 && act) reinterpret_cast<floatx4*>(Yc + (int64_t)task * H * E)[(int64_t)pos * E4 + c] = yv;
-    const float scale = 1.0f / sqrtf((float)E);
-    float m = -INFINITY;
-    for (int jb = 0; jb <= pos; jb += KPW) {
-        const int j = jb + kq;
-        floatx4 k = zero;
-        if (act && j < pos) k = Y4[(int64_t)j * E4 + c];
-        else if (act && j == pos) k = yv;
-        float d = fmaf(q[0], k[0], fmaf(q[1], k[1], fmaf(q[2], k[2], q[3] * k[3])));
-#pragma unroll
-        for (int x = 1; x < LPK; x <<= 1) d += __shfl_xor(d, x, 64);
-        if (j <= pos) {
-            d *= scale;
-            if (c == 0) pr[j] = d;
-            m = fmaxf(m, d);
-        }
-    }
-    m = wave_max(m);
-    wave_lds_sync();
-    float l = 0.f;
-    for (int j = lane; j <= pos; j += 64) {
-        const float p = expf(pr[j] - m);
-        pr[j] = p;
-        l += p;
-    }
-    const float inv = 1.0f / wave_sum(l);
-    wave_lds_sync();
+    const float scale = 1.4426950408889634f / sqrtf((float)E);  // scores in the exp2 domain
+    float m = -INFINITY, l = 0.f;
     floatx4 acc = zero;
-    for (int jb = 0; jb <= pos; jb += KPW) {
-        const int j = jb + kq;
-        if (!act || j > pos) continue;
-        const floatx4 v = j == pos ? yv : Y4[(int64_t)j * E4 + c];
-        const float p = pr[j];
+    for (int jb = 0; jb <= pos; jb += KPW * kU) {
+        floatx4 v[kU];
+        float sc[kU];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = fmaf(p, v[r], acc[r]);
+        for (int t = 0; t < kU; ++t) {
+            const int j = jb + t * KPW + kq;
+            v[t] = zero;
+            if (act && j < pos) v[t] = Y4[(int64_t)j * E4 + c];
+            else if (act && j == pos) v[t] = yv;
+        }
+        float mn = m;
+#pragma unroll
+        for (int t = 0; t < kU; ++t) {
+            const int j = jb + t * KPW + kq;
+            float d = fmaf(q[0], v[t][0], fmaf(q[1], v[t][1], fmaf(q[2], v[t][2], q[3] * v[t][3])));
+#pragma unroll
+            for (int x = 1; x < LPK; x <<= 1) d += __shfl_xor(d, x, 64);
+            sc[t] = j <= pos ? d * scale : -INFINITY;
+            mn = fmaxf(mn, sc[t]);
+        }
+        if (mn == -INFINITY) continue;  // no key of this group in the chunk yet
+        const float corr = exp2f(m - mn);  // 0 while m = -inf
+        l *= corr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] *= corr;
+#pragma unroll
+        for (int t = 0; t < kU; ++t) {
+            const float p = exp2f(sc[t] - mn);
+            l += p;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = fmaf(p, v[t][r], acc[r]);
+        }
+        m = mn;
     }
+    // merge the KPW groups' states (every group but kq = 0 may be empty: m = -inf, l = 0)
 #pragma unroll
-    for (int x = LPK; x < 64; x <<= 1)
+    for (int x = LPK; x < 64; x <<= 1) {
+        const float mo = __shfl_xor(m, x, 64), lo = __shfl_xor(l, x, 64);
+        floatx4 ao;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] += __shfl_xor(acc[r], x, 64);
-    if (kq == 0 && act) reinterpret_cast<floatx4*>(O + (int64_t)task * E)[c] = acc * inv;
+        for (int r = 0; r < 4; ++r) ao[r] = __shfl_xor(acc[r], x, 64);
+        const float mm = fmaxf(m, mo);
+        const float ca = m == -INFINITY ? 0.f : exp2f(m - mm), cb = mo == -INFINITY ? 0.f : exp2f(mo - mm);
+        l = l * ca + lo * cb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = acc[r] * ca + ao[r] * cb;
+        m = mm;
+    }
+    if (kq == 0 && act) reinterpret_cast<floatx4*>(O + (int64_t)task * E)[c] = acc * (1.0f / l);
 }
 
 struct GenEnv {
@@ -1496,7 +1510,7 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
                          : lpk == 32 ? (const void*)gen_attn_ydecode4<32>
                          : lpk == 64 ? (const void*)gen_attn_ydecode4<64>
                                      : (const void*)gen_attn_ydecode;
-    const size_t attn_lds = sizeof(float) * rows_per_block * (size_t)(lpk ? H : H + E);
+    const size_t attn_lds = lpk ? 0 : sizeof(float) * rows_per_block * (size_t)(H + E);  // (the float4 form: none)
     if (attn_lds > 160 * 1024) {
         set_error(DPT_EUNSUPPORTED, "generic bandit rollout: H=%d too long for the attention kernel", H);
         return DPT_EUNSUPPORTED;
