@@ -424,8 +424,11 @@ int dpt_train_backward(const dpt_train_desc* desc_host, const float* blob, const
  * dropout 0): an exact K/V-cache decode, one step for all N tasks at a time (the training
  * forward's row kernels, or their matrix-core forms at widths 16 / 32 / 64, on N rows; the new
  * token's attention over the task's cache), then the fused kernel's selection, draws and env
- * step.  args->kvcache = dpt_rollout_bandit_generic_workspace_numel floats (K and V caches
- * [n_layer][N][H][n_embd] plus per-step rows); the other fields as for dpt_rollout_bandit.
+ * step.  The cache holds each block's LayerNorm output y (the folded attention: u = y W_q W_k^T
+ * scores the cached rows, c_proj runs on W_v W_proj), read once per step by a flash-decoding pass.
+ * args->kvcache = dpt_rollout_bandit_generic_workspace_numel floats (the y cache
+ * [n_layer][N][H][n_embd], the folded weights, per-step rows); the other fields as for
+ * dpt_rollout_bandit.
  * Replaces the per-step path (Transformer.forward over the whole window every step) at widths
  * the fused kernel is not built for.                                                        */
 int dpt_rollout_bandit_generic_workspace_numel(const dpt_train_desc* desc_host, int32_t N, int32_t H,
