@@ -453,23 +453,27 @@ __host__ __device__ constexpr int mm_ldb(int K, int N) {
         if (((K / 4) * (N + p)) % 32 == 16) return N + p;
     return N + 1;
 }
-template <int K, int N, bool TRANS, bool ACT, int EPI>
+// NC < N (the decode-sized rows of the generic rollout): blockIdx.y takes columns [NC y, NC y + NC),
+// and only that slice of B is staged, so R / 64 row blocks still fill the chip; every output's
+// k order is unchanged (bit-identical to NC = N).
+template <int K, int N, bool TRANS, bool ACT, int EPI, int NC = N>
 __global__ __launch_bounds__(256) void tr_mm_rows(const float* __restrict__ X, const float* __restrict__ W,
                                                   const float* __restrict__ bias, const float* __restrict__ res,
                                                   const float* __restrict__ aux, int R, float* __restrict__ Y) {
-    static_assert(K % 16 == 0 && N % 16 == 0, "K, N multiples of 16");
+    static_assert(K % 16 == 0 && N % 16 == 0 && NC % 16 == 0 && N % NC == 0, "K, N, NC multiples of 16");
     constexpr int KS = K / 4;  // k-steps
-    constexpr int LDB = mm_ldb(K, N);
+    constexpr int LDB = mm_ldb(K, NC);
     extern __shared__ float Bs[];  // [K][LDB]
+    const int n0 = NC == N ? 0 : blockIdx.y * NC;
     if constexpr (TRANS) {
-        for (int i = threadIdx.x; i < K * N; i += blockDim.x) {
-            const int k = i / N, n = i % N;
-            Bs[k * LDB + n] = W[(int64_t)n * K + k];
+        for (int i = threadIdx.x; i < K * NC; i += blockDim.x) {
+            const int k = i / NC, n = i % NC;
+            Bs[k * LDB + n] = W[(int64_t)(n0 + n) * K + k];
         }
-    } else {  // 16-B loads (N % 16 == 0: a float4 never crosses a row)
-        for (int i = threadIdx.x; i < K * N / 4; i += blockDim.x) {
-            const floatx4 v = reinterpret_cast<const floatx4*>(W)[i];
-            const int k = 4 * i / N, n = 4 * i % N;
+    } else {  // 16-B loads (NC % 16 == 0: a float4 never crosses a row)
+        for (int i = threadIdx.x; i < K * NC / 4; i += blockDim.x) {
+            const int k = 4 * i / NC, n = 4 * i % NC;
+            const floatx4 v = *reinterpret_cast<const floatx4*>(W + (int64_t)k * N + n0 + n);
 #pragma unroll
             for (int r = 0; r < 4; ++r) Bs[k * LDB + n + r] = v[r];
         }
@@ -487,12 +491,12 @@ __global__ __launch_bounds__(256) void tr_mm_rows(const float* __restrict__ X, c
     }
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < N / 16; ++c) {
+    for (int c = 0; c < NC / 16; ++c) {
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s)
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], Bs[(kq * KS + s) * LDB + 16 * c + i16], acc, 0, 0, 0);
-        const int n = 16 * c + i16;
+        const int n = n0 + 16 * c + i16;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int rr = row0 + 4 * kq + r;
@@ -869,6 +873,33 @@ static void mm(int E, int kind, const float* X, const float* W, const float* bia
     if (E == 16) mm_kind<16>(kind, X, W, bias, res, aux, R, Y, st);
     else if (E == 32) mm_kind<32>(kind, X, W, bias, res, aux, R, Y, st);
     else mm_kind<64>(kind, X, W, bias, res, aux, R, Y, st);
+}
+// the decode-row products of the generic rollout (R = N tasks, a few thousand rows): columns split so
+// that the R / 64 row blocks times N / NC column slices fill the chip, NC = max(16, N / 4)
+template <int K, int N, bool ACT, int EPI>
+static void launch_mm_dec(const float* X, const float* W, const float* bias, const float* res, int R, float* Y,
+                          hipStream_t st) {
+    constexpr int NC = N / 4 > 16 ? N / 4 : 16;
+    const size_t lds = sizeof(float) * K * mm_ldb(K, NC);
+    allow_lds(tr_mm_rows<K, N, false, ACT, EPI, NC>, lds);
+    hipLaunchKernelGGL((tr_mm_rows<K, N, false, ACT, EPI, NC>), dim3((R + 63) / 64, N / NC), dim3(256), lds, st, X, W,
+                       bias, res, nullptr, R, Y);
+}
+template <int E>
+static void mm_dec_kind(int kind, const float* X, const float* W, const float* bias, const float* res, int R, float* Y,
+                        hipStream_t st) {
+    switch (kind) {
+        case kMmU: launch_mm_dec<E, E, false, kMmBias>(X, W, bias, res, R, Y, st); break;
+        case kMmProj: launch_mm_dec<E, E, false, kMmBias | kMmRes>(X, W, bias, res, R, Y, st); break;
+        case kMmFc: launch_mm_dec<E, 4 * E, false, kMmBias>(X, W, bias, res, R, Y, st); break;
+        case kMmMp: launch_mm_dec<4 * E, E, true, kMmBias | kMmRes>(X, W, bias, res, R, Y, st); break;
+    }
+}
+static void mm_dec(int E, int kind, const float* X, const float* W, const float* bias, const float* res, int R,
+                   float* Y, hipStream_t st) {
+    if (E == 16) mm_dec_kind<16>(kind, X, W, bias, res, R, Y, st);
+    else if (E == 32) mm_dec_kind<32>(kind, X, W, bias, res, R, Y, st);
+    else mm_dec_kind<64>(kind, X, W, bias, res, R, Y, st);
 }
 
 template <int IN, int OUT, bool ACT>
@@ -1542,7 +1573,7 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
             const float *G = F, *Wvp = F + (int64_t)E * E, *g0 = F + 2ll * E * E, *bvp = g0 + E;
             float* uq = qkv;
             if (fast)
-                mm(E, kMmU, y, G, g0, nullptr, nullptr, N, uq, st);
+                mm_dec(E, kMmU, y, G, g0, nullptr, N, uq, st);
             else
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, y, G, g0, nullptr, N, E, E, 0,
                                    uq);
@@ -1556,14 +1587,14 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
                 default: hipLaunchKernelGGL(gen_attn_ydecode, dim3(row_blocks), dim3(kTrThreads), attn_lds, st, uq, y, Yc, E, N, H, h, o);
             }
             if (fast)
-                mm(E, kMmProj, o, Wvp, bvp, x, nullptr, N, x2, st);
+                mm_dec(E, kMmProj, o, Wvp, bvp, x, N, x2, st);
             else
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, o, Wvp, bvp, x, N, E, E, 0, x2);
             hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x2, blob + P.ln2_g, blob + P.ln2_b,
                                N, E, y, stt);
             if (fast) {
-                mm(E, kMmFc, y, blob + P.fc_w, blob + P.fc_b, nullptr, nullptr, N, hb, st);
-                mm(E, kMmMp, hb, blob + P.mp_w, blob + P.mp_b, x2, nullptr, N, x, st);
+                mm_dec(E, kMmFc, y, blob + P.fc_w, blob + P.fc_b, nullptr, N, hb, st);
+                mm_dec(E, kMmMp, hb, blob + P.mp_w, blob + P.mp_b, x2, N, x, st);
             } else {
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE * 4)), dim3(kTrThreads), 0, st, y, blob + P.fc_w,
                                    blob + P.fc_b, nullptr, N, E, 4 * E, 0, hb);
