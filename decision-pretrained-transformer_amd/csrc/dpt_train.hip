@@ -895,11 +895,14 @@ static void mm_dec_kind(int kind, const float* X, const float* W, const float* b
         case kMmMp: launch_mm_dec<4 * E, E, true, kMmBias | kMmRes>(X, W, bias, res, R, Y, st); break;
     }
 }
+static bool mm_dec_fast(int E) { return E == 16 || E == 32 || E == 48 || E == 64 || E == 128; }
 static void mm_dec(int E, int kind, const float* X, const float* W, const float* bias, const float* res, int R,
                    float* Y, hipStream_t st) {
     if (E == 16) mm_dec_kind<16>(kind, X, W, bias, res, R, Y, st);
     else if (E == 32) mm_dec_kind<32>(kind, X, W, bias, res, R, Y, st);
-    else mm_dec_kind<64>(kind, X, W, bias, res, R, Y, st);
+    else if (E == 48) mm_dec_kind<48>(kind, X, W, bias, res, R, Y, st);
+    else if (E == 64) mm_dec_kind<64>(kind, X, W, bias, res, R, Y, st);
+    else mm_dec_kind<128>(kind, X, W, bias, res, R, Y, st);
 }
 
 template <int IN, int OUT, bool ACT>
@@ -1549,7 +1552,7 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
     if (attn_lds > 64 * 1024) (void)hipFuncSetAttribute(attn_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)attn_lds);
     GenEnv g{N, H, a.A, 1, a.type, a.sample, a.first_task, a.var, a.seed, a.counter, a.means, a.uniforms, a.noise,
              a.actions_out, a.rewards_out, a.arm_value_out, a.logits_out};
-    const bool fast = mm_fast(E);
+    const bool fast = mm_dec_fast(E);  // the column-split matrix-core products (mm_dec)
     float* x = ws + W.x;
     float* x2 = ws + W.x2;
     float* y = ws + W.y;
