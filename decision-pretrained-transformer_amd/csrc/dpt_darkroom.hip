@@ -1167,7 +1167,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             // the workspace kernels (the product path) specialised on the block count; the
             // workspace-free fallback dispatches per phase (its specialisation computed wrong
             // logits at 101-token windows: not shipped)
-            if constexpr (kWs) {
+#ifndef DPT_DR_SPEC_NOWS
+#define DPT_DR_SPEC_NOWS 0
+#endif
+            if constexpr (kWs || DPT_DR_SPEC_NOWS) {
                 if (nb == 2) forward(std::integral_constant<int, 2>{});
                 else if (nb == 1) forward(std::integral_constant<int, 1>{});
                 else forward(std::integral_constant<int, 0>{});

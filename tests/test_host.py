@@ -138,9 +138,9 @@ def test_train_desc_rejects_bad_dropout():
 
 
 def test_generic_rollout_workspace_and_argument_checks():
-    """dpt_rollout_bandit_generic_workspace_numel: K and V caches [L][N][H][E] plus the per-step
-    rows (host-side, no GPU); a desc with dropout is rejected before any device work, and N = 0
-    is a no-op."""
+    """dpt_rollout_bandit_generic_workspace_numel: the y cache [L][N][H][E], the folded attention
+    weights [L][2E^2 + 2E] and the per-step rows (host-side, no GPU); a desc with dropout is rejected
+    before any device work, and N = 0 is a no-op."""
     import ctypes
     import pytest
     from dpt_hip import _lib
@@ -150,9 +150,10 @@ def test_generic_rollout_workspace_and_argument_checks():
     d = tr.desc(L, E, 1, A, 4 * (1 + H), 1, 1)
     n = ctypes.c_int64()
     _lib.check(lib.dpt_rollout_bandit_generic_workspace_numel(ctypes.byref(d), N, H, ctypes.byref(n)))
-    cache = 2 * L * N * H * E
+    cache = L * N * H * E
+    fold = L * (2 * E * E + 2 * E)
     rows = N * (4 * E + 2 + 3 * E + 4 * E + A + (2 + A + 1))  # x x2 y o, st, qkv, h, logits, token
-    assert cache + rows <= n.value <= cache + rows + 4 * 12
+    assert cache + fold + rows <= n.value <= cache + fold + rows + 4 * 13
     args = _lib.BanditRolloutArgs()
     args.N, args.H, args.A = 0, H, A
     _lib.check(lib.dpt_rollout_bandit_generic(ctypes.byref(d), ctypes.c_void_p(8), ctypes.byref(args), None))
