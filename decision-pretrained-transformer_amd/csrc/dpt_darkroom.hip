@@ -1164,11 +1164,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     }
                 }
             };
-            // the workspace kernels (the product path) specialised on the block count; the
-            // workspace-free fallback dispatches per phase (its specialisation computed wrong
-            // logits at 101-token windows: not shipped)
+            // specialised on the wave's block count (DPT_DR_SPEC_NOWS = 0: the workspace-free kernels
+            // dispatch per phase instead, the A/B and diagnostic form, scripts/dr_nows_check.py)
 #ifndef DPT_DR_SPEC_NOWS
-#define DPT_DR_SPEC_NOWS 0
+#define DPT_DR_SPEC_NOWS 1
 #endif
             if constexpr (kWs || DPT_DR_SPEC_NOWS) {
                 if (nb == 2) forward(std::integral_constant<int, 2>{});

@@ -17,7 +17,7 @@ import bench  # noqa: E402
 import dpt_hip  # noqa: E402
 
 dim = int(os.environ.get("DR_DIM", "10"))
-R, horizon, Heps, N = 1, 100, 3, 64
+R, horizon, Heps, N = int(os.environ.get("DR_R", "1")), 100, 3, 64
 sd, _ = bench.synthetic_state_dict(4, 2, 5, R * horizon)
 m = dpt_hip.DeviceModel(sd, 4, 2, 5, 4 * (1 + R * horizon))
 goals = np.random.RandomState(3).randint(0, dim, (N, 2))
@@ -31,6 +31,20 @@ for ws in (True, False):
 dpt_hip.set_darkroom_workspace(True)
 a, b = outs[True], outs[False]
 res = {"lib": sys.argv[1], "dim": dim}
+# the float64 C oracle on a few tasks, same draws (the workspace-free run): largest logit error per episode
+sys.path.insert(0, ROOT)
+from oracle import c_oracle  # noqa: E402
+tasks = np.arange(0, N, 8)
+ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, 4).numpy(), 4, 4 * (1 + R * horizon), goals[tasks], Heps,
+                                horizon, R, u[:, tasks], True, dim=dim, threads=16, want_logits=True)
+rl = np.asarray(ref["logits"])  # (steps, tasks, A)
+ra = np.asarray(ref["actions"])
+for ep in range(Heps):
+    sl = slice(ep * horizon, (ep + 1) * horizon)
+    same = (b["actions"][tasks][:, sl] == ra[:, sl]).all(1)
+    d = np.abs(b["logits"][sl][:, tasks] - rl[sl]) / np.maximum(1.0, np.abs(rl[sl]))
+    res[f"oracle_ep{ep}"] = {"max_scaled_err_same_tasks": float(d[:, same].max()) if same.any() else None,
+                             "tasks_same_actions": int(same.sum())}
 for ep in range(Heps):
     sl = slice(ep * horizon, (ep + 1) * horizon)
     same = (a["actions"][:, sl] == b["actions"][:, sl]).all(1)
