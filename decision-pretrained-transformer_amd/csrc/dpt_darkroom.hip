@@ -946,8 +946,21 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     DR_STAMP(1);
                 }
 
+// DPT_DR_TAIL_LD_EARLY: the MLP waves' 48 fp32 tail weights per lane issued before the last layer's
+// attention partials (1, the default: no spill at the 168-VGPR bound, -0.8 % at config 3,
+// profiles/r5e/ab_darkroom_tail_ld_early.json), at the start of the last layer (2: 128 B/lane of
+// spill) or after the partials' barrier (0)
+#ifndef DPT_DR_TAIL_LD_EARLY
+#define DPT_DR_TAIL_LD_EARLY 1
+#endif
+                DrTailW tlw;  // the last block's fp32 tail weights (dr_tail_ld_*)
                 for (int layer = 1; layer < L; ++layer) {
                     const bool last = layer == L - 1;
+                    if (DPT_DR_TAIL_LD_EARLY == 2 && last && wave < kFF / 32) {  // in flight across the last layer
+                        const float* tw0 = p.frag + (size_t)L * (Frag3::bytes / 4);
+                        dr_tail_ld_early(tw0, wave, tlw);
+                        dr_tail_ld_late(tw0, wave, tlw);
+                    }
                     auto& kv = S.kv;
                     const float* W = P + layer * PL::size;
                     float q[2][8];
@@ -1024,7 +1037,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     constexpr int kMlpWaves = kFF / 32;
                     static_assert(kMlpWaves == 4 && NW >= kMlpWaves && kTailWave < kMlpWaves, "four MLP waves");
                     const float* tw = p.frag + (size_t)L * (Frag3::bytes / 4);
-                    DrTailW tlw;
+                    if (DPT_DR_TAIL_LD_EARLY == 1 && wave < kMlpWaves) {  // in flight across the attention partials
+                        dr_tail_ld_early(tw, wave, tlw);
+                        dr_tail_ld_late(tw, wave, tlw);
+                    }
                     // (1) the attention as flash partials (m, l, o), in attend's convention (exp2
                     // domain; l and o at 2^kPExp and 2^(attn_ey + kPExp), so o / l is the output at
                     // the c_proj split's scale): with split values key tiles 2 wave and 2 wave + 1
@@ -1124,10 +1140,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     // selection and the env step
                     float x1 = 0.f;
                     if (wave < kMlpWaves) {
-                        // the weights here, not before (1): live across the attention partials they push the
-                        // kernel past 256 VGPRs (spills); their latency runs under the merge
-                        dr_tail_ld_early(tw, wave, tlw);
-                        dr_tail_ld_late(tw, wave, tlw);
+                        if (!DPT_DR_TAIL_LD_EARLY) {
+                            dr_tail_ld_early(tw, wave, tlw);
+                            dr_tail_ld_late(tw, wave, tlw);
+                        }
     #ifndef DPT_DR_SKIP_TAIL
                         x1 = dr_tail_mlp(S, W, tlw, wave, nparts, M);
     #endif
