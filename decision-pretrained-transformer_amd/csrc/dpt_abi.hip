@@ -514,11 +514,15 @@ static int train_dims(const dpt_train_desc* d, TrDims& o) {
                 d->window <= d->n_positions,
             "train desc: n_layer=%d n_embd=%d sd=%d A=%d n_positions=%d batch=%d window=%d", d->n_layer, d->n_embd,
             d->state_dim, d->action_dim, d->n_positions, d->batch, d->window);
-    REQUIRE((d->reserved & ~DPT_TRAIN_FORWARD_ONLY) == 0 && d->reserved2 == 0, "train desc: unknown flags 0x%x",
-            d->reserved);
+    REQUIRE((d->reserved & ~(DPT_TRAIN_FORWARD_ONLY | DPT_TRAIN_LAST_ONLY)) == 0 && d->reserved2 == 0,
+            "train desc: unknown flags 0x%x", d->reserved);
+    REQUIRE(!(d->reserved & DPT_TRAIN_LAST_ONLY) || ((d->reserved & DPT_TRAIN_FORWARD_ONLY) && d->dropout == 0.0f),
+            "train desc: DPT_TRAIN_LAST_ONLY needs DPT_TRAIN_FORWARD_ONLY and no dropout");
     REQUIRE(d->dropout >= 0.0f && d->dropout < 1.0f, "train desc: dropout %g outside [0, 1)", (double)d->dropout);
+    // fwd_only: 1 = forward-only workspace, 3 = that and preds at the last position only
+    const int fo = (d->reserved & DPT_TRAIN_FORWARD_ONLY) ? ((d->reserved & DPT_TRAIN_LAST_ONLY) ? 3 : 1) : 0;
     o = TrDims{d->n_layer, d->n_embd, 2 * d->state_dim + d->action_dim + 1, d->action_dim, d->batch, d->window,
-               d->n_positions, (d->reserved & DPT_TRAIN_FORWARD_ONLY) ? 1 : 0, 0u, 1.0f, d->dropout_seed};
+               d->n_positions, fo, 0u, 1.0f, d->dropout_seed};
     if (d->dropout > 0.0f) {  // keep iff word >= ceil(p 2^32): P(keep) = 1 - p to 2^-32
         const double t = std::ceil((double)d->dropout * 4294967296.0);
         o.drop_thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;

@@ -955,6 +955,53 @@ static void attn_bwd_fast(int E, const float* qkv, const float* P, const float* 
     else attn_bwd_e<64>(qkv, P, O, dO, d, dS, dqkv, st);
 }
 
+// DPT_TRAIN_LAST_ONLY: the last block for the last position of each sequence alone.  One wave per
+// sequence: the causal row of query T-1 over all T keys (tr_attn_fwd's arithmetic for that row).
+__global__ void tr_attn_last(const float* __restrict__ qkv, TrDims d, float* __restrict__ O) {
+    extern __shared__ float sm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x / 64) + wave;
+    if (b >= d.B) return;
+    const int T = d.T, E = d.E;
+    float* pr = sm + (size_t)wave * (T + E);
+    float* q = pr + T;
+    const float* base = qkv + (int64_t)b * T * 3 * E;
+    for (int e = lane; e < E; e += 64) q[e] = base[(int64_t)(T - 1) * 3 * E + e];
+    wave_lds_sync();
+    const float scale = 1.0f / sqrtf((float)E);
+    float m = -INFINITY;
+    for (int j = lane; j < T; j += 64) {
+        const float* k = base + (int64_t)j * 3 * E + E;
+        float s = 0.f;
+        for (int e = 0; e < E; ++e) s = fmaf(q[e], k[e], s);
+        s *= scale;
+        pr[j] = s;
+        m = fmaxf(m, s);
+    }
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = lane; j < T; j += 64) {
+        const float p = expf(pr[j] - m);
+        pr[j] = p;
+        l += p;
+    }
+    const float inv = 1.0f / wave_sum(l);
+    wave_lds_sync();
+    for (int e = lane; e < E; e += 64) {
+        float acc = 0.f;
+        for (int j = 0; j < T; ++j) acc = fmaf(pr[j], base[(int64_t)j * 3 * E + 2 * E + e], acc);
+        O[(int64_t)b * E + e] = acc * inv;
+    }
+}
+// dst[b][c] = src[(b T + T - 1)][c] (gather), or the reverse (scatter into the sequences' last rows)
+__global__ void tr_last_rows(const float* __restrict__ src, float* __restrict__ dst, int B, int T, int C, int scatter) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)B * C) return;
+    const int64_t b = i / C, c = i % C, r = (b * T + T - 1) * C + c;
+    if (scatter) dst[r] = src[i];
+    else dst[i] = src[r];
+}
+
 int train_forward(const TrDims& d, const float* blob, const float* tok, float* ws, float* preds, hipStream_t st) {
     if (int rc = train_dims_check(d)) return rc;
     const TrBlob B = TrBlob::make(d);
@@ -977,9 +1024,63 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
                                  ws + W.x);
     // slot of layer l's arrays: l, or 0 (x: l & 1) in the forward-only workspace
     auto xs = [&](int l) -> int64_t { return d.fwd_only ? (l & 1) : l; };
+    // DPT_TRAIN_LAST_ONLY (fwd_only == 3, no dropout, T > 1): the last block after its keys and values
+    // for the last position of each sequence alone, then ln_f and the head on those rows
+    const bool last_only = d.fwd_only == 3 && !drop && d.T > 1;
     for (int l = 0; l < d.L; ++l) {
         const TrLayer P = TrLayer::make(B.layers + l * d.layer_size(), E);
         const int64_t sl = d.fwd_only ? 0 : l;
+        if (last_only && l == d.L - 1) {
+            const float* x = ws + W.x + xs(l) * RE;
+            float* y1 = ws + W.y1;
+            float* qkv = ws + W.qkv;
+            hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x,
+                               blob + P.ln1_g, blob + P.ln1_b, R, E, y1, ws + W.st1);
+            if (mm_fast(E))
+                mm(E, kMmQkv, y1, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, R, qkv, st);
+            else
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 3)), dim3(kTrThreads), 0, st, y1, blob + P.attn_w,
+                                   blob + P.attn_b, nullptr, R, E, 3 * E, 0, qkv);
+            const int Bn = d.B;
+            const int64_t BE = (int64_t)Bn * E;
+            float* ol = ws + W.o;         // [B][E]
+            float* xl = ws + W.y2;        // [B][E]: the last rows of x
+            float* x2l = ws + W.x2;       // [B][E]
+            float* y2l = ws + W.y1;       // [B][E] (y1 is done with)
+            float* hl = ws + W.hpre;      // [B][4E]
+            float* xnl = ws + W.x + xs(l + 1) * RE;  // [B][E]
+            float* pl = ws + W.hpre + 4 * BE;        // [B][A] (4E (R - B) >= A B for T > 1)
+            const size_t lds = sizeof(float) * rows_per_block * (size_t)(d.T + E);
+            if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)tr_attn_last, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(tr_attn_last, dim3((Bn + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), lds, st,
+                               qkv, d, ol);
+            hipLaunchKernelGGL(tr_last_rows, dim3(blocks_for(BE)), dim3(kTrThreads), 0, st, x, xl, Bn, d.T, E, 0);
+            const unsigned bb = (Bn + rows_per_block - 1) / rows_per_block;
+            if (mm_fast(E)) {
+                mm(E, kMmProj, ol, blob + P.proj_w, blob + P.proj_b, xl, nullptr, Bn, x2l, st);
+            } else {
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(BE)), dim3(kTrThreads), 0, st, ol, blob + P.proj_w,
+                                   blob + P.proj_b, xl, Bn, E, E, 0, x2l);
+            }
+            hipLaunchKernelGGL(tr_layernorm, dim3(bb), dim3(kTrThreads), 0, st, x2l, blob + P.ln2_g, blob + P.ln2_b, Bn, E,
+                               y2l, ws + W.st2);
+            if (mm_fast(E)) {
+                mm(E, kMmFc, y2l, blob + P.fc_w, blob + P.fc_b, nullptr, nullptr, Bn, hl, st);
+                mm(E, kMmMp, hl, blob + P.mp_w, blob + P.mp_b, x2l, nullptr, Bn, xnl, st);
+            } else {
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(BE * 4)), dim3(kTrThreads), 0, st, y2l, blob + P.fc_w,
+                                   blob + P.fc_b, nullptr, Bn, E, 4 * E, 0, hl);
+                hipLaunchKernelGGL(tr_linear, dim3(blocks_for(BE)), dim3(kTrThreads), 0, st, hl, blob + P.mp_w,
+                                   blob + P.mp_b, x2l, Bn, 4 * E, E, 1, xnl);
+            }
+            hipLaunchKernelGGL(tr_layernorm, dim3(bb), dim3(kTrThreads), 0, st, xnl, blob + B.lnf_g, blob + B.lnf_b, Bn, E,
+                               ws + W.yf, ws + W.stf);
+            hipLaunchKernelGGL(tr_linear, dim3(blocks_for((int64_t)Bn * d.A)), dim3(kTrThreads), 0, st, ws + W.yf,
+                               blob + B.head_w, blob + B.head_b, nullptr, Bn, E, d.A, 0, pl);
+            hipLaunchKernelGGL(tr_last_rows, dim3(blocks_for((int64_t)Bn * d.A)), dim3(kTrThreads), 0, st, pl, preds, Bn,
+                               d.T, d.A, 1);
+            return launched("train forward (last position only)");
+        }
         const float* x = ws + W.x + xs(l) * RE;
         float* y1 = ws + W.y1 + sl * RE;
         float* st1 = ws + W.st1 + sl * R * 2;

@@ -189,6 +189,7 @@ class TrainDesc(ctypes.Structure):
 
 
 TRAIN_FORWARD_ONLY = 1  # dpt_train_desc.reserved flag (DPT_TRAIN_FORWARD_ONLY)
+TRAIN_LAST_ONLY = 2  # with it: preds at the last position only (DPT_TRAIN_LAST_ONLY)
 
 
 SIGNATURES["dpt_train_blob_numel"] = (_i32, [ctypes.POINTER(TrainDesc), ctypes.POINTER(_i64)])

@@ -158,8 +158,10 @@ class Transformer(nn.Module):
         p, seed = 0.0, 0
         if self.training and self.dropout > 0:  # fresh masks per call, from torch's (seedable) CPU generator
             p, seed = float(self.dropout), int(torch.randint(0, 2 ** 62, (1,)).item())
+        # inference in test mode reads the last position only (LAST_ONLY: the last block for that row alone)
+        flags = 0 if grad else tr.FORWARD_ONLY | (tr.LAST_ONLY if self.test and p == 0.0 else 0)
         dims = (self.n_layer, self.n_embd, self.state_dim, self.action_dim, self.n_positions, tok.shape[0],
-                tok.shape[1], 0 if grad else tr.FORWARD_ONLY, p, seed)
+                tok.shape[1], flags, p, seed)
         preds = tr.TransformerFunction.apply(tok, dims, *tr.param_list(self))
         return preds[:, -1, :] if self.test else preds[:, 1:, :]
 

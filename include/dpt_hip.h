@@ -395,7 +395,7 @@ int dpt_regret_moments(const double* arm_value, const double* opt, int32_t N, in
 typedef struct dpt_train_desc {
     int32_t n_layer, n_embd, state_dim, action_dim, n_positions;
     int32_t batch, window;        /* sequences and tokens per sequence (1 + context length) */
-    int32_t reserved;             /* flags: DPT_TRAIN_FORWARD_ONLY or 0 */
+    int32_t reserved;             /* flags: DPT_TRAIN_FORWARD_ONLY [| DPT_TRAIN_LAST_ONLY] or 0 */
     float dropout;                /* GPT2Config embd/attn/resid_pdrop (net.py:30-32), 0 <= p < 1 */
     int32_t reserved2;            /* 0 */
     uint64_t dropout_seed;        /* Philox key of this forward's masks (a fresh one per step) */
@@ -412,6 +412,10 @@ typedef struct dpt_train_desc {
  * layer's activations and no attention probabilities or backward scratch
  * (dpt_train_workspace_numel sizes it by the flag); dpt_train_backward rejects the desc. */
 #define DPT_TRAIN_FORWARD_ONLY 1
+/* with DPT_TRAIN_FORWARD_ONLY and no dropout: preds only at the last position of each sequence
+ * (models/net.py:56-58 test mode reads preds[:, -1]); the last block runs for that position alone
+ * (its keys and values still cover the window) and the other rows of preds are left unwritten */
+#define DPT_TRAIN_LAST_ONLY 2
 int dpt_train_blob_numel(const dpt_train_desc* desc_host, int64_t* numel_out_host);
 int dpt_train_workspace_numel(const dpt_train_desc* desc_host, int64_t* numel_out_host);
 int dpt_train_forward(const dpt_train_desc* desc_host, const float* blob, const float* tokens, float* workspace,

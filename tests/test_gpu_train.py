@@ -326,6 +326,27 @@ def test_other_widths_darkroom_online(E, memo):
     assert np.array_equal(ret, ref["returns"])
 
 
+@pytest.mark.parametrize("E,T", [(16, 38), (48, 101), (64, 101), (32, 1)])
+def test_forward_last_position_only(E, T):
+    """DPT_TRAIN_LAST_ONLY (Transformer.forward in test mode without autograd): the last block runs
+    for the last position alone; preds[:, -1] agrees with the full forward-only pass within the logit
+    bar at widths on the matrix cores (16, 64), on the row kernels (48), and at T = 1 (the flag is a
+    no-op there)."""
+    from dpt_hip import train as tr
+    m = _width_model(E, 3, max(T, 2), E + T)
+    rs = np.random.RandomState(E + T)
+    B = 9
+    tok = torch.from_numpy(rs.randn(B, T, 2 + 5 + 1).astype(np.float32)).cuda()
+    dims = (m.n_layer, m.n_embd, m.state_dim, m.action_dim, m.n_positions, B, T)
+    blob = tr.pack_params(tr.param_list(m), torch.device("cuda"))
+    full, _ = tr.forward(tr.desc(*dims, flags=tr.FORWARD_ONLY), blob, tok)
+    last, _ = tr.forward(tr.desc(*dims, flags=tr.FORWARD_ONLY | tr.LAST_ONLY), blob, tok)
+    a, b = last[:, -1].cpu().numpy(), full[:, -1].cpu().numpy()
+    assert (np.abs(a - b) <= 1e-5 * np.maximum(1, np.abs(b))).all(), np.abs(a - b).max()
+    with pytest.raises(ValueError, match="LAST_ONLY"):
+        tr.forward(tr.desc(*dims, flags=tr.LAST_ONLY), blob, tok)
+
+
 def test_forward_only_workspace_and_second_backward():
     """Without autograd the generic forward runs on the forward-only workspace (DPT_TRAIN_FORWARD_ONLY:
     one layer's activations, no attention probabilities): same preds bit for bit as the training
