@@ -183,6 +183,65 @@ __global__ void tr_layernorm(const float* __restrict__ x, const float* __restric
     }
 }
 
+// tr_layernorm for rows of E <= 256 floats (E % 4 == 0): LPR lanes per row (E / 4 rounded up to a
+// power of two), 64 / LPR rows per wave, the row read once into registers (one float4 per lane) and
+// reduced over its lane group by xor shuffles.  At E = 16 a wave normalises 16 rows where
+// tr_layernorm normalises one with 16 of its 64 lanes (the inference forward's row count is tasks x
+// window, so the kernel is latency-bound on the per-row reductions, not on its bytes)
+template <int LPR>
+__global__ void tr_layernorm_rows(const float* __restrict__ x, const float* __restrict__ g,
+                                  const float* __restrict__ bb, int R, int E, float* __restrict__ y,
+                                  float* __restrict__ st) {
+    constexpr int RPW = 64 / LPR;
+    const int lane = threadIdx.x & 63, c = lane % LPR;
+    const int64_t wrow = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * RPW;
+    if (wrow >= R) return;  // whole wave past the end: no shuffle partner is left waiting
+    const int64_t row = wrow + lane / LPR;
+    const bool live = row < R, act = live && c < (E >> 2);
+    const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+    const floatx4 v = act ? reinterpret_cast<const floatx4*>(x + row * E)[c] : zero;
+    float s = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+    for (int k = 1; k < LPR; k <<= 1) s += __shfl_xor(s, k, 64);
+    const float mean = s / E;
+    const floatx4 dv = act ? v - mean : zero;
+    float q = (dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]);
+#pragma unroll
+    for (int k = 1; k < LPR; k <<= 1) q += __shfl_xor(q, k, 64);
+    const float rstd = 1.0f / sqrtf(q / E + 1e-5f);
+    if (act) {
+        floatx4 out;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r] = dv[r] * rstd * g[4 * c + r] + bb[4 * c + r];
+        reinterpret_cast<floatx4*>(y + row * E)[c] = out;
+    }
+    if (live && c == 0) {
+        st[2 * row] = mean;
+        st[2 * row + 1] = rstd;
+    }
+}
+
+// LayerNorm of R rows: the row-group kernel where E and the pointers allow float4 rows, else tr_layernorm
+static void layernorm(const float* x, const float* g, const float* bb, int R, int E, float* y, float* st,
+                      hipStream_t s) {
+    const int wpb = kTrThreads / 64;
+    if (E % 4 == 0 && E <= 256 && !(((uintptr_t)x | (uintptr_t)y) & 15)) {
+        int lpr = 1;
+        while (lpr < E / 4) lpr <<= 1;
+        const unsigned blocks = (unsigned)((R + (int64_t)wpb * (64 / lpr) - 1) / ((int64_t)wpb * (64 / lpr)));
+        switch (lpr) {
+            case 1: hipLaunchKernelGGL(tr_layernorm_rows<1>, dim3(blocks), dim3(kTrThreads), 0, s, x, g, bb, R, E, y, st); return;
+            case 2: hipLaunchKernelGGL(tr_layernorm_rows<2>, dim3(blocks), dim3(kTrThreads), 0, s, x, g, bb, R, E, y, st); return;
+            case 4: hipLaunchKernelGGL(tr_layernorm_rows<4>, dim3(blocks), dim3(kTrThreads), 0, s, x, g, bb, R, E, y, st); return;
+            case 8: hipLaunchKernelGGL(tr_layernorm_rows<8>, dim3(blocks), dim3(kTrThreads), 0, s, x, g, bb, R, E, y, st); return;
+            case 16: hipLaunchKernelGGL(tr_layernorm_rows<16>, dim3(blocks), dim3(kTrThreads), 0, s, x, g, bb, R, E, y, st); return;
+            case 32: hipLaunchKernelGGL(tr_layernorm_rows<32>, dim3(blocks), dim3(kTrThreads), 0, s, x, g, bb, R, E, y, st); return;
+            default: hipLaunchKernelGGL(tr_layernorm_rows<64>, dim3(blocks), dim3(kTrThreads), 0, s, x, g, bb, R, E, y, st); return;
+        }
+    }
+    hipLaunchKernelGGL(tr_layernorm, dim3((R + wpb - 1) / wpb), dim3(kTrThreads), 0, s, x, g, bb, R, E, y, st);
+}
+
 // Y[r][o] = bias[o] + sum_i act(X[r][i]) W[i][o] (+ res[r][o]); act = gelu_new when gelu != 0
 __global__ void tr_linear(const float* __restrict__ X, const float* __restrict__ W, const float* __restrict__ bias,
                           const float* __restrict__ res, int R, int IN, int OUT, int gelu, float* __restrict__ Y) {
@@ -1034,8 +1093,7 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
             const float* x = ws + W.x + xs(l) * RE;
             float* y1 = ws + W.y1;
             float* qkv = ws + W.qkv;
-            hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x,
-                               blob + P.ln1_g, blob + P.ln1_b, R, E, y1, ws + W.st1);
+            layernorm(x, blob + P.ln1_g, blob + P.ln1_b, R, E, y1, ws + W.st1, st);
             if (mm_fast(E))
                 mm(E, kMmQkv, y1, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, R, qkv, st);
             else
@@ -1055,15 +1113,13 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
             hipLaunchKernelGGL(tr_attn_last, dim3((Bn + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), lds, st,
                                qkv, d, ol);
             hipLaunchKernelGGL(tr_last_rows, dim3(blocks_for(BE)), dim3(kTrThreads), 0, st, x, xl, Bn, d.T, E, 0);
-            const unsigned bb = (Bn + rows_per_block - 1) / rows_per_block;
             if (mm_fast(E)) {
                 mm(E, kMmProj, ol, blob + P.proj_w, blob + P.proj_b, xl, nullptr, Bn, x2l, st);
             } else {
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(BE)), dim3(kTrThreads), 0, st, ol, blob + P.proj_w,
                                    blob + P.proj_b, xl, Bn, E, E, 0, x2l);
             }
-            hipLaunchKernelGGL(tr_layernorm, dim3(bb), dim3(kTrThreads), 0, st, x2l, blob + P.ln2_g, blob + P.ln2_b, Bn, E,
-                               y2l, ws + W.st2);
+            layernorm(x2l, blob + P.ln2_g, blob + P.ln2_b, Bn, E, y2l, ws + W.st2, st);
             if (mm_fast(E)) {
                 mm(E, kMmFc, y2l, blob + P.fc_w, blob + P.fc_b, nullptr, nullptr, Bn, hl, st);
                 mm(E, kMmMp, hl, blob + P.mp_w, blob + P.mp_b, x2l, nullptr, Bn, xnl, st);
@@ -1073,8 +1129,7 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(BE)), dim3(kTrThreads), 0, st, hl, blob + P.mp_w,
                                    blob + P.mp_b, x2l, Bn, 4 * E, E, 1, xnl);
             }
-            hipLaunchKernelGGL(tr_layernorm, dim3(bb), dim3(kTrThreads), 0, st, xnl, blob + B.lnf_g, blob + B.lnf_b, Bn, E,
-                               ws + W.yf, ws + W.stf);
+            layernorm(xnl, blob + B.lnf_g, blob + B.lnf_b, Bn, E, ws + W.yf, ws + W.stf, st);
             hipLaunchKernelGGL(tr_linear, dim3(blocks_for((int64_t)Bn * d.A)), dim3(kTrThreads), 0, st, ws + W.yf,
                                blob + B.head_w, blob + B.head_b, nullptr, Bn, E, d.A, 0, pl);
             hipLaunchKernelGGL(tr_last_rows, dim3(blocks_for((int64_t)Bn * d.A)), dim3(kTrThreads), 0, st, pl, preds, Bn,
@@ -1092,8 +1147,7 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
         float* st2 = ws + W.st2 + sl * R * 2;
         float* hpre = ws + W.hpre + sl * RE * 4;
         float* xn = ws + W.x + xs(l + 1) * RE;
-        hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x,
-                           blob + P.ln1_g, blob + P.ln1_b, R, E, y1, st1);
+        layernorm(x, blob + P.ln1_g, blob + P.ln1_b, R, E, y1, st1, st);
         const bool fast = mm_fast(E) && !drop;
         if (fast)
             mm(E, kMmQkv, y1, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, R, qkv, st);
@@ -1112,8 +1166,7 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
                                blob + P.proj_b, drop ? nullptr : x, R, E, E, 0, x2);
         if (drop)  // x2 = x + drop(o W_proj + b_proj)
             hipLaunchKernelGGL(tr_dropout, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, x2, x, RE, d, 2 + 3 * l, x2);
-        hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st, x2,
-                           blob + P.ln2_g, blob + P.ln2_b, R, E, y2, st2);
+        layernorm(x2, blob + P.ln2_g, blob + P.ln2_b, R, E, y2, st2, st);
         if (fast) {
             mm(E, kMmFc, y2, blob + P.fc_w, blob + P.fc_b, nullptr, nullptr, R, hpre, st);
             mm(E, kMmMp, hpre, blob + P.mp_w, blob + P.mp_b, x2, nullptr, R, xn, st);
@@ -1128,8 +1181,7 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
         }
         if (int rc = launched("train forward layer")) return rc;
     }
-    hipLaunchKernelGGL(tr_layernorm, dim3((R + rows_per_block - 1) / rows_per_block), dim3(kTrThreads), 0, st,
-                       ws + W.x + xs(d.L) * RE, blob + B.lnf_g, blob + B.lnf_b, R, E, ws + W.yf, ws + W.stf);
+    layernorm(ws + W.x + xs(d.L) * RE, blob + B.lnf_g, blob + B.lnf_b, R, E, ws + W.yf, ws + W.stf, st);
     hipLaunchKernelGGL(tr_linear, dim3(blocks_for((int64_t)R * d.A)), dim3(kTrThreads), 0, st, ws + W.yf,
                        blob + B.head_w, blob + B.head_b, nullptr, R, E, d.A, 0, preds);
     return launched("train forward head");
@@ -1670,8 +1722,7 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
         hipLaunchKernelGGL(gen_embed, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, ws + W.tok, blob, d, B, N, h, x);
         for (int l = 0; l < L; ++l) {
             const TrLayer P = TrLayer::make(B.layers + l * d.layer_size(), E);
-            hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x, blob + P.ln1_g, blob + P.ln1_b,
-                               N, E, y, stt);
+            layernorm(x, blob + P.ln1_g, blob + P.ln1_b, N, E, y, stt, st);
             // u = y G + g0, the folded attention over the y cache, c_proj on Wvp (GenFold)
             const float* F = ws + W.fold + l * GenFold::size(E);
             const float *G = F, *Wvp = F + (int64_t)E * E, *g0 = F + 2ll * E * E, *bvp = g0 + E;
@@ -1694,8 +1745,7 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
                 mm_dec(E, kMmProj, o, Wvp, bvp, x, N, x2, st);
             else
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, o, Wvp, bvp, x, N, E, E, 0, x2);
-            hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x2, blob + P.ln2_g, blob + P.ln2_b,
-                               N, E, y, stt);
+            layernorm(x2, blob + P.ln2_g, blob + P.ln2_b, N, E, y, stt, st);
             if (fast) {
                 mm_dec(E, kMmFc, y, blob + P.fc_w, blob + P.fc_b, nullptr, N, hb, st);
                 mm_dec(E, kMmMp, hb, blob + P.mp_w, blob + P.mp_b, x2, N, x, st);
@@ -1706,8 +1756,7 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
                                    blob + P.mp_b, x2, N, 4 * E, E, 1, x);
             }
         }
-        hipLaunchKernelGGL(tr_layernorm, dim3(row_blocks), dim3(kTrThreads), 0, st, x, blob + B.lnf_g, blob + B.lnf_b, N,
-                           E, y, stt);
+        layernorm(x, blob + B.lnf_g, blob + B.lnf_b, N, E, y, stt, st);
         hipLaunchKernelGGL(tr_linear, dim3(blocks_for((int64_t)N * d.A)), dim3(kTrThreads), 0, st, y, blob + B.head_w,
                            blob + B.head_b, nullptr, N, E, d.A, 0, ws + W.lg);
         hipLaunchKernelGGL(gen_select_env, dim3((N + 255) / 256), dim3(256), 0, st, ws + W.lg, g, h, ws + W.tok);

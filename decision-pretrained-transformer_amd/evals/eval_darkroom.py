@@ -37,7 +37,9 @@ class _GenericWindow:
     (dpt_train_forward on the forward-only workspace) over [query | context], last position."""
 
     def __init__(self, model):
+        from dpt_hip import train as tr
         self.model = model
+        self.blob = tr.pack_params(tr.param_list(model), dpt_hip.device())  # fixed for the eval
 
     def forward_window(self, query, cs=None, ca=None, cn=None, cr=None):
         x = {"query_states": query}
@@ -45,6 +47,27 @@ class _GenericWindow:
             x.update(context_states=cs, context_actions=ca, context_next_states=cn, context_rewards=cr)
         with torch.no_grad():
             return self.model._forward_generic(x)
+
+    def episode(self, n, ctx):
+        """fwd(state, rows) -> the last-position logits of tasks ``rows`` (None: all n) with their
+        current ``state`` as query: the episode's token rows (_tokens: [query | context], models/net.py
+        :42-54) are packed once, and a step rewrites the query slot and gathers the rows it forwards."""
+        from dpt_hip import train as tr
+        m = self.model
+        sd = m.state_dim
+        x = {"query_states": torch.zeros((n, sd), device=dpt_hip.device())}
+        if ctx:
+            x.update(context_states=ctx[0], context_actions=ctx[1], context_next_states=ctx[2],
+                     context_rewards=ctx[3])
+        tok = m._tokens(x)
+        flags = tr.FORWARD_ONLY | tr.LAST_ONLY  # _forward_generic's flags for a test-mode model without grad
+
+        def fwd(state, rows=None):
+            tok[:, 0, :sd].copy_(state)
+            t = tok if rows is None else tok.index_select(0, rows)
+            d = tr.desc(m.n_layer, m.n_embd, sd, m.action_dim, m.n_positions, t.shape[0], t.shape[1], flags=flags)
+            return tr.forward(d, self.blob, t)[0][:, -1]
+        return fwd
 
 
 def _window_model(model):
@@ -71,16 +94,21 @@ def _episode_device(dm, ctrl, vec_env, ctx, horizon):
         memo = torch.empty((N, dim * dim, vec_env.action_dim), dtype=torch.float32, device=dev)
         seen = torch.zeros((N, dim * dim), dtype=torch.bool, device=dev)
         rows = torch.arange(N, device=dev)
+    win = dm.episode(N, ctx) if hasattr(dm, "episode") else None
     for t in range(horizon):
         if memo is None:
-            logits = dm.forward_window(state.float(), *ctx)
+            logits = win(state) if win else dm.forward_window(state.float(), *ctx)
         else:
             cell = state[:, 0].long() * dim + state[:, 1].long()
             need = (~seen[rows, cell]).nonzero().squeeze(1)
             if need.numel():
-                lg = dm.forward_window(state.index_select(0, need).float(), *(c.index_select(0, need) for c in ctx))
-                memo[need, cell[need]] = lg
-                seen[need, cell[need]] = True
+                cn = cell.index_select(0, need)
+                if win:
+                    lg = win(state, need)
+                else:
+                    lg = dm.forward_window(state.index_select(0, need).float(), *(c.index_select(0, need) for c in ctx))
+                memo[need, cn] = lg
+                seen[need, cn] = True
             logits = memo[rows, cell]
         a = ctrl.select(logits, first_task=first_task)
         es[:, t] = state

@@ -21,12 +21,12 @@ N, Heps, horizon = int(os.environ.get("DR_N", "4096")), int(os.environ.get("DR_H
 goals = np.stack(np.unravel_index(np.arange(N) % 100, (10, 10)), 1)
 out = {}
 device_ok = eval_darkroom._device_ok
-for E in (16, 64):
+for E in (int(w) for w in os.environ.get("DR_WIDTHS", "16,64").split(",")):
     torch.manual_seed(E)
     m = Transformer(dict(horizon=horizon, state_dim=2, action_dim=5, n_layer=4, n_embd=E, n_head=1, dropout=0.0,
                          test=True)).cuda().eval()
     res = {}
-    for path in ("device_loop", "controller_loop"):
+    for path in os.environ.get("DR_PATHS", "device_loop,controller_loop").split(","):
         eval_darkroom._device_ok = device_ok if path == "device_loop" else (lambda *a: False)
         ts, rets = [], None
         for rnd in range(2):
@@ -41,6 +41,7 @@ for E in (16, 64):
         res[path] = {"ms": ts[-1] * 1e3, "env_steps_per_s": N * Heps * horizon / ts[-1],
                      "return_total": int(np.asarray(rets).sum())}
     eval_darkroom._device_ok = device_ok
-    res["speedup"] = res["controller_loop"]["ms"] / res["device_loop"]["ms"]
+    if len(res) == 2:
+        res["speedup"] = res["controller_loop"]["ms"] / res["device_loop"]["ms"]
     out[f"E{E}"] = res
 print(json.dumps({"tasks": N, "episodes": Heps, "horizon": horizon, "window": 1 + horizon, "n_layer": 4, **out}))
