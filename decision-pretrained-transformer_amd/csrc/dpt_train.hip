@@ -504,7 +504,9 @@ __global__ void tr_wpe_grad(const float* __restrict__ dx, TrDims d, float* __res
 // per workgroup.  The k order inside a lane is permuted -- lane (row i, kq) holds
 // k = kq (K/4) + s at step s, a contiguous run of its row -- and B is read at the same k.
 // EPI: bit 0 + bias[n], bit 1 + res[r][n], bit 2 x gelu'(aux[r][n]); ACT: gelu_new on X.
-constexpr int kMmBias = 1, kMmRes = 2, kMmGeluGrad = 4;
+// kMmLnIn: X's rows LayerNorm'd on load (the forward-only inference path: ln_1 -> c_attn, ln_2 -> c_fc,
+// no y1 / y2 round trip), gamma = aux[k], beta = aux[K + k] (the blob's ln_g, ln_b pair)
+constexpr int kMmBias = 1, kMmRes = 2, kMmGeluGrad = 4, kMmLnIn = 8;
 // LDS row stride of B (floats): the four 16-lane groups of a B read hit rows KS apart, so pad
 // N until two groups of one 32-lane half land 16 banks apart (2-way at worst when impossible)
 __host__ __device__ constexpr int mm_ldb(int K, int N) {
@@ -548,6 +550,35 @@ __global__ __launch_bounds__(256) void tr_mm_rows(const float* __restrict__ X, c
 #pragma unroll
         for (int q = 0; q < 4; ++q) a[4 * s4 + q] = ACT ? tr_gelu(v[q]) : v[q];
     }
+    if constexpr ((EPI & kMmLnIn) != 0) {
+        // the row's K values sit on lanes i16 + 16 kq (kq < 4), K / 4 contiguous each; the sums take
+        // tr_layernorm_rows' order (float4 partials, then a balanced pairwise tree in row order: in
+        // lane, then across the kq lanes), so y is bit-identical to the separate LayerNorm
+        static_assert(KS % 4 == 0 && ((KS / 4) & (KS / 4 - 1)) == 0, "K / 16 a power of two");
+        constexpr int NCH = KS / 4;
+        auto tree = [&](float (&p)[NCH]) {
+#pragma unroll
+            for (int w = 1; w < NCH; w <<= 1)
+#pragma unroll
+                for (int j = 0; j < NCH; j += 2 * w) p[j] += p[j + w];
+            float t = p[0];
+            t += __shfl_xor(t, 16, 64);
+            t += __shfl_xor(t, 32, 64);
+            return t;
+        };
+        float p[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) p[j] = (a[4 * j] + a[4 * j + 1]) + (a[4 * j + 2] + a[4 * j + 3]);
+        const float mean = tree(p) / K;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) a[k] -= mean;
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
+            p[j] = (a[4 * j] * a[4 * j] + a[4 * j + 1] * a[4 * j + 1]) + (a[4 * j + 2] * a[4 * j + 2] + a[4 * j + 3] * a[4 * j + 3]);
+        const float rstd = 1.0f / sqrtf(tree(p) / K + 1e-5f);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) a[k] = a[k] * rstd * aux[kq * KS + k] + aux[K + kq * KS + k];
+    }
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < NC / 16; ++c) {
@@ -564,7 +595,7 @@ __global__ __launch_bounds__(256) void tr_mm_rows(const float* __restrict__ X, c
             float v = acc[r];
             if (EPI & kMmBias) v += bias[n];
             if (EPI & kMmRes) v += res[o];
-            if (EPI & kMmGeluGrad) v *= tr_gelu_grad(aux[o]);
+            if constexpr ((EPI & kMmGeluGrad) != 0) v *= tr_gelu_grad(aux[o]);
             Y[o] = v;
         }
     }
@@ -892,7 +923,7 @@ static int ln_param_grad(const float* x, const float* stt, const float* dy, int 
 
 // ---- matrix-core dispatch (widths 16, 32, 64; other widths keep the row kernels)
 static bool mm_fast(int E) { return E == 16 || E == 32 || E == 64; }
-enum MmKind { kMmQkv, kMmProj, kMmFc, kMmMp, kMmBdMp, kMmBdFc, kMmBdProj, kMmBdQkv, kMmU };
+enum MmKind { kMmQkv, kMmProj, kMmFc, kMmMp, kMmBdMp, kMmBdFc, kMmBdProj, kMmBdQkv, kMmU, kMmLnQkv, kMmLnFc };
 
 template <class Kern>
 static void allow_lds(Kern k, size_t bytes) {
@@ -925,6 +956,9 @@ static void mm_kind(int kind, const float* X, const float* W, const float* bias,
         case kMmBdProj: launch_mm<E, E, true, false, 0>(X, W, bias, res, aux, R, Y, st); break;
         case kMmBdQkv: launch_mm<3 * E, E, true, false, 0>(X, W, bias, res, aux, R, Y, st); break;
         case kMmU: launch_mm<E, E, false, false, kMmBias>(X, W, bias, res, aux, R, Y, st); break;
+        // X = the residual stream, aux = ln_g (ln_b follows): ln_1 -> c_attn and ln_2 -> c_fc in one pass
+        case kMmLnQkv: launch_mm<E, 3 * E, false, false, kMmBias | kMmLnIn>(X, W, bias, res, aux, R, Y, st); break;
+        case kMmLnFc: launch_mm<E, 4 * E, false, false, kMmBias | kMmLnIn>(X, W, bias, res, aux, R, Y, st); break;
     }
 }
 static void mm(int E, int kind, const float* X, const float* W, const float* bias, const float* res, const float* aux,
@@ -1093,12 +1127,13 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
             const float* x = ws + W.x + xs(l) * RE;
             float* y1 = ws + W.y1;
             float* qkv = ws + W.qkv;
-            layernorm(x, blob + P.ln1_g, blob + P.ln1_b, R, E, y1, ws + W.st1, st);
-            if (mm_fast(E))
-                mm(E, kMmQkv, y1, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, R, qkv, st);
-            else
+            if (mm_fast(E)) {  // ln_1 on load (kMmLnQkv)
+                mm(E, kMmLnQkv, x, blob + P.attn_w, blob + P.attn_b, nullptr, blob + P.ln1_g, R, qkv, st);
+            } else {
+                layernorm(x, blob + P.ln1_g, blob + P.ln1_b, R, E, y1, ws + W.st1, st);
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 3)), dim3(kTrThreads), 0, st, y1, blob + P.attn_w,
                                    blob + P.attn_b, nullptr, R, E, 3 * E, 0, qkv);
+            }
             const int Bn = d.B;
             const int64_t BE = (int64_t)Bn * E;
             float* ol = ws + W.o;         // [B][E]
@@ -1119,11 +1154,11 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(BE)), dim3(kTrThreads), 0, st, ol, blob + P.proj_w,
                                    blob + P.proj_b, xl, Bn, E, E, 0, x2l);
             }
-            layernorm(x2l, blob + P.ln2_g, blob + P.ln2_b, Bn, E, y2l, ws + W.st2, st);
-            if (mm_fast(E)) {
-                mm(E, kMmFc, y2l, blob + P.fc_w, blob + P.fc_b, nullptr, nullptr, Bn, hl, st);
+            if (mm_fast(E)) {  // ln_2 on load (kMmLnFc)
+                mm(E, kMmLnFc, x2l, blob + P.fc_w, blob + P.fc_b, nullptr, blob + P.ln2_g, Bn, hl, st);
                 mm(E, kMmMp, hl, blob + P.mp_w, blob + P.mp_b, x2l, nullptr, Bn, xnl, st);
             } else {
+                layernorm(x2l, blob + P.ln2_g, blob + P.ln2_b, Bn, E, y2l, ws + W.st2, st);
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(BE * 4)), dim3(kTrThreads), 0, st, y2l, blob + P.fc_w,
                                    blob + P.fc_b, nullptr, Bn, E, 4 * E, 0, hl);
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(BE)), dim3(kTrThreads), 0, st, hl, blob + P.mp_w,
@@ -1147,9 +1182,13 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
         float* st2 = ws + W.st2 + sl * R * 2;
         float* hpre = ws + W.hpre + sl * RE * 4;
         float* xn = ws + W.x + xs(l + 1) * RE;
-        layernorm(x, blob + P.ln1_g, blob + P.ln1_b, R, E, y1, st1, st);
         const bool fast = mm_fast(E) && !drop;
-        if (fast)
+        // forward only (nothing saved for a backward): ln_1 / ln_2 applied as the products load their rows
+        const bool ln_in = fast && d.fwd_only;
+        if (!ln_in) layernorm(x, blob + P.ln1_g, blob + P.ln1_b, R, E, y1, st1, st);
+        if (ln_in)
+            mm(E, kMmLnQkv, x, blob + P.attn_w, blob + P.attn_b, nullptr, blob + P.ln1_g, R, qkv, st);
+        else if (fast)
             mm(E, kMmQkv, y1, blob + P.attn_w, blob + P.attn_b, nullptr, nullptr, R, qkv, st);
         else
             hipLaunchKernelGGL(tr_linear, dim3(blocks_for(RE * 3)), dim3(kTrThreads), 0, st, y1, blob + P.attn_w,
@@ -1166,8 +1205,11 @@ int train_forward(const TrDims& d, const float* blob, const float* tok, float* w
                                blob + P.proj_b, drop ? nullptr : x, R, E, E, 0, x2);
         if (drop)  // x2 = x + drop(o W_proj + b_proj)
             hipLaunchKernelGGL(tr_dropout, dim3(blocks_for(RE)), dim3(kTrThreads), 0, st, x2, x, RE, d, 2 + 3 * l, x2);
-        layernorm(x2, blob + P.ln2_g, blob + P.ln2_b, R, E, y2, st2, st);
-        if (fast) {
+        if (!ln_in) layernorm(x2, blob + P.ln2_g, blob + P.ln2_b, R, E, y2, st2, st);
+        if (ln_in) {
+            mm(E, kMmLnFc, x2, blob + P.fc_w, blob + P.fc_b, nullptr, blob + P.ln2_g, R, hpre, st);
+            mm(E, kMmMp, hpre, blob + P.mp_w, blob + P.mp_b, x2, nullptr, R, xn, st);
+        } else if (fast) {
             mm(E, kMmFc, y2, blob + P.fc_w, blob + P.fc_b, nullptr, nullptr, R, hpre, st);
             mm(E, kMmMp, hpre, blob + P.mp_w, blob + P.mp_b, x2, nullptr, R, xn, st);
         } else {
