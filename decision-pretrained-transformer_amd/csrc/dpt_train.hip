@@ -971,16 +971,21 @@ static void mm(int E, int kind, const float* X, const float* W, const float* bia
 // that the R / 64 row blocks times N / NC column slices fill the chip, NC = max(16, N / 4)
 template <int K, int N, bool ACT, int EPI>
 static void launch_mm_dec(const float* X, const float* W, const float* bias, const float* res, int R, float* Y,
-                          hipStream_t st) {
+                          hipStream_t st, const float* aux = nullptr) {
     constexpr int NC = N / 4 > 16 ? N / 4 : 16;
     const size_t lds = sizeof(float) * K * mm_ldb(K, NC);
     allow_lds(tr_mm_rows<K, N, false, ACT, EPI, NC>, lds);
     hipLaunchKernelGGL((tr_mm_rows<K, N, false, ACT, EPI, NC>), dim3((R + 63) / 64, N / NC), dim3(256), lds, st, X, W,
-                       bias, res, nullptr, R, Y);
+                       bias, res, aux, R, Y);
 }
+// LayerNorm on load at the widths whose row splits into a power-of-two count of float4 chunks per lane
+// (tr_layernorm_rows' summation tree without its idle lanes)
+static bool mm_ln_in_ok(int E) { return E == 16 || E == 32 || E == 64 || E == 128; }
 template <int E>
 static void mm_dec_kind(int kind, const float* X, const float* W, const float* bias, const float* res, int R, float* Y,
-                        hipStream_t st) {
+                        hipStream_t st, const float* aux = nullptr) {
+    if constexpr (E == 16 || E == 32 || E == 64 || E == 128)
+        if (kind == kMmLnFc) return launch_mm_dec<E, 4 * E, false, kMmBias | kMmLnIn>(X, W, bias, res, R, Y, st, aux);
     switch (kind) {
         case kMmU: launch_mm_dec<E, E, false, kMmBias>(X, W, bias, res, R, Y, st); break;
         case kMmProj: launch_mm_dec<E, E, false, kMmBias | kMmRes>(X, W, bias, res, R, Y, st); break;
@@ -990,12 +995,12 @@ static void mm_dec_kind(int kind, const float* X, const float* W, const float* b
 }
 static bool mm_dec_fast(int E) { return E == 16 || E == 32 || E == 48 || E == 64 || E == 128; }
 static void mm_dec(int E, int kind, const float* X, const float* W, const float* bias, const float* res, int R,
-                   float* Y, hipStream_t st) {
-    if (E == 16) mm_dec_kind<16>(kind, X, W, bias, res, R, Y, st);
-    else if (E == 32) mm_dec_kind<32>(kind, X, W, bias, res, R, Y, st);
-    else if (E == 48) mm_dec_kind<48>(kind, X, W, bias, res, R, Y, st);
-    else if (E == 64) mm_dec_kind<64>(kind, X, W, bias, res, R, Y, st);
-    else mm_dec_kind<128>(kind, X, W, bias, res, R, Y, st);
+                   float* Y, hipStream_t st, const float* aux = nullptr) {
+    if (E == 16) mm_dec_kind<16>(kind, X, W, bias, res, R, Y, st, aux);
+    else if (E == 32) mm_dec_kind<32>(kind, X, W, bias, res, R, Y, st, aux);
+    else if (E == 48) mm_dec_kind<48>(kind, X, W, bias, res, R, Y, st, aux);
+    else if (E == 64) mm_dec_kind<64>(kind, X, W, bias, res, R, Y, st, aux);
+    else mm_dec_kind<128>(kind, X, W, bias, res, R, Y, st, aux);
 }
 
 template <int IN, int OUT, bool ACT>
@@ -1787,11 +1792,15 @@ int rollout_bandit_generic(const TrDims& d, const float* blob, const dpt_bandit_
                 mm_dec(E, kMmProj, o, Wvp, bvp, x, N, x2, st);
             else
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, o, Wvp, bvp, x, N, E, E, 0, x2);
-            layernorm(x2, blob + P.ln2_g, blob + P.ln2_b, N, E, y, stt, st);
-            if (fast) {
+            if (fast && mm_ln_in_ok(E)) {  // ln_2 on load (bit-identical to the separate LayerNorm)
+                mm_dec(E, kMmLnFc, x2, blob + P.fc_w, blob + P.fc_b, nullptr, N, hb, st, blob + P.ln2_g);
+                mm_dec(E, kMmMp, hb, blob + P.mp_w, blob + P.mp_b, x2, N, x, st);
+            } else if (fast) {
+                layernorm(x2, blob + P.ln2_g, blob + P.ln2_b, N, E, y, stt, st);
                 mm_dec(E, kMmFc, y, blob + P.fc_w, blob + P.fc_b, nullptr, N, hb, st);
                 mm_dec(E, kMmMp, hb, blob + P.mp_w, blob + P.mp_b, x2, N, x, st);
             } else {
+                layernorm(x2, blob + P.ln2_g, blob + P.ln2_b, N, E, y, stt, st);
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE * 4)), dim3(kTrThreads), 0, st, y, blob + P.fc_w,
                                    blob + P.fc_b, nullptr, N, E, 4 * E, 0, hb);
                 hipLaunchKernelGGL(tr_linear, dim3(blocks_for(NE)), dim3(kTrThreads), 0, st, hb, blob + P.mp_w,
