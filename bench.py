@@ -329,6 +329,65 @@ def darkroom_workload(L, H, Heps, N, first, count, n_total, dist, memo):
                 cfg={"tasks_per_gpu": N, "horizon": H, "episodes": Heps}, sd=sd, goals=goals_all)
 
 
+def bandit_workload(wl, L, H, var, first, count, n_total, rank):
+    """BASELINE config 2 (wl "bandit": 5 arms, H=500, means ~ U(0,1)) or config 4's per-GPU shard
+    (wl "linear": 20 arms, H=1000, collect_data.py:230-231 arms, theta ~ N(0,1)/sqrt(2)): the
+    online eval (evals/eval_bandit.py:56-103 / eval_linear_bandit.py:54-97, DPT sampling
+    controller) over this rank's task block, then the regret mean / SEM curves over all tasks."""
+    import dpt_hip
+    from dpt_hip.distributed import regret_stats_allreduce
+    A, H = (5, H or 500) if wl == "bandit" else (20, H or 1000)
+    sd, _ = synthetic_state_dict(L, 1, A, H, seed=0)
+    model = dpt_hip.DeviceModel(sd, L, 1, A, 4 * (1 + H))
+    if wl == "bandit":
+        means_all = np.random.RandomState(1).uniform(0, 1, (n_total, A))  # SURVEY.md §8(d) C2
+    else:  # collect_data.py:230-231 arms; theta ~ N(0,1)/sqrt(d) (SURVEY.md §8(d) C4)
+        arms = np.random.RandomState(1234).normal(size=(A, 2)) / np.sqrt(2)
+        thetas = np.random.RandomState(2).normal(0, 1, (n_total, 2)) / np.sqrt(2)
+        means_all = np.stack([arms @ t for t in thetas])
+    means = torch.from_numpy(means_all[first:first + count]).cuda()
+    opt = means.max(dim=1, keepdim=True).values  # the Opt controller's arm value (eval_bandit.py:123-128)
+
+    def one(step_idx, ev=None):
+        if ev is not None:
+            ev[0].record()
+        out = model.rollout_bandit(means, H, var, True, seed=1000 + step_idx, first_task=first)
+        if ev is not None:  # the rollout kernel's own span (the roofline's launch duration)
+            ev[1].record()
+        # the eval's output: suboptimality / cumulative-regret mean and SEM curves over all tasks
+        # (evals/eval_bandit.py:169-178), from two all_reduces of 2 x H fp64 moments (RCCL for N>1)
+        return regret_stats_allreduce(opt, out["arm_value"], n_total)
+
+    def roofline(kern_ms, with_stream_ceiling=False):
+        # kern_ms: HIP events around the one rollout launch (draws + rollout_bandit_kernel) on the
+        # current stream
+        abytes = algorithmic_bytes(count, H, L)
+        achieved = abytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_rollout_{'bandit' if wl == 'bandit' else 'linear'}.json")
+        if os.path.exists(pmc):
+            p = json.load(open(pmc))
+            if p.get("algorithmic_bytes_per_launch") == abytes:
+                traffic = p.get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "rollout_bandit_kernel",
+                "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": abytes,
+                "kvcache_bytes_per_launch": kvcache_bytes(count, H, L)}
+        if with_stream_ceiling:
+            pin = ctypes_pin_positions(count, H, L)
+            sc = stream_ceiling(count, H, L, pin, kern_ms) if pin is not None else None
+            if sc is not None:
+                roof["stream_ceiling"] = sc
+        return roof
+
+    workload = (f"{A}-arm {'Gaussian' if wl == 'bandit' else 'linear (d=2)'} bandit online eval, DPT sampling "
+                f"policy in the loop, H={H}, {count} tasks/GPU, var={var}, L={L} E=32 1 head")
+    # rollout_bandit_kernel: fp32 VALU + v_mfma_f32_16x16x4_f32 products; env arithmetic fp64
+    dtype = "f32 (model: VALU + f32 MFMA) / f64 (env, rewards)"
+    return dict(one=one, roofline=roofline, env_steps=n_total * H, workload=workload, dtype=dtype,
+                cfg={"tasks_per_gpu": count, "horizon": H, "arms": A}, sd=sd, means_all=means_all, H=H, A=A)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -342,6 +401,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-darkroom", action="store_true",
                     help="bandit: skip the DarkRoom sub-object (darkroom_c3 / darkroom_c5_shard)")
+    ap.add_argument("--no-linear", action="store_true",
+                    help="bandit: skip the linear_c4_shard sub-object (BASELINE config 4's per-GPU shard)")
     ap.add_argument("--darkroom-memo", type=int, choices=(0, 1), default=1,
                     help="darkroom: 1 = one window forward per distinct state per episode, 0 = one per step")
     args = ap.parse_args()
@@ -361,42 +422,16 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-    import dpt_hip
-    from dpt_hip.distributed import regret_stats_allreduce, shard
+    from dpt_hip.distributed import shard
 
     N, L, wl = args.tasks, args.layers, args.workload
     n_total = N * world
     first, count = shard(n_total, world, rank)
     if wl in ("bandit", "linear"):
-        A, H = (5, args.H or 500) if wl == "bandit" else (20, args.H or 1000)
-        sd, _ = synthetic_state_dict(L, 1, A, H, seed=0)
-        model = dpt_hip.DeviceModel(sd, L, 1, A, 4 * (1 + H))
-        if wl == "bandit":
-            means_all = np.random.RandomState(1).uniform(0, 1, (n_total, A))
-        else:  # collect_data.py:230-231 arms; theta ~ N(0,1)/sqrt(d)
-            arms = np.random.RandomState(1234).normal(size=(A, 2)) / np.sqrt(2)
-            thetas = np.random.RandomState(2).normal(0, 1, (n_total, 2)) / np.sqrt(2)
-            means_all = np.stack([arms @ t for t in thetas])
-        means = torch.from_numpy(means_all[first:first + count]).cuda()
-
-        opt = means.max(dim=1, keepdim=True).values  # the Opt controller's arm value (eval_bandit.py:123-128)
-
-        def one(step_idx, ev=None):
-            if ev is not None:
-                ev[0].record()
-            out = model.rollout_bandit(means, H, args.var, True, seed=1000 + step_idx, first_task=first)
-            if ev is not None:  # the rollout kernel's own span (the roofline's launch duration)
-                ev[1].record()
-            # the eval's output: suboptimality / cumulative-regret mean and SEM curves over all tasks
-            # (evals/eval_bandit.py:169-178), from two all_reduces of 2 x H fp64 moments (RCCL for N>1)
-            return regret_stats_allreduce(opt, out["arm_value"], n_total)
-
-        env_steps_per_step = n_total * H
-        workload = (f"{A}-arm {'Gaussian' if wl == 'bandit' else 'linear (d=2)'} bandit online eval, DPT sampling "
-                    f"policy in the loop, H={H}, {N} tasks/GPU, var={args.var}, L={L} E=32 1 head")
-        cfg = {"tasks_per_gpu": N, "horizon": H, "arms": A}
-        # rollout_bandit_kernel: fp32 VALU + v_mfma_f32_16x16x4_f32 products; env arithmetic fp64
-        dtype = "f32 (model: VALU + f32 MFMA) / f64 (env, rewards)"
+        bw = bandit_workload(wl, L, args.H, args.var, first, count, n_total, rank)
+        one, env_steps_per_step, workload, cfg, dtype = bw["one"], bw["env_steps"], bw["workload"], bw["cfg"], \
+            bw["dtype"]
+        sd, means_all, H, A = bw["sd"], bw["means_all"], bw["H"], bw["A"]
     else:
         H, Heps = args.H or 100, 40
         dw = darkroom_workload(L, H, Heps, N, first, count, n_total, dist, args.darkroom_memo)
@@ -406,25 +441,7 @@ def main():
     elapsed, kern_ms = run_timed(one, args.steps, args.warmup, dist, backend, wl in ("bandit", "linear"))
     value = env_steps_per_step * args.steps / elapsed
     if wl in ("bandit", "linear"):
-        # kern_ms: HIP events around the one rollout launch (draws + rollout_bandit_kernel) on the
-        # current stream
-        abytes = algorithmic_bytes(count, H, L)
-        achieved = abytes / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_rollout_bandit.json")
-        if wl == "bandit" and os.path.exists(pmc):
-            p = json.load(open(pmc))
-            if p.get("algorithmic_bytes_per_launch") == abytes:
-                traffic = p.get("hbm_bytes_per_launch")
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "rollout_bandit_kernel",
-                "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": abytes,
-                "kvcache_bytes_per_launch": kvcache_bytes(count, H, L)}
-        if rank == 0:
-            pin = ctypes_pin_positions(count, H, L)
-            sc = stream_ceiling(count, H, L, pin, kern_ms) if pin is not None else None
-            if sc is not None:
-                roof["stream_ceiling"] = sc
+        roof = bw["roofline"](kern_ms, with_stream_ceiling=rank == 0)
     else:
         roof = dw["roofline"](kern_ms)
     line = {
@@ -469,6 +486,35 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             sub["cpu_baseline"] = cpu_baseline_darkroom(dw["sd"], dw["goals"], 100, L)
         line["darkroom_c3" if world == 1 else "darkroom_c5_shard"] = sub
+        if world == 1:
+            # config 5's per-GPU shard on one GPU: rank 0's 8192 of the 65,536 tasks (goals of the
+            # global ids, Philox keyed by the global task id), one timed step
+            dw = darkroom_workload(L, 100, 40, 8192, 0, 8192, 65536, None, 1)
+            c5_steps = 1
+            el, km = run_timed(dw["one"], c5_steps, 1, None, backend, False)
+            env5 = 8192 * 40 * 100
+            line["darkroom_c5_shard"] = {
+                "metric": "env-steps/sec (DarkRoom online eval, DPT policy in loop)",
+                "value": env5 * c5_steps / el, "unit": "env-steps/s (one GPU's shard)", "steps": c5_steps,
+                "warmup": 1, "ms_per_step": el / c5_steps * 1e3, "dtype": dw["dtype"],
+                "config": {"workload": dw["workload"].replace("65536 tasks/GPU", "8192 tasks/GPU") +
+                           " (rank 0 of BASELINE config 5: 65,536 tasks over 8 GPUs)",
+                           "env_steps_per_step": env5, "tasks_per_gpu": 8192, "horizon": 100, "episodes": 40},
+                "roofline": dw["roofline"](km)}
+    if wl == "bandit" and not args.no_linear:
+        # BASELINE config 4 (20-arm linear, H=1000, 32,768 tasks over 8 GPUs): its 4096-task per-GPU
+        # shard on every rank (config 4 itself at 8 GPUs), two timed steps
+        f_l, c_l = shard(4096 * world, world, rank)
+        lw = bandit_workload("linear", L, None, args.var, f_l, c_l, 4096 * world, rank)
+        lin_steps = 2
+        el, km = run_timed(lw["one"], lin_steps, 1, dist, backend, True)
+        line["linear_c4_shard" if world < 8 else "linear_c4"] = {
+            "metric": "env-steps/sec (20-arm linear bandit online eval, DPT policy in loop)",
+            "value": lw["env_steps"] * lin_steps / el, "unit": "env-steps/s (whole job, all GPUs)",
+            "steps": lin_steps, "warmup": 1, "ms_per_step": el / lin_steps * 1e3, "dtype": lw["dtype"],
+            "config": dict(workload=lw["workload"] + " (BASELINE config 4: 32,768 tasks over 8 GPUs)",
+                           env_steps_per_step=lw["env_steps"], **lw["cfg"]),
+            "roofline": lw["roofline"](km)}
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:

@@ -220,7 +220,11 @@ int dpt_tuning_set(int32_t key, int64_t value) {
         return DPT_OK;
     }
     if (key == DPT_TUNE_POLICY_WAVE) {
-        REQUIRE(set_policy_wave((int)value) == DPT_OK, "policy wave kernel %lld: 0 or 1", (long long)value);
+        if (set_policy_wave((int)value) != DPT_OK) {
+            set_error(DPT_EUNSUPPORTED, "policy kernel %lld: only 1 (the wave-per-task kernel; the lane kernel "
+                      "was retired)", (long long)value);
+            return DPT_EUNSUPPORTED;
+        }
         return DPT_OK;
     }
     if (key == DPT_TUNE_BLOCK0_MFMA) {
@@ -419,9 +423,9 @@ int dpt_rollin_darkroom(const int32_t* goal, const int32_t* perm, int32_t N, int
 
 int dpt_policy_workspace_numel(int32_t N, int32_t A, int32_t H, int64_t* numel) {
     REQUIRE(numel && N >= 1 && A >= 1 && H >= 1, "N=%d A=%d H=%d", N, A, H);
-    // per-arm reward lists [A][H][N]; LinUCB keeps its context there instead (fp64 rewards +
-    // int32 arm indices per (k, task): 1.5 doubles), hence at least 2 doubles per (k, task)
-    *numel = (int64_t)(A < 2 ? 2 : A) * H * N;
+    // 0 since round 6: the policy kernel keeps each task's context in LDS (the retired lane kernel
+    // kept per-arm reward lists here)
+    *numel = 0;
     return DPT_OK;
 }
 
@@ -432,8 +436,6 @@ int dpt_rollout_policy(const dpt_policy_rollout_args* a, void* stream) {
     REQUIRE(a->C == 0 || (a->ctx_actions && a->ctx_rewards), "null prefix context with C=%d", a->C);
     REQUIRE(a->means && a->actions_out && a->rewards_out && a->arm_value_out, "null pointer");
     REQUIRE(a->policy >= DPT_POLICY_OPT && a->policy <= DPT_POLICY_LINUCB, "policy=%d", a->policy);
-    REQUIRE(a->policy == DPT_POLICY_OPT || a->workspace,
-            "policy %d needs the per-arm workspace", a->policy);
     REQUIRE(a->policy != DPT_POLICY_LINUCB || (a->arms && a->lin_d >= 1 && a->lin_d <= 8), "LinUCB needs arms, d<=8");
     if (a->type != DPT_BANDIT_GAUSSIAN && a->type != DPT_BANDIT_BERNOULLI) {
         set_error(DPT_EUNSUPPORTED, "bandit type %d", a->type);

@@ -4,70 +4,16 @@
 // LinUCBPolicy (:447-528) and OptPolicy (:22-38), each stepped inside
 // evals/eval_bandit.py:56-103 deploy_online_vec.
 //
-// One lane per task runs all H steps.  The reference recomputes every
-// per-arm statistic from the whole context each step with numpy (fp64,
-// pairwise summation), so the per-arm reward lists are kept in a workspace laid
-// out [arm][k][task] (lane-contiguous: coalesced) and summed with numpy's
-// pairwise order each step: means, bounds and therefore action indices are
-// bit-identical to the reference for the same draws (LinUCB: see linucb_choose).
+// One 64-lane workgroup per task runs all H steps with the task's context in LDS.
+// The reference recomputes every per-arm statistic from the whole context each
+// step with numpy (fp64, pairwise summation); the kernel sums the per-arm reward
+// lists in numpy's pairwise order each step, so means, bounds and therefore action
+// indices are bit-identical to the reference for the same draws (LinUCB: the BLAS
+// orders of dpt_linucb.h).
 #include "dpt_common.h"
 #include "dpt_linucb.h"
 
 namespace dpt {
-
-constexpr int kPolThreads = 128;  // launch bound
-#ifndef DPT_POL_BLOCK
-#define DPT_POL_BLOCK 64
-#endif
-constexpr int kPolBlock = DPT_POL_BLOCK;  // lanes per workgroup at launch
-
-// numpy pairwise_sum for float64 over a strided sequence x[k*stride], k < n
-// (loops_utils.h.src): blocks of <= 128 with 8 partials, recursive halving above.
-__device__ double pw_block(const double* x, size_t stride, int n) {
-    if (n < 8) {
-        double res = 0.0;
-        for (int i = 0; i < n; ++i) res += x[(size_t)i * stride];
-        return res;
-    }
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = x[(size_t)j * stride];
-    int i = 8;
-    for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] += x[(size_t)(i + j) * stride];
-    }
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res += x[(size_t)i * stride];
-    return res;
-}
-
-__device__ double pw_sum(const double* x, size_t stride, int n) {
-    // explicit recursion unrolled to depth 4 (n <= 2048)
-    if (n <= 128) return pw_block(x, stride, n);
-    int a = n / 2;
-    a -= a % 8;
-    auto lvl2 = [&](const double* y, int m) -> double {
-        if (m <= 128) return pw_block(y, stride, m);
-        int b = m / 2;
-        b -= b % 8;
-        auto lvl3 = [&](const double* z, int k) -> double {
-            if (k <= 128) return pw_block(z, stride, k);
-            int c = k / 2;
-            c -= c % 8;
-            auto lvl4 = [&](const double* w, int q) -> double {
-                if (q <= 128) return pw_block(w, stride, q);
-                int d = q / 2;
-                d -= d % 8;
-                return pw_block(w, stride, d) + pw_block(w + (size_t)d * stride, stride, q - d);
-            };
-            return lvl4(z, c) + lvl4(z + (size_t)c * stride, k - c);
-        };
-        return lvl3(y, b) + lvl3(y + (size_t)b * stride, m - b);
-    };
-    return lvl2(x, a) + lvl2(x + (size_t)a * stride, n - a);
-}
-
 
 struct PolicyParams {
     int N, H, A, policy, online, type, sample, d, C, step0;
@@ -80,165 +26,29 @@ struct PolicyParams {
     const double* arms;
     const double* noise;
     const double* policy_noise;
-    double* lists;   // [A][H][N]
     int32_t* actions_out;
     double* rewards_out;
     double* arm_value_out;
 };
 
-// LIN: the LinUCB instantiation (its own kernel, so the per-arm-sum policies keep their code and
-// registers); LinUCB's arm features (A x d) sit in LDS, read by every transition of every step.
-template <bool LIN>
-__global__ __launch_bounds__(kPolThreads) void rollout_policy_kernel(PolicyParams P) {
-    __shared__ double arms_s[LIN ? kMaxA * kMaxD : 1];
-    if constexpr (LIN) {
-        for (int t = threadIdx.x; t < P.A * P.d; t += blockDim.x) arms_s[t] = P.arms[t];
-        __syncthreads();
-    }
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.N) return;
-    const int A = P.A;
-    const int64_t task = P.first_task + i;
-    const double* mrow = P.means + (size_t)i * A;
-    int cnt[kMaxA];
-    for (int k = 0; k < A; ++k) cnt[k] = 0;
-    int opt = 0;
-    for (int k = 1; k < A; ++k)
-        if (mrow[k] > mrow[opt]) opt = k;
-    const int L = P.C + P.H;                   // list capacity per arm
-    const size_t lstride = (size_t)L * P.N;    // arm stride of the lists
-    // LinUCB keeps the context itself in the workspace (it re-reads it every step):
-    // rewards [k][task] fp64, then arm indices [k][task] int32, lane-contiguous
-    constexpr bool lin = LIN;
-    double* lin_r = P.lists;
-    int32_t* lin_a = reinterpret_cast<int32_t*>(P.lists + lstride);
-    int n_ctx = 0;
-    auto append = [&](int a, double r) {
-        if (lin) {
-            lin_r[(size_t)n_ctx * P.N + i] = r;
-            lin_a[(size_t)n_ctx * P.N + i] = a;
-        } else if (P.lists) {
-            P.lists[a * lstride + (size_t)cnt[a] * P.N + i] = r;
-        }
-        ++cnt[a];
-        ++n_ctx;
-    };
-    for (int c = 0; c < P.C; ++c)  // prefix context (set_batch_numpy_vec), time order
-        append(P.ctx_actions[(size_t)i * P.C + c], P.ctx_rewards[(size_t)i * P.C + c]);
-    for (int h = 0; h < P.H; ++h) {
-        int a = 0;
-        if (!LIN && P.policy == DPT_POLICY_OPT) {
-            a = opt;
-        } else if constexpr (LIN) {
-            if (P.C + h == 0) {  // np.random.choice(np.arange(dim)) for an empty context
-                const double u = P.policy_noise ? P.policy_noise[(size_t)i]
-                                                : philox_uniform(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_POLICY);
-                a = min((int)(u * A), A - 1);
-            } else {
-                a = linucb_choose([&](int k) { return lin_a[(size_t)k * P.N + i]; },
-                                  [&](int k) { return lin_r[(size_t)k * P.N + i]; }, n_ctx, arms_s, A, P.d, P.c);
-            }
-        } else {
-            // per-arm sums over the context (numpy pairwise order, fp64)
-            double bmean[kMaxA];
-            for (int k = 0; k < A; ++k) {
-                const double s = cnt[k] ? pw_sum(P.lists + k * lstride + i, P.N, cnt[k]) : 0.0;
-                bmean[k] = (P.policy == DPT_POLICY_THOMPSON) ? (cnt[k] ? s / cnt[k] : 0.0) : s / fmax(1.0, (double)cnt[k]);
-            }
-            int amin = 0;
-            for (int k = 1; k < A; ++k)
-                if (cnt[k] < cnt[amin]) amin = k;
-            if (P.policy == DPT_POLICY_THOMPSON) {
-                const double variance = P.ts_std * P.ts_std, pv = P.ts_prior_var, pm = P.ts_prior_mean;
-                double post_m[kMaxA], post_s[kMaxA];
-                for (int k = 0; k < A; ++k) {
-                    if (cnt[k] > 0) {  // update_posterior_all (ctrl_bandit.py:218-226)
-                        const double n = (double)cnt[k];
-                        const double w = variance / (variance + n * pv);
-                        post_m[k] = w * pm + (1.0 - w) * bmean[k];
-                        post_s[k] = sqrt(1.0 / (1.0 / pv + n / variance));
-                    } else {
-                        post_m[k] = pm;
-                        post_s[k] = sqrt(pv);
-                    }
-                }
-                if (P.sample) {  // values = normal(means, sqrt(variances)); argmax
-                    double best = -INFINITY;
-                    for (int k = 0; k < A; ++k) {
-                        const double g = P.policy_noise ? P.policy_noise[((size_t)h * P.N + i) * A + k]
-                                                        : philox_normal(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_POLICY + k);
-                        const double v = post_m[k] + post_s[k] * g;
-                        if (v > best) { best = v; a = k; }
-                    }
-                } else {  // 100 posterior draws, most frequent argmax (ctrl_bandit.py:238-244)
-                    int freq[kMaxA];
-                    for (int k = 0; k < A; ++k) freq[k] = 0;
-                    for (int s = 0; s < 100; ++s) {
-                        double best = -INFINITY;
-                        int am = 0;
-                        for (int k = 0; k < A; ++k) {
-                            const double g = P.policy_noise
-                                                 ? P.policy_noise[(((size_t)h * 100 + s) * P.N + i) * A + k]
-                                                 : philox_normal(P.seed, ((uint64_t)P.step0 + h) * 128 + s, task,
-                                                                 DPT_STREAM_POLICY + k);
-                            const double v = post_m[k] + post_s[k] * g;
-                            if (v > best) { best = v; am = k; }
-                        }
-                        ++freq[am];
-                    }
-                    for (int k = 1; k < A; ++k)
-                        if (freq[k] > freq[a]) a = k;
-                }
-            } else {
-                double best = -INFINITY;
-                for (int k = 0; k < A; ++k) {
-                    double v = bmean[k];
-                    if (P.policy != DPT_POLICY_EMP) {  // UCB / LCB bonus c / max(1, sqrt(n))
-                        const double bon = P.c / fmax(1.0, sqrt((double)cnt[k]));
-                        v = (P.policy == DPT_POLICY_UCB) ? v + bon : v - bon;
-                    }
-                    if (v > best) { best = v; a = k; }
-                }
-                // EmpMean(online) and UCB play an unseen arm first (ctrl_bandit.py:107-110, :373-375)
-                if ((P.policy == DPT_POLICY_UCB || (P.policy == DPT_POLICY_EMP && P.online)) && cnt[amin] == 0)
-                    a = amin;
-            }
-        }
-        // env step (BanditEnv.transit, envs/bandit_env.py:56-64)
-        const double mean = mrow[a];
-        double r;
-        if (P.type == DPT_BANDIT_BERNOULLI) {
-            const double ur = P.noise ? P.noise[(size_t)h * P.N + i] : philox_uniform(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_REWARD);
-            r = (ur < mean) ? 1.0 : 0.0;
-        } else {
-            const double g = P.noise ? P.noise[(size_t)h * P.N + i] : philox_normal(P.seed, (uint64_t)P.step0 + h, task, DPT_STREAM_REWARD);
-            r = gaussian_reward(mean, P.var, g);
-        }
-        append(a, r);
-        P.actions_out[(size_t)i * P.H + h] = a;
-        P.rewards_out[(size_t)i * P.H + h] = r;
-        P.arm_value_out[(size_t)i * P.H + h] = mean;
-    }
-}
-
 // ----------------------------------------------------------------------------- wave per task
-// rollout_policy_kernel gives each task one lane, so 4096 tasks are 64 waves on a 1024-SIMD chip,
-// and each lane walks its A reward lists one after the other.  rollout_policy_wave_kernel gives
-// each task a 64-lane workgroup and keeps the task's whole context in LDS:
+// Each task gets a 64-lane workgroup and keeps its whole context in LDS (C + H <= 2048, so at most
+// ~36 KB at kMaxA arms):
 //  * per-arm sums: 8 lanes per arm (8 arms at a time), lane c runs numpy's pairwise chain c of
 //    every 128-element leaf (r[c] += x[8t + c]); the 8 chains combine by a xor 1 / 2 / 4
 //    butterfly, which is exactly ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)); the tail and
-//    the recursive halving above 128 follow pairwise_sum, so every sum is bit-identical to the
-//    lane kernel's pw_sum and to numpy's;
+//    the recursive halving above 128 follow pairwise_sum, so every sum is bit-identical to
+//    numpy's (loops_utils.h.src pairwise_sum);
 //  * the lists are 8-element chunks of one pool, in arrival order (element j of arm a sits at
-//    pool[tab[a][j / 8] * 8 + j % 8]): Σ_a ceil(cnt_a / 8) <= cap / 8 + A chunks, instead of A
+//    pool[tab[a][j / 8] * 8 + j % 8]): sum_a ceil(cnt_a / 8) <= cap / 8 + A chunks, instead of A
 //    lists of full capacity;
 //  * LinUCB: X^T X entries on d(d+1)/2 lanes, ci . x of every arm on d * A lanes (the per-k
 //    factor m(k) of theta's dgemv_t depends on the arm index alone), theta's rows on d lanes,
-//    the arm values on A lanes, all in the BLAS orders of linucb_choose;
+//    the arm values on A lanes, all in the BLAS orders of dpt_linucb.h;
 //  * selection, the env step and the appends on lane 0, which owns the step's outputs.
-// Same arithmetic in the same order as rollout_policy_kernel, so the two are bit-identical
-// (tested); the lane kernel stays for contexts whose lists do not fit in LDS.
+// Round 6 retired the round-4 lane-per-task kernel (one lane per task, lists in a global
+// workspace): it only served contexts too large for LDS, which the C + H <= 2048 bound of the
+// pairwise depth never produces.
 constexpr int kPwLeaf = 128;  // numpy PW_BLOCKSIZE
 
 struct WaveLds {
@@ -557,11 +367,9 @@ __global__ __launch_bounds__(64) void rollout_policy_wave_kernel(PolicyParams P)
     }
 }
 
-static bool g_policy_wave = true;  // DPT_TUNE_POLICY_WAVE
-
 int set_policy_wave(int on) {
-    if (on != 0 && on != 1) return DPT_EINVAL;
-    g_policy_wave = on == 1;
+    // DPT_TUNE_POLICY_WAVE: 1 is the only kernel (the lane-per-task form was retired in round 6)
+    if (on != 1) return DPT_EUNSUPPORTED;
     return DPT_OK;
 }
 
@@ -571,30 +379,22 @@ int launch_rollout_policy(const dpt_policy_rollout_args& a, hipStream_t st) {
     P.sample = a.sample; P.d = a.lin_d; P.C = a.C; P.step0 = a.step0; P.ctx_actions = a.ctx_actions; P.ctx_rewards = a.ctx_rewards;
     P.first_task = a.first_task; P.var = a.var; P.c = a.c;
     P.ts_std = a.ts_std; P.ts_prior_mean = a.ts_prior_mean; P.ts_prior_var = a.ts_prior_var; P.seed = a.seed;
-    P.means = a.means; P.arms = a.arms; P.noise = a.noise; P.policy_noise = a.policy_noise; P.lists = a.workspace;
+    P.means = a.means; P.arms = a.arms; P.noise = a.noise; P.policy_noise = a.policy_noise;
     P.actions_out = a.actions_out; P.rewards_out = a.rewards_out; P.arm_value_out = a.arm_value_out;
     const bool lin = a.policy == DPT_POLICY_LINUCB;
-    if (g_policy_wave) {
-        const size_t lds = (size_t)WaveLds::make(a.A, a.C + a.H, lin, a.lin_d).total;
-        if (lds <= 160 * 1024) {
-            const void* kern = lin ? reinterpret_cast<const void*>(rollout_policy_wave_kernel<true>)
-                                   : reinterpret_cast<const void*>(rollout_policy_wave_kernel<false>);
-            if (lds > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (lin)
-                hipLaunchKernelGGL(rollout_policy_wave_kernel<true>, dim3(a.N), dim3(64), lds, st, P);
-            else
-                hipLaunchKernelGGL(rollout_policy_wave_kernel<false>, dim3(a.N), dim3(64), lds, st, P);
-            return check_hip(hipGetLastError(), "rollout_policy_wave_kernel launch");
-        }
+    const size_t lds = (size_t)WaveLds::make(a.A, a.C + a.H, lin, a.lin_d).total;
+    if (lds > 160 * 1024) {  // unreachable under dpt_rollout_policy's C + H <= 2048, A <= kMaxA
+        set_error(DPT_EUNSUPPORTED, "policy context of %d steps x %d arms needs %zu B of LDS", a.C + a.H, a.A, lds);
+        return DPT_EUNSUPPORTED;
     }
-    // one lane per task, so 4096 tasks fill only 32..64 CUs: 64-lane workgroups spread them wider
-    const int bs = kPolBlock;
-    const dim3 grid((a.N + bs - 1) / bs);
-    if (a.policy == DPT_POLICY_LINUCB)
-        hipLaunchKernelGGL(rollout_policy_kernel<true>, grid, dim3(bs), 0, st, P);
+    const void* kern = lin ? reinterpret_cast<const void*>(rollout_policy_wave_kernel<true>)
+                           : reinterpret_cast<const void*>(rollout_policy_wave_kernel<false>);
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (lin)
+        hipLaunchKernelGGL(rollout_policy_wave_kernel<true>, dim3(a.N), dim3(64), lds, st, P);
     else
-        hipLaunchKernelGGL(rollout_policy_kernel<false>, grid, dim3(bs), 0, st, P);
-    return check_hip(hipGetLastError(), "rollout_policy_kernel launch");
+        hipLaunchKernelGGL(rollout_policy_wave_kernel<false>, dim3(a.N), dim3(64), lds, st, P);
+    return check_hip(hipGetLastError(), "rollout_policy_wave_kernel launch");
 }
 
 }  // namespace dpt

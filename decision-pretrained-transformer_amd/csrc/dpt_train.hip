@@ -155,9 +155,10 @@ __device__ inline float tr_keep(const TrDims& d, int site, int64_t e) {
 }
 
 // out[i] = (add ? add[i] : 0) + x[i] keep(site, i) over n elements: the dropout of the embedding
-// (in place), the residual adds x + drop(y) after c_proj / mlp.c_proj, and the gradients through them
-__global__ void tr_dropout(const float* __restrict__ x, const float* __restrict__ add, int64_t n, TrDims d, int site,
-                           float* __restrict__ out) {
+// (in place), the residual adds x + drop(y) after c_proj / mlp.c_proj, and the gradients through them.
+// Launched in place (out == x, and out == add), so no pointer is __restrict__: each thread reads
+// its own element before writing it.
+__global__ void tr_dropout(const float* x, const float* add, int64_t n, TrDims d, int site, float* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float v = x[i] * tr_keep(d, site, i);

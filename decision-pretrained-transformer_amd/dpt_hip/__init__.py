@@ -358,8 +358,8 @@ def rollout_policy(policy, means, H, var, bandit_type=BANDIT_GAUSSIAN, online=Tr
         elif int(policy) == POLICY_LINUCB and got < N:  # only step 0's row (N,) is read
             raise ValueError(f"policy_noise has {got} draws; LinUCB reads the first {N}")
     n = ctypes.c_int64()
-    _lib.call("dpt_policy_workspace_numel", N, A, C + H, ctypes.byref(n))
-    ws = torch.empty(n.value, dtype=torch.float64, device=dev)
+    _lib.call("dpt_policy_workspace_numel", N, A, C + H, ctypes.byref(n))  # 0: contexts live in LDS
+    ws = torch.empty(max(n.value, 1), dtype=torch.float64, device=dev)
     out = dict(actions=torch.empty((N, H), dtype=torch.int32, device=dev),
                rewards=torch.empty((N, H), dtype=torch.float64, device=dev),
                arm_value=torch.empty((N, H), dtype=torch.float64, device=dev))
@@ -423,12 +423,6 @@ def set_select_fast(on):
     """select_action for 5 and 20 arms: the fp32 cdf with the exact fp64 cdf within 2^-15 of an edge
     (default), or the fp64 cdf for every sample.  Bit-identical either way."""
     _lib.call("dpt_tuning_set", _lib.TUNE_SELECT_FAST, int(bool(on)))
-
-
-def set_policy_wave(on):
-    """dpt_rollout_policy: one 64-lane workgroup per task with its context in LDS (default) or one
-    lane per task.  Bit-identical either way."""
-    _lib.call("dpt_tuning_set", _lib.TUNE_POLICY_WAVE, int(bool(on)))
 
 
 _darkroom_memo = True

@@ -42,10 +42,13 @@ def deploy_online(env, controller, horizon):
 
 
 def _fused_ok(vec_env, controller, horizon):
+    """The one-launch rollout: our controller, env and model, with no dropout in play (a
+    training-mode model with dropout > 0 takes the per-step loop, whose forward applies it)."""
     from models.net import Transformer
+    m = controller.model
     return (isinstance(controller, BanditTransformerController) and isinstance(vec_env, BanditEnvVec)
-            and isinstance(controller.model, Transformer) and controller.model.state_dim == 1
-            and controller.batch_size == vec_env.num_envs and horizon <= controller.model.n_positions)
+            and isinstance(m, Transformer) and m.state_dim == 1 and not (m.training and m.dropout > 0)
+            and controller.batch_size == vec_env.num_envs and horizon <= m.n_positions)
 
 
 def rollout_fused(vec_env, controller, horizon, uniforms=None, noise=None, seed=None, first_task=None):

@@ -24,12 +24,13 @@ device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
 def _device_ok(vec_env, controller):
     """The per-step device loop: our controller, env and model.  Width 32 forwards through the packed
     device model; other widths through the generic kernels (_GenericWindow), for an inference-mode
-    model (test: the last position's logits; no dropout in play)."""
+    model (test: the last position's logits).  At every width no dropout may be in play: a
+    training-mode model with dropout > 0 takes the controller's loop, whose forward applies it."""
     from models.net import Transformer
     m = controller.model
     return (isinstance(controller, DarkroomTransformerController) and isinstance(vec_env, DarkroomEnvVec)
             and isinstance(m, Transformer) and controller.batch_size == vec_env.num_envs
-            and (m.n_embd == dpt_hip.E or (m.test and not (m.training and m.dropout > 0))))
+            and not (m.training and m.dropout > 0) and (m.n_embd == dpt_hip.E or m.test))
 
 
 class _GenericWindow:

@@ -70,6 +70,23 @@ class GPT2Stack(nn.Module):
         self.ln_f = nn.LayerNorm(E, eps=1e-5)
 
 
+def _dropout_seed():
+    """A fresh Philox seed for one dropout call, from the CUDA generator as the reference's dropout
+    draws its masks: the seed mixes the generator's initial seed with its Philox offset, and the
+    offset advances as a dropout kernel would advance it.  torch.manual_seed (which resets the
+    offset) reproduces a run, no device synchronisation is needed, and the CPU stream -- the
+    DataLoader shuffle (train.py:203,249) and the per-item context permutation (dataset.py:85) --
+    never sees dropout, as in the reference."""
+    dev = dpt_hip.device()
+    g = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+    off = g.get_offset()
+    g.set_offset(off + 4)
+    z = (g.initial_seed() * 0x9E3779B97F4A7C15 + off + 1) & 0xFFFFFFFFFFFFFFFF  # splitmix64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return (z ^ (z >> 31)) & ((1 << 62) - 1)
+
+
 class Transformer(nn.Module):
     """Transformer class (models/net.py:9-60)."""
 
@@ -156,8 +173,8 @@ class Transformer(nn.Module):
         tok = self._tokens(x)
         grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         p, seed = 0.0, 0
-        if self.training and self.dropout > 0:  # fresh masks per call, from torch's (seedable) CPU generator
-            p, seed = float(self.dropout), int(torch.randint(0, 2 ** 62, (1,)).item())
+        if self.training and self.dropout > 0:  # fresh masks per call (_dropout_seed)
+            p, seed = float(self.dropout), _dropout_seed()
         # inference in test mode reads the last position only (LAST_ONLY: the last block for that row alone)
         flags = 0 if grad else tr.FORWARD_ONLY | (tr.LAST_ONLY if self.test and p == 0.0 else 0)
         dims = (self.n_layer, self.n_embd, self.state_dim, self.action_dim, self.n_positions, tok.shape[0],
@@ -179,8 +196,9 @@ class Transformer(nn.Module):
         Dropout: the reference's GPT2Config applies embd/attn/resid dropout with p = ``dropout``
         (models/net.py:30-32) in training mode -- with or without grad (train.py:265-278's test
         loss runs in training mode).  Such calls take the training kernels with dropout: masks
-        from Philox keyed by a seed drawn from torch's CPU generator per call (include/dpt_hip.h
-        dpt_train_desc), the same distribution as torch's dropout, not its random stream."""
+        from Philox keyed by a seed taken per call from the CUDA generator (_dropout_seed;
+        include/dpt_hip.h dpt_train_desc), the same distribution as torch's dropout, not its
+        random stream."""
         if (self.training and (self.dropout > 0 or (torch.is_grad_enabled()
                                                     and any(p.requires_grad for p in self.parameters())))) \
                 or self.n_embd != dpt_hip.E:

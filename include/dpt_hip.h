@@ -88,10 +88,10 @@ const char* dpt_last_error(void);
  * samples on the fp32 cdf when the uniform is more than 2^-15 from every cdf
  * edge and runs the exact fp64 cdf otherwise (the rollouts always do); 0: the
  * fp64 cdf for every sample.  Bit-identical either way.
- * DPT_TUNE_POLICY_WAVE = 1 (default): dpt_rollout_policy runs one 64-lane
+ * DPT_TUNE_POLICY_WAVE = 1 (the only value): dpt_rollout_policy runs one 64-lane
  * workgroup per task with the task's context in LDS (the per-arm pairwise sums
- * split over lanes in numpy's order); 0: one lane per task (the lane kernel, also
- * taken when a context does not fit in LDS).  Bit-identical either way.  */
+ * split over lanes in numpy's order); 0 returns DPT_EUNSUPPORTED since round 6
+ * (the lane-per-task kernel was retired).  */
 #define DPT_TUNE_DECODE_TILE 1
 #define DPT_TUNE_PREFILL 2
 #define DPT_TUNE_DARKROOM_MEMO 3
@@ -305,7 +305,7 @@ typedef struct dpt_policy_rollout_args {
     const double* arms;         /* (A, lin_d) or NULL */
     const double* noise;        /* (H, N) or NULL */
     const double* policy_noise; /* see above, or NULL */
-    double* workspace;          /* dpt_policy_workspace_numel(N, A, C + H) doubles */
+    double* workspace;          /* unused since round 6 (may be NULL): dpt_policy_workspace_numel = 0 */
     int32_t* actions_out;       /* (N, H) */
     double* rewards_out;        /* (N, H) */
     double* arm_value_out;      /* (N, H) */

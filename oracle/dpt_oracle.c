@@ -14,6 +14,7 @@
  *
  * Weights use the packed blob layout of include/dpt_hip.h.  OpenMP over tasks.
  */
+#include <immintrin.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -336,9 +337,88 @@ static void linear_d(const double* x, int in, const float* W, const float* b, in
     }
 }
 
-/* causal forward over T packed tokens (T x F), logits of position T-1 (5 actions, double) */
-static void window_forward_d(const view_t* v, const double* toks, int T, double* X, double* K, double* V,
-                             double* sc, double* logits) {
+/* glibc libmvec's AVX2 exp (4 doubles, within 4 ulp; 1.1 ns per value against 6 ns for libm's
+ * scalar exp here): the DarkRoom float64 forward's softmax and gelu_new run through it -- most
+ * of that oracle's time was scalar libm calls.  Its float64 results move by ~1e-16 relative,
+ * far below the 1e-5 logit bar they check (the recorded logits and rollouts stay equal). */
+extern __m256d _ZGVdN4v_exp(__m256d);
+
+static void vexp_d(double* x, int n) {
+    int i = 0;
+    for (; i + 4 <= n; i += 4) _mm256_storeu_pd(x + i, _ZGVdN4v_exp(_mm256_loadu_pd(x + i)));
+    if (i < n) {
+        double t[4] = {0.0, 0.0, 0.0, 0.0};
+        memcpy(t, x + i, sizeof(double) * (size_t)(n - i));
+        _mm256_storeu_pd(t, _ZGVdN4v_exp(_mm256_loadu_pd(t)));
+        memcpy(x + i, t, sizeof(double) * (size_t)(n - i));
+    }
+}
+
+/* gelu_new (activations.py:65) over n values (n a multiple of 4):
+ * 0.5 x (1 + tanh(z)) = x / (1 + exp(-2z)), z = sqrt(2/pi) (x + 0.044715 x^3) */
+static void vgelu_d(double* h, int n) {
+    for (int i = 0; i < n; i += 4) {
+        double t[4];
+        for (int j = 0; j < 4; ++j) {
+            const double x = h[i + j];
+            t[j] = -2.0 * 0.7978845608028654 * (x + 0.044715 * x * x * x);
+        }
+        _mm256_storeu_pd(t, _ZGVdN4v_exp(_mm256_loadu_pd(t)));
+        for (int j = 0; j < 4; ++j) h[i + j] = h[i + j] / (1.0 + t[j]);
+    }
+}
+
+/* linear_d over 4 rows at once (x: [4][in], y: [4][out], out a multiple of 8): each output
+ * keeps linear_d's order (bias, then += x[k]*w[k][o] for k ascending; separate multiply and
+ * add, as -ffp-contract=off compiles linear_d), so the values are identical.  A 4-row x
+ * 8-column block of y stays in registers over the whole k loop. */
+static void linear_d4(const double* x, int in, const float* W, const float* b, int out, double* y) {
+    for (int o0 = 0; o0 < out; o0 += 8) {
+        const __m256d b0 = _mm256_cvtps_pd(_mm_loadu_ps(b + o0)), b1 = _mm256_cvtps_pd(_mm_loadu_ps(b + o0 + 4));
+        __m256d a00 = b0, a01 = b1, a10 = b0, a11 = b1, a20 = b0, a21 = b1, a30 = b0, a31 = b1;
+        for (int k = 0; k < in; ++k) {
+            const float* w = W + (size_t)k * out + o0;
+            const __m256d w0 = _mm256_cvtps_pd(_mm_loadu_ps(w)), w1 = _mm256_cvtps_pd(_mm_loadu_ps(w + 4));
+            const __m256d x0 = _mm256_set1_pd(x[k]), x1 = _mm256_set1_pd(x[in + k]);
+            const __m256d x2 = _mm256_set1_pd(x[2 * in + k]), x3 = _mm256_set1_pd(x[3 * in + k]);
+            a00 = _mm256_add_pd(a00, _mm256_mul_pd(x0, w0));
+            a01 = _mm256_add_pd(a01, _mm256_mul_pd(x0, w1));
+            a10 = _mm256_add_pd(a10, _mm256_mul_pd(x1, w0));
+            a11 = _mm256_add_pd(a11, _mm256_mul_pd(x1, w1));
+            a20 = _mm256_add_pd(a20, _mm256_mul_pd(x2, w0));
+            a21 = _mm256_add_pd(a21, _mm256_mul_pd(x2, w1));
+            a30 = _mm256_add_pd(a30, _mm256_mul_pd(x3, w0));
+            a31 = _mm256_add_pd(a31, _mm256_mul_pd(x3, w1));
+        }
+        _mm256_storeu_pd(y + o0, a00);
+        _mm256_storeu_pd(y + o0 + 4, a01);
+        _mm256_storeu_pd(y + out + o0, a10);
+        _mm256_storeu_pd(y + out + o0 + 4, a11);
+        _mm256_storeu_pd(y + 2 * out + o0, a20);
+        _mm256_storeu_pd(y + 2 * out + o0 + 4, a21);
+        _mm256_storeu_pd(y + 3 * out + o0, a30);
+        _mm256_storeu_pd(y + 3 * out + o0 + 4, a31);
+    }
+}
+
+/* rows [p0, p1) of y = linear(x): blocks of 4 through linear_d4, the rest one by one */
+static void linear_rows_d(const double* x, int in, const float* W, const float* b, int out, double* y, int p0,
+                          int p1) {
+    int p = p0;
+    for (; p + 4 <= p1; p += 4) linear_d4(x + (size_t)p * in, in, W, b, out, y + (size_t)p * out);
+    for (; p < p1; ++p) linear_d(x + (size_t)p * in, in, W, b, out, y + (size_t)p * out);
+}
+
+/* causal forward over T packed tokens (T x F), logits of position T-1 (5 actions, double).
+ * Buffers (Tmax = the caller's capacity, a multiple of 16): X, O [Tmax][E]; KT [E][Tmax] (keys
+ * transposed, zero-filled: a query's scores over its keys are vector loops over the features,
+ * each score summed over the features in order); V, Q [Tmax][E]; H [Tmax][FF]; sc [Tmax].  Every value is computed by the
+ * same operations in the same order as the token-at-a-time form (per token: ln_1, c_attn,
+ * causal softmax attention, c_proj, residual, ln_2, c_fc, gelu_new, mlp.c_proj, residual); the
+ * per-token steps of a layer are independent once its keys and values exist, so they run
+ * phase by phase over the tokens. */
+static void window_forward_d(const view_t* v, const double* toks, int T, int Tmax, double* X, double* KT,
+                             double* V, double* Q, double* O, double* H, double* sc, double* logits) {
     const int F = v->F;
     for (int p = 0; p < T; ++p) {
         double* x = X + (size_t)p * E;
@@ -350,46 +430,70 @@ static void window_forward_d(const view_t* v, const double* toks, int T, double*
         }
         for (int o = 0; o < E; ++o) x[o] += v->wpe[(size_t)p * E + o];
     }
-    double xn[E], qkv[3 * E], o[E], t[E], h[FF];
+    double xn[E];
+    const double rs = sqrt((double)E);
     for (int l = 0; l < v->L; ++l) {
         const float* W = v->layers + (size_t)l * LSIZE;
-        const int last = (l == v->L - 1);
-        double* Q = sc + (size_t)T;  /* queries [T][E] after the score row */
+        /* the last block: only position T-1 reaches the head */
+        const int p0 = (l == v->L - 1) ? T - 1 : 0;
+        /* ln_1 -> c_attn, 4 tokens at a time (O holds ln_1's output, H the qkv rows) */
+        for (int p = 0; p < T; ++p) layer_norm_d(X + (size_t)p * E, W + 0, W + 32, O + (size_t)p * E);
+        linear_rows_d(O, E, W + 64, W + 3136, 3 * E, H, 0, T);
         for (int p = 0; p < T; ++p) {
-            layer_norm_d(X + (size_t)p * E, W + 0, W + 32, xn);
-            linear_d(xn, E, W + 64, W + 3136, 3 * E, qkv);
+            const double* qkv = H + (size_t)p * 3 * E;
             memcpy(Q + (size_t)p * E, qkv, E * sizeof(double));
-            memcpy(K + (size_t)p * E, qkv + E, E * sizeof(double));
+            for (int k = 0; k < E; ++k) KT[(size_t)k * Tmax + p] = qkv[E + k];
             memcpy(V + (size_t)p * E, qkv + 2 * E, E * sizeof(double));
         }
-        /* the last block: only position T-1 reaches the head */
-        for (int p = last ? T - 1 : 0; p < T; ++p) {
-            double* x = X + (size_t)p * E;
+        for (int p = p0; p < T; ++p) {
             const double* q = Q + (size_t)p * E;
+            double* o = O + (size_t)p * E;
             double m = -INFINITY, s = 0.0;
+            /* 16 scores at a time, each summed over the features in order from 0.0 (KT's rows
+             * are padded to a multiple of 16; scores past p are never read) */
+            for (int j0 = 0; j0 <= p; j0 += 16) {
+                __m256d s0 = _mm256_setzero_pd(), s1 = s0, s2 = s0, s3 = s0;
+                for (int k = 0; k < E; ++k) {
+                    const __m256d qk = _mm256_set1_pd(q[k]);
+                    const double* kt = KT + (size_t)k * Tmax + j0;
+                    s0 = _mm256_add_pd(s0, _mm256_mul_pd(qk, _mm256_loadu_pd(kt)));
+                    s1 = _mm256_add_pd(s1, _mm256_mul_pd(qk, _mm256_loadu_pd(kt + 4)));
+                    s2 = _mm256_add_pd(s2, _mm256_mul_pd(qk, _mm256_loadu_pd(kt + 8)));
+                    s3 = _mm256_add_pd(s3, _mm256_mul_pd(qk, _mm256_loadu_pd(kt + 12)));
+                }
+                _mm256_storeu_pd(sc + j0, s0);
+                _mm256_storeu_pd(sc + j0 + 4, s1);
+                _mm256_storeu_pd(sc + j0 + 8, s2);
+                _mm256_storeu_pd(sc + j0 + 12, s3);
+            }
             for (int j = 0; j <= p; ++j) {
-                double d = 0.0;
-                for (int k = 0; k < E; ++k) d += q[k] * K[(size_t)j * E + k];
-                sc[j] = d / sqrt((double)E);
+                sc[j] = sc[j] / rs;
                 if (sc[j] > m) m = sc[j];
             }
+            for (int j = 0; j <= p; ++j) sc[j] = sc[j] - m;
+            vexp_d(sc, p + 1);
+            for (int j = 0; j <= p; ++j) s += sc[j];
+            /* o = sum_j (sc[j] / s) v_j in j order, the 32 features in 8 registers */
+            __m256d o8[E / 4];
+            for (int i = 0; i < E / 4; ++i) o8[i] = _mm256_setzero_pd();
             for (int j = 0; j <= p; ++j) {
-                sc[j] = exp(sc[j] - m);
-                s += sc[j];
+                const __m256d pj = _mm256_set1_pd(sc[j] / s);
+                const double* vj = V + (size_t)j * E;
+                for (int i = 0; i < E / 4; ++i) o8[i] = _mm256_add_pd(o8[i], _mm256_mul_pd(pj, _mm256_loadu_pd(vj + 4 * i)));
             }
-            for (int k = 0; k < E; ++k) o[k] = 0.0;
-            for (int j = 0; j <= p; ++j) {
-                const double pj = sc[j] / s;
-                for (int k = 0; k < E; ++k) o[k] += pj * V[(size_t)j * E + k];
-            }
-            linear_d(o, E, W + 3232, W + 4256, E, t);
-            for (int j = 0; j < E; ++j) x[j] += t[j];
-            layer_norm_d(x, W + 4288, W + 4320, xn);
-            linear_d(xn, E, W + 4352, W + 8448, FF, h);
-            for (int j = 0; j < FF; ++j) h[j] = 0.5 * h[j] * (1.0 + tanh(0.7978845608028654 * (h[j] + 0.044715 * h[j] * h[j] * h[j])));
-            linear_d(h, FF, W + 8576, W + 12672, E, t);
-            for (int j = 0; j < E; ++j) x[j] += t[j];
+            for (int i = 0; i < E / 4; ++i) _mm256_storeu_pd(o + 4 * i, o8[i]);
         }
+        /* c_proj + residual (Q reused for c_proj's output) */
+        linear_rows_d(O, E, W + 3232, W + 4256, E, Q, p0, T);
+        for (int p = p0; p < T; ++p)
+            for (int j = 0; j < E; ++j) X[(size_t)p * E + j] += Q[(size_t)p * E + j];
+        /* ln_2 -> c_fc -> gelu_new -> mlp.c_proj + residual */
+        for (int p = p0; p < T; ++p) layer_norm_d(X + (size_t)p * E, W + 4288, W + 4320, O + (size_t)p * E);
+        linear_rows_d(O, E, W + 4352, W + 8448, FF, H, p0, T);
+        vgelu_d(H + (size_t)p0 * FF, (T - p0) * FF);
+        linear_rows_d(H, FF, W + 8576, W + 12672, E, Q, p0, T);
+        for (int p = p0; p < T; ++p)
+            for (int j = 0; j < E; ++j) X[(size_t)p * E + j] += Q[(size_t)p * E + j];
     }
     layer_norm_d(X + (size_t)(T - 1) * E, v->lnf_g, v->lnf_b, xn);
     linear_d(xn, E, v->head_w, v->head_b, v->A, logits);
@@ -438,6 +542,7 @@ int dpt_oracle_darkroom_rollout(const float* blob, int L, int npos, const int32_
                                 double* margin_out) {
     const int Tmax = 1 + R * horizon, F = 10, steps = Heps * horizon;
     if (Tmax > npos || dim * dim > 4096) return -1;
+    const int Tpad = (Tmax + 15) & ~15; /* window_forward_d's buffer capacity */
     view_t v = make_view(blob, L, 2, 5, npos);
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
@@ -445,10 +550,13 @@ int dpt_oracle_darkroom_rollout(const float* blob, int L, int npos, const int32_
     for (int i = 0; i < N; ++i) {
         double* toks = (double*)calloc((size_t)Tmax * F, sizeof(double));
         double* hist = (double*)calloc((size_t)(R + 1) * horizon * F, sizeof(double)); /* ring of episodes */
-        double* X = (double*)malloc(sizeof(double) * (size_t)Tmax * E);
-        double* K = (double*)malloc(sizeof(double) * (size_t)Tmax * E);
-        double* V = (double*)malloc(sizeof(double) * (size_t)Tmax * E);
-        double* sc = (double*)malloc(sizeof(double) * (size_t)Tmax * (E + 1));
+        double* X = (double*)malloc(sizeof(double) * (size_t)Tpad * E);
+        double* K = (double*)calloc((size_t)Tpad * E, sizeof(double));
+        double* V = (double*)malloc(sizeof(double) * (size_t)Tpad * E);
+        double* Q = (double*)malloc(sizeof(double) * (size_t)Tpad * E);
+        double* Ob = (double*)malloc(sizeof(double) * (size_t)Tpad * E);
+        double* Hb = (double*)malloc(sizeof(double) * (size_t)Tpad * FF);
+        double* sc = (double*)malloc(sizeof(double) * (size_t)Tpad);
         float* memo_lg = (float*)malloc(sizeof(float) * (size_t)dim * dim * 5);
         char* seen = (char*)malloc((size_t)dim * dim);
         const int32_t* perm = perms ? perms + (size_t)i * 5 : NULL;
@@ -470,7 +578,7 @@ int dpt_oracle_darkroom_rollout(const float* blob, int L, int npos, const int32_
                     memset(toks, 0, sizeof(double) * F);
                     toks[0] = x;
                     toks[1] = y;
-                    window_forward_d(&v, toks, T, X, K, V, sc, lgd);
+                    window_forward_d(&v, toks, T, Tpad, X, K, V, Q, Ob, Hb, sc, lgd);
                     for (int a = 0; a < 5; ++a) lg[a] = (float)lgd[a];
                     memcpy(memo_lg + (size_t)cell * 5, lg, sizeof lg);
                     seen[cell] = 1;
@@ -500,7 +608,8 @@ int dpt_oracle_darkroom_rollout(const float* blob, int L, int npos, const int32_
                 memmove(hist, hist + (size_t)horizon * F, sizeof(double) * (size_t)R * horizon * F);
             }
         }
-        free(toks); free(hist); free(X); free(K); free(V); free(sc); free(memo_lg); free(seen);
+        free(toks); free(hist); free(X); free(K); free(V); free(Q); free(Ob); free(Hb); free(sc); free(memo_lg);
+        free(seen);
     }
     return 0;
 }

@@ -447,16 +447,25 @@ def policy_action(policy, acts_ctx, rews_ctx, A, online=True, c=1.0, ts=None, ts
     return i
 
 
-def bandit_policy_rollout(policy, means, H, var, g, **kw):
+def bandit_policy_rollout(policy, means, H, var, g, ctx_actions=None, ctx_rewards=None, bernoulli=False, **kw):
     """evals/eval_bandit.py:56-103 with a classical controller; draws injected.
+    g (H, N): reward normals, or uniforms with bernoulli=True (BanditEnv.transit's Binomial(1, mean),
+    envs/bandit_env.py:56-64, as u < mean).  ctx_actions / ctx_rewards (N, C): a prefix context the
+    controller sees before the first step (set_batch_numpy_vec, evals/eval_bandit.py:214-301).
     kw: online, c, ts (dict std/prior_mean/prior_var), ts_g (H, N, A), arms, first_u_idx."""
     means = np.asarray(means, np.float64)
     N, A = means.shape
-    acts = np.zeros((N, H), np.int64)
-    rews = np.zeros((N, H))
+    C = 0 if ctx_actions is None else np.asarray(ctx_actions).shape[1]
+    acts = np.zeros((N, C + H), np.int64)
+    rews = np.zeros((N, C + H))
+    if C:
+        acts[:, :C] = ctx_actions
+        rews[:, :C] = ctx_rewards
     ts_g = kw.pop("ts_g", None)
     for h in range(H):
-        a = policy_action(policy, acts[:, :h], rews[:, :h], A, ts_g=None if ts_g is None else ts_g[h], **kw)
-        acts[:, h] = a
-        rews[:, h] = bandit_reward(means, a, g[h], var)
+        n = C + h
+        a = policy_action(policy, acts[:, :n], rews[:, :n], A, ts_g=None if ts_g is None else ts_g[h], **kw)
+        acts[:, n] = a
+        rews[:, n] = bernoulli_reward(means, a, g[h]) if bernoulli else bandit_reward(means, a, g[h], var)
+    acts, rews = acts[:, C:], rews[:, C:]
     return dict(actions=acts, rewards=rews, cum_means=np.stack([arm_value(means, acts[:, h]) for h in range(H)]))

@@ -1,8 +1,8 @@
 """Classical baseline rollouts (dpt_rollout_policy: evals/eval_bandit.py's Emp / UCB / Thompson /
 LCB / LinUCB controllers, ctrls/ctrl_bandit.py) at the bench shapes: 5-arm bandit H = 500 and the
 20-arm linear bandit H = 1000 (d = 2), 4096 tasks.  HIP events around each launch, best of 3.
-Prints one JSON line of ms per launch and env-steps/s per kernel (POL_KERNELS=wave,lane: the
-wave-per-task kernel and the lane-per-task one)."""
+Prints one JSON line of ms per launch and env-steps/s (the wave-per-task kernel; the round-4
+lane-per-task kernel was retired in round 6, its timings are in profiles/r5a/policy_timing.jsonl)."""
 import json
 import os
 import sys
@@ -23,9 +23,7 @@ theta = rs.normal(0, 1, (N, 2)) / np.sqrt(2)
 cases.append(("linear20_H1000", 20, 1000, arms, theta @ arms.T))
 pols = {"emp": dpt_hip.POLICY_EMP, "ucb": dpt_hip.POLICY_UCB, "thompson": dpt_hip.POLICY_THOMPSON,
         "lcb": dpt_hip.POLICY_LCB, "linucb": dpt_hip.POLICY_LINUCB}
-kernels = [k for k in os.environ.get("POL_KERNELS", "wave,lane").split(",") if k]
-for kern in kernels:
-    dpt_hip.set_policy_wave(kern == "wave")
+for kern in ("wave",):
     for name, A, H, arm_feats, means in cases:
         for pn, pol in pols.items():
             if pn == "linucb" and arm_feats is None:
@@ -42,5 +40,4 @@ for kern in kernels:
                     best = min(best or 1e30, a.elapsed_time(e))
             res[f"{kern}/{name}/{pn}"] = {"ms": best, "env_steps_per_s": N * H / (best * 1e-3)}
             print(json.dumps({f"{kern}/{name}/{pn}": res[f"{kern}/{name}/{pn}"]}), flush=True)
-dpt_hip.set_policy_wave(True)
 print(json.dumps(res))

@@ -608,37 +608,66 @@ def test_training_mode_no_grad_test_loss_loop():
     assert all(gr is not None and gr.device.type == "cpu" and torch.isfinite(gr).all() for gr in grads)
 
 
-@pytest.mark.parametrize("A,H,C,d", [(5, 500, 0, 0), (20, 300, 0, 2), (7, 40, 150, 4), (3, 30, 0, 3)])
-def test_policy_wave_kernel_equals_lane_kernel(A, H, C, d):
-    """dpt_rollout_policy's wave-per-task kernel (context in LDS, per-arm pairwise sums split over
-    lanes) against the lane-per-task kernel on the same Philox draws: actions, rewards and arm
-    values bit-identical for every policy (Thompson sampled and 100-draw vote, Bernoulli rewards,
-    a prefix context, LinUCB at lin_d 2, 3 and 4)."""
+@pytest.mark.parametrize("A,H,C", [(5, 500, 0), (20, 300, 0), (7, 40, 150), (3, 30, 0)])
+def test_policy_wave_kernel_vs_oracle(A, H, C):
+    """dpt_rollout_policy (one 64-lane workgroup per task, context in LDS, per-arm pairwise sums split
+    over lanes) against the float64 numpy oracle's classical controllers (oracle/dpt_oracle.py
+    policy_action: ctrls/ctrl_bandit.py:22-380) on the same injected draws, at the shapes the retired
+    lane-per-task kernel was compared at: Opt, Emp (online and offline), UCB, LCB and Thompson
+    (sampled posterior), Gaussian and -- for UCB -- Bernoulli rewards, with and without a prefix
+    context.  Actions, rewards and arm values bit-identical.  LinUCB and the Thompson 100-draw vote
+    are pinned by the reference's own recorded runs (test_linucb_kernel_and_drop_in at lin_d 2..8,
+    test_linear_offline_and_graph_match_reference): numpy's BLAS on this host may round LinUCB
+    differently from the host those were recorded on (LinUCB orders)."""
     import dpt_hip
+    from oracle import dpt_oracle as O
     rs = np.random.RandomState(A * 1000 + H + C)
-    N = 300
-    arms = rs.normal(size=(A, max(d, 1))) / np.sqrt(max(d, 1))
-    means = rs.uniform(0, 1, (N, A)) if not d else rs.normal(0, 1, (N, arms.shape[1])) @ arms.T
-    ctx = {}
+    N = 48
+    means = rs.uniform(0, 1, (N, A))
+    ctx, octx = {}, {}
     if C:
-        ctx = dict(ctx_actions=rs.randint(0, A, (N, C)).astype(np.int32), ctx_rewards=rs.normal(0.5, 0.5, (N, C)))
-    cases = [(dpt_hip.POLICY_OPT, {}), (dpt_hip.POLICY_EMP, dict(online=True)), (dpt_hip.POLICY_EMP, dict(online=False)),
-             (dpt_hip.POLICY_UCB, dict(c=1.0)), (dpt_hip.POLICY_LCB, dict(c=0.8)),
-             (dpt_hip.POLICY_THOMPSON, dict(ts_std=0.3)), (dpt_hip.POLICY_THOMPSON, dict(ts_std=0.3, sample=False))]
-    if d:
-        cases.append((dpt_hip.POLICY_LINUCB, dict(c=1.0, arms=arms)))
-    for pol, kw in cases:
-        for bt in ((dpt_hip.BANDIT_GAUSSIAN, dpt_hip.BANDIT_BERNOULLI) if pol == dpt_hip.POLICY_UCB
-                   else (dpt_hip.BANDIT_GAUSSIAN,)):
-            m = np.clip(means, 0, 1) if bt == dpt_hip.BANDIT_BERNOULLI else means
-            hh = 3 if kw.get("sample") is False else H  # the vote draws 100 x A normals per step
-            outs = []
-            try:
-                for wave in (True, False):
-                    dpt_hip.set_policy_wave(wave)
-                    o = dpt_hip.rollout_policy(pol, m, hh, 0.3, bandit_type=bt, seed=99, first_task=5, **ctx, **kw)
-                    outs.append({k: o[k].cpu().numpy() for k in ("actions", "rewards", "arm_value")})
-            finally:
-                dpt_hip.set_policy_wave(True)
-            for k in ("actions", "rewards", "arm_value"):
-                assert np.array_equal(outs[0][k], outs[1][k]), (pol, kw, bt, k)
+        ca, cr = rs.randint(0, A, (N, C)).astype(np.int32), rs.normal(0.5, 0.5, (N, C))
+        ctx = dict(ctx_actions=ca, ctx_rewards=cr)
+        octx = dict(ctx_actions=ca.astype(np.int64), ctx_rewards=cr)
+    ts = dict(std=0.3, prior_mean=0.5, prior_var=1 / 12.0)
+    cases = [("opt", dpt_hip.POLICY_OPT, {}, {}),
+             ("emp", dpt_hip.POLICY_EMP, dict(online=True), dict(online=True)),
+             ("emp", dpt_hip.POLICY_EMP, dict(online=False), dict(online=False)),
+             ("ucb", dpt_hip.POLICY_UCB, dict(c=1.0), dict(c=1.0)),
+             ("lcb", dpt_hip.POLICY_LCB, dict(c=0.8), dict(c=0.8)),
+             ("thompson", dpt_hip.POLICY_THOMPSON, dict(ts_std=0.3, ts_prior_mean=0.5, ts_prior_var=1 / 12.0),
+              dict(ts=ts))]
+    for name, pol, kw, okw in cases:
+        for bern in ((False, True) if name == "ucb" else (False,)):
+            g = rs.uniform(size=(H, N)) if bern else rs.normal(size=(H, N))
+            pn = rs.normal(size=(H, N, A)) if name == "thompson" else None
+            bt = dpt_hip.BANDIT_BERNOULLI if bern else dpt_hip.BANDIT_GAUSSIAN
+            o = dpt_hip.rollout_policy(pol, means, H, 0.3, bandit_type=bt, noise=g, policy_noise=pn, **ctx, **kw)
+            got = {k: o[k].cpu().numpy() for k in ("actions", "rewards", "arm_value")}
+            if name == "opt":  # OptPolicy: the optimal arm every step (ctrl_bandit.py:22-38)
+                acts = np.repeat(means.argmax(1)[:, None], H, 1)
+                rew = np.stack([(O.bernoulli_reward(means, acts[:, h], g[h]) if bern
+                                 else O.bandit_reward(means, acts[:, h], g[h], 0.3)) for h in range(H)], 1)
+                ref = dict(actions=acts, rewards=rew, cum_means=np.stack([O.arm_value(means, acts[:, h])
+                                                                          for h in range(H)]))
+            else:
+                ref = O.bandit_policy_rollout(name, means, H, 0.3, g, bernoulli=bern, ts_g=pn, **octx, **okw)
+            assert np.array_equal(got["actions"], ref["actions"]), (name, kw, bern)
+            assert np.array_equal(got["rewards"], ref["rewards"]), (name, kw, bern)
+            assert np.array_equal(got["arm_value"].T, ref["cum_means"]), (name, kw, bern)
+
+
+def test_policy_lane_kernel_retired():
+    """DPT_TUNE_POLICY_WAVE accepts only the wave kernel since round 6; dpt_policy_workspace_numel is
+    0 (the contexts live in LDS) and a null workspace is accepted."""
+    import ctypes
+    import dpt_hip
+    from dpt_hip import _lib
+    with pytest.raises(NotImplementedError):
+        _lib.call("dpt_tuning_set", _lib.TUNE_POLICY_WAVE, 0)
+    _lib.call("dpt_tuning_set", _lib.TUNE_POLICY_WAVE, 1)
+    n = ctypes.c_int64(-1)
+    _lib.call("dpt_policy_workspace_numel", 4096, 20, 1000, ctypes.byref(n))
+    assert n.value == 0
+    o = dpt_hip.rollout_policy(dpt_hip.POLICY_UCB, np.random.RandomState(0).uniform(0, 1, (8, 5)), 20, 0.3)
+    assert o["actions"].shape == (8, 20)

@@ -506,6 +506,22 @@ def first_tie(margin, bar=1e-5):
     return int(tie[0]) if tie.size else len(margin)
 
 
+def compared_steps(acts, ref_acts, margin, bar=1e-5):
+    """Per task, the number of leading steps whose trajectory equals the oracle's: the first step
+    whose action differs, or all steps.  A differing action is legitimate only at a near-tie draw (a
+    uniform within ``bar`` of one of the oracle's cdf edges, where fp32 rounding of the logits may
+    decide); anywhere else it fails.  Steps up to and including that one were computed on identical
+    windows, so their logits are comparable.  acts, ref_acts: (tasks, steps); margin: (steps, tasks)."""
+    steps = acts.shape[1]
+    diff = acts != ref_acts
+    n = np.where(diff.any(1), diff.argmax(1), steps)
+    j = np.nonzero(n < steps)[0]
+    flip_margin = margin[n[j], j]
+    assert (flip_margin < bar).all(), ("action differs away from a near-tie", j[flip_margin >= bar][:8],
+                                       n[j][flip_margin >= bar][:8], flip_margin[flip_margin >= bar][:8])
+    return n
+
+
 @pytest.mark.parametrize("A,H,var,N", [(5, 500, 0.3, 4096), (20, 1000, 0.3, 4096), (5, 500, 0.3, 4093)])
 def test_rollout_full_config_all_tasks(A, H, var, N):
     """BASELINE configs 2 (5 arms, H=500) and 4 (20 arms, H=1000; one GPU's 4096-task shard) at full
@@ -513,9 +529,10 @@ def test_rollout_full_config_all_tasks(A, H, var, N):
     with the float64 C oracle (pinned to the reference's rollouts by
     test_c_bandit_oracle_matches_reference; K/V-cache form, bit-identical to its re-forward form)
     fed the same Philox draws -- logits within 1e-5 at every compared step and actions / arm values
-    exactly, each task up to its first near-tie draw (a uniform within 1e-5 of a cdf edge, where
-    numpy's own expf decides).  The fraction of tasks compared over the whole horizon is printed
-    (reference: eval_bandit.py:56-103 / ctrl_bandit.py:422-444)."""
+    exactly, each task up to its first differing action, which must fall on a near-tie draw (a
+    uniform within 1e-5 of a cdf edge, where numpy's own expf decides).  The fraction of task-steps
+    compared is printed and must be >= 0.9 (reference: eval_bandit.py:56-103 /
+    ctrl_bandit.py:422-444)."""
     import bench
     import dpt_hip
     from oracle import c_oracle
@@ -541,41 +558,41 @@ def test_rollout_full_config_all_tasks(A, H, var, N):
     blob = dpt_hip.pack_weights(sd, L).numpy()
     ref = c_oracle.bandit_rollout_f64(blob, L, A, 4 * (1 + H), means, H, var, u, g, True, False,
                                       bench.host_cpus()[0], want_logits=True)
-    margin = ref["margin"]  # (H, N)
-    tie = margin < 1e-5
-    n_cmp = np.where(tie.any(0), tie.argmax(0), H)  # steps 0..n-1 agree exactly; a near-tie may flip step n
+    n_cmp = compared_steps(acts, ref["actions"], ref["margin"])  # a differing action only at a near-tie
     step = np.arange(H)[:, None]
-    # logits: every step up to and including each task's first near-tie
+    # logits: every step up to and including each task's first differing action
     sel = step <= np.minimum(n_cmp, H - 1)[None, :]
     got, want = lg[sel], ref["logits"][sel]
     bad = np.abs(got - want) > 1e-5 * np.maximum(1, np.abs(want))
     assert not bad.any(), (int(bad.sum()), float(np.abs(got - want).max()))
     okmask = (step < n_cmp[None, :]).T  # (N, H)
-    assert np.array_equal(acts[okmask], ref["actions"][okmask])
     assert np.array_equal(av[okmask], ref["arm_value"][okmask])
     full = float((n_cmp == H).mean())
-    print(f"\nA={A} H={H} N={N}: {full:.4f} of tasks compared over all {H} steps, "
+    print(f"\nA={A} H={H} N={N}: {full:.4f} of tasks identical over all {H} steps, "
           f"{okmask.mean():.5f} of all task-steps compared exactly")
-    # near-ties are rare (a uniform within 1e-5 of one of the A - 1 interior edges: ~2e-5 (A - 1) per
-    # step), so most task-steps are compared: ~0.97 at 5 arms x 500 steps, ~0.84 at 20 arms x 1000
-    assert okmask.mean() >= 0.75
+    assert okmask.mean() >= 0.9
 
 
-def check_darkroom_tasks(out, tasks, ref, Heps, horizon):
-    """Device rollout rows ``tasks`` against the C oracle's rows (same order): logits within 1e-5,
-    actions exactly and per-episode returns exactly, each task up to its first near-tie draw."""
+def check_darkroom_tasks(out, tasks, ref, Heps, horizon, min_frac=0.9, label=""):
+    """Device rollout rows ``tasks`` against the C oracle's rows (same order), every task: actions
+    exactly up to the first step whose action differs (which must be a near-tie draw,
+    compared_steps), logits within 1e-5 at every step up to and including it, and the returns of
+    every episode that ends before it.  The fraction of task-steps compared is printed and must be
+    >= ``min_frac``; returns it."""
     steps = Heps * horizon
     lg = out["logits"].cpu().numpy()[:, tasks]
     acts = out["actions"].cpu().numpy()[tasks]
     rets = out["returns"].cpu().numpy()[tasks]
-    full = 0
+    n = compared_steps(acts, ref["actions"], ref["margin"])
     for j in range(len(tasks)):
-        n = first_tie(ref["margin"][:, j])
-        full += n == steps
-        assert_logits(lg[:min(n + 1, steps), j], ref["logits"][:min(n + 1, steps), j])
-        assert np.array_equal(acts[j, :n], ref["actions"][j, :n]), tasks[j]
-        assert np.array_equal(rets[j, :n // horizon], ref["returns"][j, :n // horizon]), tasks[j]
-    return full
+        k = min(n[j] + 1, steps)
+        assert_logits(lg[:k, j], ref["logits"][:k, j])
+        assert np.array_equal(rets[j, :n[j] // horizon], ref["returns"][j, :n[j] // horizon]), tasks[j]
+    frac = float(n.sum()) / (len(tasks) * steps)
+    print(f"\n{label}: {len(tasks)} tasks, {(n == steps).mean():.4f} of them identical over all {steps} steps, "
+          f"{frac:.5f} of task-steps compared exactly")
+    assert frac >= min_frac, frac
+    return frac
 
 
 def darkroom_config(N_total, seed=0):
@@ -588,9 +605,10 @@ def darkroom_config(N_total, seed=0):
 
 def test_rollout_darkroom_full_config3_sampled_tasks():
     """BASELINE config 3 at full size (4096 tasks, Heps=40, horizon=100, goals in collect_data.py's
-    shuffled order, logits memo on): 256+ sampled tasks agree with the float64 C oracle fed the same
-    Philox draws -- logits within 1e-5, actions and per-episode returns exactly, each task up to
-    its first near-tie draw."""
+    shuffled order, logits memo on): 1024+ tasks (the first and last 16 and 1024 random ones) agree
+    with the float64 C oracle fed the same Philox draws -- logits within 1e-5, actions and
+    per-episode returns exactly, each task up to a flip at a near-tie draw; >= 0.9 of the task-steps
+    compared (reference: evals/eval_darkroom.py:53-82)."""
     import bench
     import dpt_hip
     from oracle import c_oracle
@@ -600,23 +618,22 @@ def test_rollout_darkroom_full_config3_sampled_tasks():
     m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + horizon))
     goals = darkroom_config(N)
     out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, counter=ctr, want_actions=True, want_logits=True)
-    tasks = sampled_tasks(N, tile=1, n_random=256)
+    rs = np.random.RandomState(0)
+    tasks = np.unique(np.concatenate([np.arange(16), np.arange(N - 16, N), rs.choice(N, 1024, replace=False)]))
     steps = Heps * horizon
     u = np.stack([philox_np.uniform(seed, ctr + k, tasks, d.STREAM_SELECT) for k in range(steps)])
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + horizon), goals[tasks], Heps,
                                     horizon, 1, u, True, threads=bench.host_cpus()[0], want_logits=True)
-    assert len(tasks) >= 256
-    full = check_darkroom_tasks(out, tasks, ref, Heps, horizon)
-    print(f"\nC3: {full} of {len(tasks)} sampled tasks compared over all {steps} steps")
-    assert full >= len(tasks) // 2
+    assert len(tasks) >= 1024
+    check_darkroom_tasks(out, tasks, ref, Heps, horizon, label="C3")
 
 
 @pytest.mark.parametrize("first_task", [0, 57344])
 def test_rollout_darkroom_config5_shard(first_task):
     """BASELINE config 5 (DarkRoom, 65,536 tasks over 8 GPUs): one GPU's 8,192-task shard, the first
     and the last rank's, as bench.py runs it (goals of the global ids, Philox keyed by the global
-    task id, C3 weights, 40 episodes, memo on): 64 sampled tasks of both halves of the shard agree
-    with the float64 C oracle fed the same draws."""
+    task id, C3 weights, 40 episodes, memo on): 256+ tasks over both halves of the shard agree
+    with the float64 C oracle fed the same draws; >= 0.9 of the task-steps compared."""
     import bench
     import dpt_hip
     from oracle import c_oracle
@@ -628,14 +645,14 @@ def test_rollout_darkroom_config5_shard(first_task):
     out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, first_task=first_task, want_actions=True,
                              want_logits=True)
     rs = np.random.RandomState(first_task)
-    tasks = np.unique(np.concatenate([[0, 1, 4095, 4096, 8191], rs.choice(4096, 32, replace=False),
-                                      4096 + rs.choice(4096, 32, replace=False)]))
+    tasks = np.unique(np.concatenate([[0, 1, 4095, 4096, 8191], rs.choice(4096, 128, replace=False),
+                                      4096 + rs.choice(4096, 128, replace=False)]))
     steps = Heps * horizon
     u = np.stack([philox_np.uniform(seed, k, first_task + tasks, d.STREAM_SELECT) for k in range(steps)])
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + horizon), goals[tasks], Heps,
                                     horizon, 1, u, True, threads=bench.host_cpus()[0], want_logits=True)
-    assert len(tasks) >= 64
-    assert check_darkroom_tasks(out, tasks, ref, Heps, horizon) >= len(tasks) // 2
+    assert len(tasks) >= 256
+    check_darkroom_tasks(out, tasks, ref, Heps, horizon, label=f"C5 shard at {first_task}")
 
 
 def test_empty_batches():
@@ -781,7 +798,56 @@ def test_rollout_darkroom_dim12_workspace_without_state_table():
     w = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w/")}
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(w, 4).numpy(), 4, 404, goals[tasks], Heps, horizon, R, u,
                                     True, dim=dim, threads=16, want_logits=True)
-    check_darkroom_tasks(outs[1], tasks, ref, Heps, horizon)
+    check_darkroom_tasks(outs[1], tasks, ref, Heps, horizon, label="dim 12 workspace")
+
+
+_NOWS_REF = {}
+
+
+@pytest.mark.parametrize("memo", [False, True])
+@pytest.mark.parametrize("R", [1, 2])
+@pytest.mark.parametrize("dim", [11, 12])
+def test_rollout_darkroom_workspace_free_vs_oracle(dim, R, memo):
+    """The workspace-free kernels (rollout_darkroom_kernel<false, 4|8, false>, step specialised on
+    the wave's block count) on grids over 10 x 10: dim 11 with the workspace switched off and dim 12,
+    which takes them by default (144 cells exceed the per-state table), at windows 101 (4 waves;
+    episodes of 1, 101, 101 tokens) and 201 (8 waves; 1, 101, 201, 201), memo off and on (dim 12
+    has no memo: more cells than memo rows).  This is where a 3e-3 logit error was once observed
+    (workspace-free kernels).  EVERY task of a 256-task batch agrees with the float64 C
+    oracle fed the same Philox draws: logits within 1e-5, actions and per-episode returns exactly,
+    each task up to a flip at a near-tie draw; >= 0.9 of the task-steps compared (reference:
+    evals/eval_darkroom.py:20-84, ctrls/ctrl_darkroom.py:23-66)."""
+    import bench
+    import dpt_hip
+    from oracle import c_oracle
+    d = dh()
+    L, horizon, N, seed = 4, 100, 256, 4242 + dim
+    Heps = R + 2
+    sd, _ = bench.synthetic_state_dict(L, 2, 5, R * horizon)
+    m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + R * horizon))
+    goals = np.random.RandomState(dim).randint(0, dim, (N, 2))
+    try:
+        dpt_hip.set_darkroom_workspace(False)
+        dpt_hip.set_darkroom_memo(memo)
+        out = m.rollout_darkroom(goals, Heps, horizon, R, dim=dim, seed=seed, want_actions=True, want_logits=True,
+                                 want_forwards=True)
+    finally:
+        dpt_hip.set_darkroom_workspace(True)
+        dpt_hip.set_darkroom_memo(True)
+    fw = out["forwards"].cpu().numpy()
+    if memo and dim * dim <= 128:
+        assert fw.sum() < N * Heps * horizon
+    else:
+        assert (fw == horizon).all()
+    steps = Heps * horizon
+    if (dim, R) not in _NOWS_REF:  # the oracle does not depend on the memo switch
+        tasks = np.arange(N)
+        u = np.stack([philox_np.uniform(seed, k, tasks, d.STREAM_SELECT) for k in range(steps)])
+        _NOWS_REF[dim, R] = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, 4 * (1 + R * horizon),
+                                                      goals, Heps, horizon, R, u, True, dim=dim,
+                                                      threads=bench.host_cpus()[0], want_logits=True)
+    check_darkroom_tasks(out, np.arange(N), _NOWS_REF[dim, R], Heps, horizon,
+                         label=f"workspace-free dim {dim} window {1 + R * horizon} memo {memo}")
 
 
 @pytest.mark.parametrize("Heps,horizon,R,dim", [(4, 100, 3, 10), (2, 511, 1, 10), (2, 300, 1, 12)])
@@ -826,7 +892,7 @@ def test_rollout_darkroom_windows_over_256(Heps, horizon, R, dim):
     ref = c_oracle.darkroom_rollout(dpt_hip.pack_weights(sd, L).numpy(), L, npos, goals[tasks], Heps, horizon, R, u,
                                     True, dim=dim, threads=16, want_logits=True)
     res = {k: torch.from_numpy(on[k]) for k in ("logits", "actions", "returns")}
-    assert check_darkroom_tasks(res, tasks, ref, Heps, horizon) >= len(tasks) // 2
+    check_darkroom_tasks(res, tasks, ref, Heps, horizon, label=f"window {1 + R * horizon}")
 
 
 @pytest.mark.parametrize("Heps,horizon,R", [(4, 100, 2), (3, 85, 3)])
@@ -874,7 +940,7 @@ def test_rollout_darkroom_long_windows(Heps, horizon, R):
     res = {"logits": torch.from_numpy(on["logits"]), "actions": torch.from_numpy(on["actions"]),
            "returns": torch.from_numpy(on["returns"])}
     assert len(tasks) >= 64
-    assert check_darkroom_tasks(res, tasks, ref, Heps, horizon) >= len(tasks) // 2
+    check_darkroom_tasks(res, tasks, ref, Heps, horizon, label=f"window {1 + R * horizon}")
 
 
 def test_rollout_bandit_stream_base_bit31():

@@ -472,8 +472,8 @@ def test_train_dropout_other_widths_vs_oracle(E, T):
 
 def test_train_dropout_through_the_model_forward():
     """Transformer.forward in training mode with dropout > 0 (the reference's --dropout flag):
-    seeds come from torch's generator -- the same manual_seed, the same preds; a second call, new
-    masks -- and eval mode applies none (equal to the p = 0 model's preds)."""
+    seeds come from torch's CUDA generator -- the same manual_seed, the same preds; a second call,
+    new masks -- and eval mode applies none (equal to the p = 0 model's preds)."""
     g = golden("train_grads.npz")
     _, m = model_from_fixture("bandit5")
     batch, _ = batch_from(g, "bandit5")
@@ -492,6 +492,35 @@ def test_train_dropout_through_the_model_forward():
     with torch.no_grad():
         f = m(batch)
     assert torch.equal(e, f)
+
+
+def test_dropout_leaves_the_cpu_stream_alone():
+    """Dropout seeds come from the CUDA generator (models/net.py _dropout_seed), as the reference's
+    dropout masks do, so the CPU stream that drives the DataLoader shuffle (train.py:203,249) and the
+    per-item context permutation (dataset.py:85) is the same with and without dropout: a shuffled
+    DataLoader's batch order over two epochs, with a dropout training forward after every batch,
+    equals the order with dropout 0.  torch.manual_seed reproduces the seeds."""
+    from models import net
+    g = golden("train_grads.npz")
+    _, m = model_from_fixture("bandit5")
+    batch, _ = batch_from(g, "bandit5")
+    m.train()
+    orders = []
+    for p in (0.0, 0.2):
+        m.dropout = p
+        torch.manual_seed(11)
+        dl = torch.utils.data.DataLoader(torch.arange(64), batch_size=8, shuffle=True)
+        order = []
+        for _ in range(2):
+            for idx in dl:
+                order.append(idx.clone())
+                m(batch)
+        orders.append(torch.cat(order))
+    assert torch.equal(orders[0], orders[1])
+    torch.manual_seed(5)
+    s1, s2 = net._dropout_seed(), net._dropout_seed()
+    torch.manual_seed(5)
+    assert net._dropout_seed() == s1 and s1 != s2
 
 
 def _width_model(E, L, H, seed):

@@ -89,9 +89,11 @@ def test_train_blob_order_matches_pack_weights():
 def test_training_mode_dropout_takes_the_training_kernels(monkeypatch):
     """GPT2Config applies dropout in training mode (models/net.py:30-32), with or without grad
     (train.py:265-278's test loss): such calls go to the training kernels (which implement it)
-    with a fresh Philox seed drawn from torch's generator per call; eval mode ignores dropout."""
+    with a fresh Philox seed per call (net._dropout_seed, from the CUDA generator: its
+    seedability and that the CPU stream is untouched are GPU tests); eval mode ignores dropout."""
     import torch
     from dpt_hip import train as tr
+    from models import net
     from models.net import Transformer
     m = Transformer(dict(horizon=4, state_dim=1, action_dim=5, n_layer=2, n_embd=32, n_head=1, dropout=0.1,
                          test=False))
@@ -102,15 +104,15 @@ def test_training_mode_dropout_takes_the_training_kernels(monkeypatch):
         return torch.zeros((tok.shape[0], tok.shape[1], 5))
     monkeypatch.setattr(tr.TransformerFunction, "apply", fake_apply)
     monkeypatch.setattr(m, "_tokens", lambda x: torch.zeros((3, 9, 8)))
-    torch.manual_seed(5)
+    seeds = iter([11, 12, 13])
+    monkeypatch.setattr(net, "_dropout_seed", lambda: next(seeds))
     m(_tiny_batch())
     with torch.no_grad():
         m(_tiny_batch())
-    torch.manual_seed(5)
     m(_tiny_batch())
     assert [d[7] for d in seen] == [0, tr.FORWARD_ONLY, 0]
     assert all(abs(d[8] - 0.1) < 1e-12 for d in seen)
-    assert seen[0][9] != seen[1][9] and seen[0][9] == seen[2][9]   # fresh per call, seedable
+    assert [d[9] for d in seen] == [11, 12, 13]   # one seed per call
     m.eval()
     m.dropout = 0.1
     seen.clear()
