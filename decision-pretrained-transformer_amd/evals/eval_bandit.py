@@ -45,9 +45,10 @@ def _fused_ok(vec_env, controller, horizon):
     """The one-launch rollout: our controller, env and model, with no dropout in play (a
     training-mode model with dropout > 0 takes the per-step loop, whose forward applies it)."""
     from models.net import Transformer
+    if not (isinstance(controller, BanditTransformerController) and isinstance(vec_env, BanditEnvVec)):
+        return False
     m = controller.model
-    return (isinstance(controller, BanditTransformerController) and isinstance(vec_env, BanditEnvVec)
-            and isinstance(m, Transformer) and m.state_dim == 1 and not (m.training and m.dropout > 0)
+    return (isinstance(m, Transformer) and m.state_dim == 1 and not (m.training and m.dropout > 0)
             and controller.batch_size == vec_env.num_envs and horizon <= m.n_positions)
 
 
