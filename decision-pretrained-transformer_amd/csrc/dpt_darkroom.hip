@@ -214,7 +214,7 @@ __device__ inline void ws_load(const float* d, float (&v)[8]) {
 
 // DPT_DR_L0LIN episode prologue: c = Wvp o' + bvp from attend's (o, l) (o / l = o' x 2^attn_ey), at true
 // scale, and x += c (A); the token-0 column (no key in 1..0: l = 0) gets c = 0
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void l0_cproj(const float* W, const FragSrc3& f3, float (&o)[2][8], const float (&l)[2],
                                 float (&x)[2][8], const int (&qb)[2], const ModelView& M) {
     const int lane = lane_id(), g = lane >> 4;
@@ -223,7 +223,7 @@ __device__ inline void l0_cproj(const float* W, const FragSrc3& f3, float (&o)[2
     const floatx4 b0 = ld4(W + PL::proj_b + 4 * g), b1 = ld4(W + PL::proj_b + 16 + 4 * g);  // scaled (PL)
     const float down = exp2i(-(M.attn_ew + M.attn_ey));
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
+    for (int j = J0; j < J0 + NB; ++j) {
         const Split2 os = split2(o[j], l[j] > 0.f ? __builtin_amdgcn_rcpf(l[j]) : 0.f);
         const floatx4 c0 = mfma_x3(w0, os, b0), c1 = mfma_x3(w1, os, b1);
         const bool tok0 = qb[j] == 0 && (lane & 15) == 0;
@@ -514,18 +514,34 @@ __device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
 #define DPT_DR_OPAQUE 1
 #endif
 #define DR_OPQ(v) asm volatile("" : "+s"(v))
+#ifndef DPT_DR_SEQ_BLOCKS
+#define DPT_DR_SEQ_BLOCKS 1
+#endif
 // one phase over the wave's blocks inside the step: specialised on NBC when it is known at compile
 // time (no-op for 0), else dispatched on the run-time count (DPT_BLOCKS)
-#define DR_BLOCKS(...)                        \
-    do {                                      \
-        if constexpr (NBC >= 0) {             \
-            if constexpr (NBC > 0) {          \
-                constexpr int NB = NBC;       \
-                __VA_ARGS__;                  \
-            }                                 \
-        } else {                              \
-            DPT_BLOCKS(nb, __VA_ARGS__);      \
-        }                                     \
+// With kSeqBlocks (the register-starved 8- and 16-wave geometries, 128 VGPRs per wave) a two-block
+// wave runs each phase for one block after the other (NB = 1 at slots J0 = 0 and 1): the same
+// arithmetic per block, so the same results, with one block's products and split operands live at a
+// time instead of two.
+#define DR_BLOCKS(...)                                      \
+    do {                                                    \
+        if constexpr (NBC >= 0) {                           \
+            if constexpr (NBC == 2 && kSeqBlocks) {         \
+                {                                           \
+                    constexpr int NB = 1, J0 = 0;           \
+                    __VA_ARGS__;                            \
+                }                                           \
+                {                                           \
+                    constexpr int NB = 1, J0 = 1;           \
+                    __VA_ARGS__;                            \
+                }                                           \
+            } else if constexpr (NBC > 0) {                 \
+                constexpr int NB = NBC, J0 = 0;             \
+                __VA_ARGS__;                                \
+            }                                               \
+        } else {                                            \
+            DPT_BLOCKS(nb, __VA_ARGS__);                    \
+        }                                                   \
     } while (0)
 
 
@@ -535,6 +551,7 @@ template <bool kWs, int NW, bool kTab = kWs>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? (kWs && DPT_DR_WG3 ? DPT_DR_WG3_N : 2) : (NW == 8 && kWs && DPT_DR_NW8_2 ? 4 : 1))
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     static_assert(kWs || !kTab, "the state table lives in the workspace");
+    constexpr bool kSeqBlocks = DPT_DR_SEQ_BLOCKS && NW >= 8;  // DR_BLOCKS
     __shared__ DrSmem<kWs, NW> S;
     constexpr bool kSplitV = decltype(S.kv)::kSplitV;
     extern __shared__ float P[];
@@ -595,14 +612,18 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         }
         // the tail thread's copy of the state and the episode's return (it runs every selection)
         int cur_x = 0, cur_y = 0, cur_ret = 0;
-        for (int i = tid; i < kMemoStates; i += blockDim.x) {
+        // an opaque thread id for the episode's LDS initialisation: its addresses are recomputed per
+        // episode instead of being hoisted out of the episode loop and spilled (128-VGPR geometries)
+        int tid_p = tid;
+        asm volatile("" : "+v"(tid_p));
+        for (int i = tid_p; i < kMemoStates; i += blockDim.x) {
             S.memo[i][0] = -1.0f;
             S.memo[i][S.kMemoLg] = __builtin_nanf("");
         }
         // the episode's selection uniforms up front, one thread per step (off the serial
         // select chain of thread 0; ordered before their use by the barriers below)
         if (p.sample) {
-            for (int t = tid; t < p.horizon; t += blockDim.x) {
+            for (int t = tid_p; t < p.horizon; t += blockDim.x) {
                 const int step = ep * p.horizon + t;
                 S.u_ep[t] = p.uniforms ? p.uniforms[(size_t)step * p.N + task]
                                        : philox_uniform(p.seed, p.counter + step, p.first_task + task, DPT_STREAM_SELECT);
@@ -619,7 +640,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 if (j < NBR) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
-            DR_BLOCKS((ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b), u_proj_kv3_n<NB>(P, split0, xn, q, S.kv, qb, M)));
+            DR_BLOCKS((ln_n<NB, J0>(x, xn, P + PL::ln1_g, P + PL::ln1_b), u_proj_kv3_n<NB, J0>(P, split0, xn, q, S.kv, qb, M)));
             if constexpr (kWs) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -645,7 +666,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         S.l0l[qb[j] * 16 + lane] = l[j] * exp2i(-kPExp);
                     }
                 }
-                DR_BLOCKS(l0_cproj<NB>(P, split0, o, l, x, qb, M));
+                DR_BLOCKS(l0_cproj<NB, J0>(P, split0, o, l, x, qb, M));
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     if (j >= NBR) break;
@@ -798,8 +819,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         if constexpr (kWs) {
                             if (own0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
                         } else {
-                            DR_BLOCKS((ln_n<NB>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                                           u_proj3_n<NB>(P, split0, xn, q, M)));
+                            DR_BLOCKS((ln_n<NB, J0>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
+                                           u_proj3_n<NB, J0>(P, split0, xn, q, M)));
                         }
                         if (own0) {  // block 0: key/value (= y) of the query token (the merge below reads them)
                             const int lane = lane_id();
@@ -864,8 +885,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                             }
                         }
                         float xn[2][8];
-                        DR_BLOCKS((ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
-                                   mlp3_n<NB>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
+                        DR_BLOCKS((ln_n<NB, J0>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                                   mlp3_n<NB, J0>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
                     } else
 #endif
                     if (NBR > 0) {
@@ -937,10 +958,10 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         float xn[2][8];
                         // o is the attention output x 2^attn_ey already (the merge's inv)
     #ifndef DPT_DR_SKIP_MLP  // (timing-only diagnostic builds: DPT_DR_SKIP_* leave phases out; results wrong)
-                        DR_BLOCKS((attn_proj3<NB>(P, split0, o, x, M, 1.0f), ln_n<NB>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
-                                       mlp3_n<NB>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
+                        DR_BLOCKS((attn_proj3<NB, J0>(P, split0, o, x, M, 1.0f), ln_n<NB, J0>(x, xn, P + PL::ln2_g, P + PL::ln2_b),
+                                       mlp3_n<NB, J0>(P, split0, xn, x, M.mlp_ew, M.mlp_ex)));
     #else
-                        DR_BLOCKS(attn_proj3<NB>(P, split0, o, x, M, 1.0f));
+                        DR_BLOCKS(attn_proj3<NB, J0>(P, split0, o, x, M, 1.0f));
     #endif
                     }
                     DR_STAMP(1);
@@ -956,7 +977,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 DrTailW tlw;  // the last block's fp32 tail weights (dr_tail_ld_*)
                 for (int layer = 1; layer < L; ++layer) {
                     const bool last = layer == L - 1;
-                    if (DPT_DR_TAIL_LD_EARLY == 2 && last && wave < kFF / 32) {  // in flight across the last layer
+                    if (DPT_DR_TAIL_LD_EARLY == 2 && !kSeqBlocks && last && wave < kFF / 32) {  // in flight across the last layer
                         const float* tw0 = p.frag + (size_t)L * (Frag3::bytes / 4);
                         dr_tail_ld_early(tw0, wave, tlw);
                         dr_tail_ld_late(tw0, wave, tlw);
@@ -967,11 +988,11 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     {
                         float xn[2][8];
                         if (!last) {
-                            DR_BLOCKS((ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
-                                           u_proj_kv3_n<NB>(W, split0.layer(layer), xn, q, kv, qb, M)));
+                            DR_BLOCKS((ln_n<NB, J0>(x, xn, W + PL::ln1_g, W + PL::ln1_b),
+                                           u_proj_kv3_n<NB, J0>(W, split0.layer(layer), xn, q, kv, qb, M)));
                         } else {
                             // the last layer needs q only for token T-1 (block qlast)
-                            DR_BLOCKS((ln_n<NB>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB>(kv, qb, xn, M)));
+                            DR_BLOCKS((ln_n<NB, J0>(x, xn, W + PL::ln1_g, W + PL::ln1_b), kv_from_y<NB, J0>(kv, qb, xn, M)));
     #pragma unroll
                             for (int j = 0; j < 2; ++j) {
                                 if (j < NBR && qb[j] == qlast) {
@@ -1013,7 +1034,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                                 attend(kv, q[j], qb[j], 0, scale, m, l[j], o[j], M, diag_bias);
                             }
                         }
-                        DR_BLOCKS(attn_proj3_ol<NB>(W, split0.layer(layer), o, l, x, M));
+                        DR_BLOCKS(attn_proj3_ol<NB, J0>(W, split0.layer(layer), o, l, x, M));
                     }
     #endif
                     bar_lds();  // every read of this layer's K/V is done
@@ -1021,8 +1042,8 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     #ifndef DPT_DR_SKIP_MLP
                     {
                         float xn[2][8];
-                        DR_BLOCKS((ln_n<NB>(x, xn, W + PL::ln2_g, W + PL::ln2_b),
-                                       mlp3_n<NB>(W, split0.layer(layer), xn, x, M.mlp_ew, M.mlp_ex)));
+                        DR_BLOCKS((ln_n<NB, J0>(x, xn, W + PL::ln2_g, W + PL::ln2_b),
+                                       mlp3_n<NB, J0>(W, split0.layer(layer), xn, x, M.mlp_ew, M.mlp_ex)));
                     }
     #endif
                 }
@@ -1037,7 +1058,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     constexpr int kMlpWaves = kFF / 32;
                     static_assert(kMlpWaves == 4 && NW >= kMlpWaves && kTailWave < kMlpWaves, "four MLP waves");
                     const float* tw = p.frag + (size_t)L * (Frag3::bytes / 4);
-                    if (DPT_DR_TAIL_LD_EARLY == 1 && wave < kMlpWaves) {  // in flight across the attention partials
+                    if (DPT_DR_TAIL_LD_EARLY == 1 && !kSeqBlocks && wave < kMlpWaves) {  // in flight across the attention partials
                         dr_tail_ld_early(tw, wave, tlw);
                         dr_tail_ld_late(tw, wave, tlw);
                     }
@@ -1140,7 +1161,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     // selection and the env step
                     float x1 = 0.f;
                     if (wave < kMlpWaves) {
-                        if (!DPT_DR_TAIL_LD_EARLY) {
+                        if (!DPT_DR_TAIL_LD_EARLY || kSeqBlocks) {  // (the 128-VGPR geometries: after the barrier)
                             dr_tail_ld_early(tw, wave, tlw);
                             dr_tail_ld_late(tw, wave, tlw);
                         }
@@ -1206,9 +1227,13 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         }
         const int R = p.R, H = p.horizon;
         int2 v[2] = {make_int2(0, 0), make_int2(0, 0)};
+        // an opaque thread id: the LDS addresses below are recomputed per episode, not hoisted out
+        // of the episode loop and spilled (the 8- and 16-wave kernels sit at 128 VGPRs)
+        int tid_e = tid;
+        asm volatile("" : "+v"(tid_e));
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int i = tid + h * blockDim.x;
+            const int i = tid_e + h * blockDim.x;
             if (i < R * H) {
                 if (ep < R) v[h] = (i >= ep * H && i < (ep + 1) * H) ? S.cur[i - ep * H] : S.ctx[i];
                 else v[h] = i < (R - 1) * H ? S.ctx[i + H] : S.cur[i - (R - 1) * H];
@@ -1217,7 +1242,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         __syncthreads();
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int i = tid + h * blockDim.x;
+            const int i = tid_e + h * blockDim.x;
             if (i < R * H) S.ctx[i] = v[h];
         }
         __syncthreads();

@@ -372,13 +372,14 @@ __device__ inline Split2 gelu_split(const floatx4& a, const floatx4& b, const Ge
                   __builtin_bit_cast(halfx8, uint4{mm[0], mm[1], mm[2], mm[3]})};
 }
 
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void ln_n(const float (&x)[2][8], float (&xn)[2][8], const float* gam, const float* bet) {
+    static_assert(NB == 1 || J0 == 0, "two blocks start at slot 0");
     if constexpr (NB == 2) {
         ln_cols2(x, xn, gam, bet);
     } else {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) ln_cols(x[j], xn[j], gam, bet);
+        for (int j = J0; j < J0 + NB; ++j) ln_cols(x[j], xn[j], gam, bet);
     }
 }
 
@@ -401,7 +402,7 @@ __device__ inline void resid_add(float (&x)[8], const floatx4& a, const floatx4&
 // per pair of chunks (its K = 32 input is the two chunks' gelu outputs, C-layout).  Products
 // accumulate at scale 2^(mlp_ew + mlp_ex) (the biases enter scaled, exactly) and are scaled
 // back by the exact power of two.
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&x)[2][8],
                               int ew, int ex) {
     const int g = lane_id() >> 4;
@@ -416,7 +417,7 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
     Split2 wf0 = f3.ld2(Frag3::fc, vo), wf1 = f3.ld2(Frag3::fc + 1, vo);
     Split2 xs[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_2 output x 2^mlp_ex (PL)
+    for (int j = J0; j < J0 + NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_2 output x 2^mlp_ex (PL)
 #pragma unroll
     for (int p = 0; p < kFF / 32; ++p) {
         const Split2 w0 = f3.ld2(Frag3::mp + p, vo), w1 = f3.ld2(Frag3::mp + 4 + p, vo);
@@ -424,27 +425,27 @@ __device__ inline void mlp3_n(const float* W, const FragSrc3& f3, const float (&
         const floatx4 fb0 = ld4(W + PL::fc_b + 2 * p * 16 + 4 * g);
         const floatx4 fb1 = ld4(W + PL::fc_b + (2 * p + 1) * 16 + 4 * g);
 #pragma unroll
-        for (int j = 0; j < NB; ++j)
+        for (int j = J0; j < J0 + NB; ++j)
             gs[j] = gelu_split(mfma_x3(wf0, xs[j], fb0), mfma_x3(wf1, xs[j], fb1), gk);
         if (p + 1 < kFF / 32) {
             wf0 = f3.ld2(Frag3::fc + 2 * p + 2, vo);
             wf1 = f3.ld2(Frag3::fc + 2 * p + 3, vo);
         }
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
+        for (int j = J0; j < J0 + NB; ++j) {
             y0[j] = mfma_x3(w0, gs[j], y0[j]);
             y1[j] = mfma_x3(w1, gs[j], y1[j]);
         }
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j) resid_add(x[j], y0[j], y1[j], down);
+    for (int j = J0; j < J0 + NB; ++j) resid_add(x[j], y0[j], y1[j], down);
 }
 
 // u = xn G + g0 of the NB blocks (the folded c_attn: only its q part) on fp16 two-part
 // products (mfma_x3) at scale 2^(attn_ew + attn_ey), returned at 2^attn_eq (the scale of the score
 // product's split query, so attend splits it as it stands); xs = the blocks' LayerNorm outputs
 // split at 2^attn_ey
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void u_proj3_w(const float* W, const Split2 (&wg)[2], const Split2 (&xs)[2], float (&q)[2][8],
                                  const ModelView& M) {
     const int g = lane_id() >> 4;
@@ -454,7 +455,7 @@ __device__ inline void u_proj3_w(const float* W, const Split2 (&wg)[2], const Sp
         const Split2& w = wg[ob];
         const floatx4 bias = ld4(W + PL::attn_b + ob * 16 + 4 * g);  // scaled (PL)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
+        for (int j = J0; j < J0 + NB; ++j) {
             const floatx4 acc = mfma_x3(w, xs[j], bias) * down;
 #pragma unroll
             for (int r = 0; r < 4; ++r) q[j][ob * 4 + r] = acc[r];
@@ -467,41 +468,41 @@ __device__ inline void ld_g(const FragSrc3& f3, Split2 (&wg)[2]) {
     wg[0] = f3.ld2(Frag3::attn, vo);
     wg[1] = f3.ld2(Frag3::attn + 1, vo);
 }
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void u_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&xs)[2], float (&q)[2][8],
                                  const ModelView& M) {
     Split2 wg[2];
     ld_g(f3, wg);
-    u_proj3_w<NB>(W, wg, xs, q, M);
+    u_proj3_w<NB, J0>(W, wg, xs, q, M);
 }
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void u_proj3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8],
                                  const ModelView& M) {
     Split2 xs[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
-    u_proj3_s<NB>(W, f3, xs, q, M);
+    for (int j = J0; j < J0 + NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
+    u_proj3_s<NB, J0>(W, f3, xs, q, M);
 }
 
 // attn_proj on mfma_x3: x^T += Wvp^T o^T + bvp (o, a convex combination of the values y,
 // shares their bound and scale)
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void attn_proj3_w(const float* W, const Split2& w0, const Split2& w1, const Split2 (&os)[2],
                                     float (&x)[2][8], const ModelView& M) {
     const int g = lane_id() >> 4;
     const float down = exp2i(-(M.attn_ew + M.attn_ey));
     const floatx4 b0 = ld4(W + PL::proj_b + 4 * g), b1 = ld4(W + PL::proj_b + 16 + 4 * g);  // scaled (PL)
 #pragma unroll
-    for (int j = 0; j < NB; ++j) resid_add(x[j], mfma_x3(w0, os[j], b0), mfma_x3(w1, os[j], b1), down);
+    for (int j = J0; j < J0 + NB; ++j) resid_add(x[j], mfma_x3(w0, os[j], b0), mfma_x3(w1, os[j], b1), down);
 }
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void attn_proj3_s(const float* W, const FragSrc3& f3, const Split2 (&os)[2], float (&x)[2][8],
                                     const ModelView& M) {
     const int vo = FragSrc3::lane_off();
-    attn_proj3_w<NB>(W, f3.ld2(Frag3::proj, vo), f3.ld2(Frag3::proj + 1, vo), os, x, M);
+    attn_proj3_w<NB, J0>(W, f3.ld2(Frag3::proj, vo), f3.ld2(Frag3::proj + 1, vo), os, x, M);
 }
 // (oscale: the split's scale, 2^attn_ey for an attention output at its true scale)
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const float (&o)[2][8], float (&x)[2][8],
                                   const ModelView& M, float oscale) {
     // the Wvp tiles ahead of the split
@@ -509,21 +510,21 @@ __device__ inline void attn_proj3(const float* W, const FragSrc3& f3, const floa
     const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
     Split2 os[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], oscale);
-    attn_proj3_w<NB>(W, w0, w1, os, x, M);
+    for (int j = J0; j < J0 + NB; ++j) os[j] = split2(o[j], oscale);
+    attn_proj3_w<NB, J0>(W, w0, w1, os, x, M);
 }
 // the same from attend's unnormalised (o, l): o / l is the attention output x 2^attn_ey already,
 // so the split takes 1 / l as its scale (one multiply per value; 1 / l by v_rcp_f32, 1 ulp, instead
 // of the dozen instructions of an IEEE division: -1.1 % at config 3 with the two below)
-template <int NB>
+template <int NB, int J0 = 0>
 __device__ inline void attn_proj3_ol(const float* W, const FragSrc3& f3, const float (&o)[2][8], const float (&l)[2],
                                      float (&x)[2][8], const ModelView& M) {
     const int vo = FragSrc3::lane_off();
     const Split2 w0 = f3.ld2(Frag3::proj, vo), w1 = f3.ld2(Frag3::proj + 1, vo);
     Split2 os[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) os[j] = split2(o[j], __builtin_amdgcn_rcpf(l[j]));
-    attn_proj3_w<NB>(W, w0, w1, os, x, M);
+    for (int j = J0; j < J0 + NB; ++j) os[j] = split2(o[j], __builtin_amdgcn_rcpf(l[j]));
+    attn_proj3_w<NB, J0>(W, w0, w1, os, x, M);
 }
 
 // Folded attention input of the NB blocks qb[]: keys and values are the
@@ -531,11 +532,11 @@ __device__ inline void attn_proj3_ol(const float* W, const FragSrc3& f3, const f
 // C-layout of xn is the layout c_attn's K / V tiles had).  With split keys the
 // split of y at 2^attn_ey (xs, the lane's 8 values are its A-operand k-elements) is
 // what goes to LDS.
-template <int NB, class KV>
+template <int NB, int J0 = 0, class KV>
 __device__ inline void kv_store(KV& S, const int (&qb)[2], const float (&xn)[2][8], const Split2 (&xs)[2]) {
     const int lane = lane_id(), g = lane >> 4;
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
+    for (int j = J0; j < J0 + NB; ++j) {
         const int tok = qb[j] * 16 + (lane & 15);
         if constexpr (KV::kSplitK) {
             if constexpr (KV::kKS) {
@@ -566,18 +567,18 @@ __device__ inline void kv_store(KV& S, const int (&qb)[2], const float (&xn)[2][
         }
     }
 }
-template <int NB, class KV>
+template <int NB, int J0 = 0, class KV>
 __device__ inline void kv_from_y(KV& S, const int (&qb)[2], const float (&xn)[2][8], const ModelView& M) {
     Split2 xs[2];
     if constexpr (KV::kSplitK) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
+        for (int j = J0; j < J0 + NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
     }
-    kv_store<NB>(S, qb, xn, xs);
+    kv_store<NB, J0>(S, qb, xn, xs);
 }
 // both of the above from one split of xn (the u projection's B operand and the keys / values
 // are the same LayerNorm output at the same scale)
-template <int NB, class KV>
+template <int NB, int J0 = 0, class KV>
 __device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const float (&xn)[2][8], float (&q)[2][8],
                                     KV& S, const int (&qb)[2], const ModelView& M) {
     // the G tiles first: their L2 latency runs under the split and the K/V stores
@@ -585,9 +586,9 @@ __device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const fl
     ld_g(f3, wg);
     Split2 xs[2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
-    kv_store<NB>(S, qb, xn, xs);
-    u_proj3_w<NB>(W, wg, xs, q, M);
+    for (int j = J0; j < J0 + NB; ++j) xs[j] = split2(xn[j], 1.0f);  // xn = ln_1 output x 2^attn_ey (PL)
+    kv_store<NB, J0>(S, qb, xn, xs);
+    u_proj3_w<NB, J0>(W, wg, xs, q, M);
 }
 
 // Causal flash attention of query block qb over keys [key_lo, 16*qb + c] (key_lo <= 16):
@@ -828,14 +829,16 @@ __device__ inline void load_layer_params(float* P, const ModelView& M, int tid, 
 }
 
 // One phase over the wave's blocks, dispatched on their count (uniform per wave).
-#define DPT_BLOCKS(nb, CALL)      \
+#define DPT_BLOCKS(nb, ...)       \
     do {                          \
         if ((nb) == 2) {          \
             constexpr int NB = 2; \
-            CALL;                 \
+            constexpr int J0 = 0; \
+            __VA_ARGS__;          \
         } else if ((nb) == 1) {   \
             constexpr int NB = 1; \
-            CALL;                 \
+            constexpr int J0 = 0; \
+            __VA_ARGS__;          \
         }                         \
     } while (0)
 
