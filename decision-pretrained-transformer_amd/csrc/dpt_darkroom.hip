@@ -492,8 +492,18 @@ __global__ void pack_tail_kernel(ModelView M, float* __restrict__ out) {
 // plain pairing.  Which wave computes a block changes no result (-2.2 % at config 3: the 7 blocks
 // of a 101-token window on 4 waves had wave 0 holding blocks 0 and 6 with the key-tile tail,
 // wave 3 the single block 3).  Returns the wave's block count.
+// DPT_DR_SHORT8 (experimental): windows of up to 128 tokens on the 8-wave geometry, one block per
+// wave (two workgroups per CU) instead of the 4-wave one with two blocks per wave (three per CU)
+#ifndef DPT_DR_SHORT8
+#define DPT_DR_SHORT8 0
+#endif
 template <int NW>
 __device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
+    if (DPT_DR_SHORT8 && NW == 8 && nqb <= NW) {
+        qb[0] = wave;
+        qb[1] = wave;
+        return wave < nqb ? 1 : 0;
+    }
     if (nqb < 2 * NW) {
         if (wave == NW - 1) {
             qb[0] = nqb - 1;
@@ -515,14 +525,16 @@ __device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
 #endif
 #define DR_OPQ(v) asm volatile("" : "+s"(v))
 #ifndef DPT_DR_SEQ_BLOCKS
-#define DPT_DR_SEQ_BLOCKS 1
+#define DPT_DR_SEQ_BLOCKS 0
 #endif
 // one phase over the wave's blocks inside the step: specialised on NBC when it is known at compile
 // time (no-op for 0), else dispatched on the run-time count (DPT_BLOCKS)
-// With kSeqBlocks (the register-starved 8- and 16-wave geometries, 128 VGPRs per wave) a two-block
-// wave runs each phase for one block after the other (NB = 1 at slots J0 = 0 and 1): the same
-// arithmetic per block, so the same results, with one block's products and split operands live at a
-// time instead of two.
+// With kSeqBlocks (DPT_DR_SEQ_BLOCKS = 1; the 8- and 16-wave geometries, 128 VGPRs per wave) a
+// two-block wave runs each phase for one block after the other (NB = 1 at slots J0 = 0 and 1): the
+// same arithmetic per block, so the same results (tested bit-identical), with one block's products
+// and split operands live at a time instead of two.  It cuts their scratch from 64 to 16 B/lane but
+// is 3.7 % slower at window 201 and 6 % at 301 (profiles/r6/ab_seq_blocks.json): the two blocks'
+// interleaved chains hide each other's latency, which the spills cost less than.  Off by default.
 #define DR_BLOCKS(...)                                      \
     do {                                                    \
         if constexpr (NBC >= 0) {                           \
@@ -552,6 +564,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? (kWs && DPT_DR_WG3 ? DPT_DR
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     static_assert(kWs || !kTab, "the state table lives in the workspace");
     constexpr bool kSeqBlocks = DPT_DR_SEQ_BLOCKS && NW >= 8;  // DR_BLOCKS
+    // with kSeqBlocks the last layer's fp32 tail weights load after the partials' barrier
+    constexpr bool kTailLate = kSeqBlocks;
     __shared__ DrSmem<kWs, NW> S;
     constexpr bool kSplitV = decltype(S.kv)::kSplitV;
     extern __shared__ float P[];
@@ -977,7 +991,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                 DrTailW tlw;  // the last block's fp32 tail weights (dr_tail_ld_*)
                 for (int layer = 1; layer < L; ++layer) {
                     const bool last = layer == L - 1;
-                    if (DPT_DR_TAIL_LD_EARLY == 2 && !kSeqBlocks && last && wave < kFF / 32) {  // in flight across the last layer
+                    if (DPT_DR_TAIL_LD_EARLY == 2 && !kTailLate && last && wave < kFF / 32) {  // in flight across the last layer
                         const float* tw0 = p.frag + (size_t)L * (Frag3::bytes / 4);
                         dr_tail_ld_early(tw0, wave, tlw);
                         dr_tail_ld_late(tw0, wave, tlw);
@@ -1058,7 +1072,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     constexpr int kMlpWaves = kFF / 32;
                     static_assert(kMlpWaves == 4 && NW >= kMlpWaves && kTailWave < kMlpWaves, "four MLP waves");
                     const float* tw = p.frag + (size_t)L * (Frag3::bytes / 4);
-                    if (DPT_DR_TAIL_LD_EARLY == 1 && !kSeqBlocks && wave < kMlpWaves) {  // in flight across the attention partials
+                    if (DPT_DR_TAIL_LD_EARLY == 1 && !kTailLate && wave < kMlpWaves) {  // in flight across the attention partials
                         dr_tail_ld_early(tw, wave, tlw);
                         dr_tail_ld_late(tw, wave, tlw);
                     }
@@ -1161,7 +1175,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                     // selection and the env step
                     float x1 = 0.f;
                     if (wave < kMlpWaves) {
-                        if (!DPT_DR_TAIL_LD_EARLY || kSeqBlocks) {  // (the 128-VGPR geometries: after the barrier)
+                        if (!DPT_DR_TAIL_LD_EARLY || kTailLate) {  // (the 128-VGPR geometries: after the barrier)
                             dr_tail_ld_early(tw, wave, tlw);
                             dr_tail_ld_late(tw, wave, tlw);
                         }
@@ -1353,8 +1367,10 @@ int launch_rollout_darkroom(const ModelView& M, const float* frag, const dpt_dar
     // keys and values of 512 tokens in LDS) up to 512
     const int64_t window = 1 + (int64_t)a.ctx_episodes * a.horizon;
     const bool ws = p.ws != nullptr;
-    if (window <= DrGeom<4>::kT)
+    if (window <= DrGeom<4>::kT) {
+        if (DPT_DR_SHORT8 && ws && p.tab) return launch_darkroom_geom<true, 8>(M, p, st);
         return ws ? launch_darkroom_geom<true, 4>(M, p, st) : launch_darkroom_geom<false, 4>(M, p, st);
+    }
     if (window <= DrGeom<8>::kT)
         return ws ? launch_darkroom_geom<true, 8>(M, p, st) : launch_darkroom_geom<false, 8>(M, p, st);
     if (!ws) {
@@ -1369,7 +1385,7 @@ int darkroom_max_window() { return DrGeom<kDrMaxWaves>::kT; }
 
 // per task: the stride of the geometry that runs the window (launch_rollout_darkroom's choice)
 int64_t darkroom_workspace_numel(int N, int64_t window) {
-    const int64_t per = window <= DrGeom<4>::kT ? DrGeom<4>::kWsPerTask
+    const int64_t per = window <= DrGeom<4>::kT ? (DPT_DR_SHORT8 ? DrGeom<8>::kWsPerTask : DrGeom<4>::kWsPerTask)
                         : window <= DrGeom<8>::kT ? DrGeom<8>::kWsPerTask
                                                   : DrGeom<kDrMaxWaves>::kWsPerTask;
     return kDrTab + (int64_t)N * per;

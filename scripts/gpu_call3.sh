@@ -8,7 +8,9 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -v -s -m gpu --t
     > gpurun_out/t3.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/t3.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for R in 1 2 3; do
+AB_WL=darkroom AB_DR_R=1 AB_ROUNDS=3 timeout -k 10 400 python scripts/ab_lib.py libdpt_hip_r6base.so libdpt_hip.so \
+    libdpt_hip_short8.so > gpurun_out/ab3_R1.json 2> gpurun_out/ab3_R1.err || exit $?
+for R in 2 3; do
     AB_WL=darkroom AB_DR_R=$R AB_ROUNDS=3 timeout -k 10 400 python scripts/ab_lib.py libdpt_hip_r6base.so libdpt_hip.so \
         libdpt_hip_seq0.so > gpurun_out/ab3_R$R.json 2> gpurun_out/ab3_R$R.err || exit $?
 done
