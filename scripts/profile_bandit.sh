@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=${1:-r1}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="bench.py --no-cpu-baseline --no-darkroom"
+BENCH="bench.py --no-cpu-baseline --no-darkroom --no-linear"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run -- \
     python3 $BENCH --steps 3 --warmup 1 > $OUT/bench_trace.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/pmc_fetch -o run -- \

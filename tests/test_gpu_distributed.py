@@ -110,7 +110,7 @@ def test_two_ranks_on_device_equal_one_process():
 def test_bench_under_torchrun_two_ranks():
     """bench.py --gpus 2 launched by torch.distributed.run (gloo: both ranks on this box's one GPU):
     one JSON line from rank 0 with n_gpus 2, the per-GPU workload unchanged and the whole-job
-    env-step count of both ranks."""
+    env-step count of both ranks, in the headline and in the config-5 / config-4 sub-objects."""
     env = dict(os.environ, DPT_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
@@ -124,6 +124,10 @@ def test_bench_under_torchrun_two_ranks():
     assert line["config"]["tasks_per_gpu"] == 512 and line["config"]["horizon"] == 100
     assert line["config"]["env_steps_per_step"] == 2 * 512 * 100
     assert line["value"] > 0 and line["roofline"]["kernel_ms"] > 0
+    # the config-5 and config-4 sub-objects: every rank's shard, whole-job env steps of both ranks
+    assert line["darkroom_c5_shard"]["config"]["env_steps_per_step"] == 2 * 8192 * 40 * 100
+    assert line["linear_c4_shard"]["config"]["env_steps_per_step"] == 2 * 4096 * 1000
+    assert line["linear_c4_shard"]["value"] > 0 and line["darkroom_c5_shard"]["value"] > 0
 
 
 def _worker_nccl(port, n_bandit, H, q):
