@@ -70,6 +70,12 @@ constexpr int kDrF = 10;                    // token features 2*sd + A + 1
 #endif
 constexpr int kMemoStates = DPT_DR_MEMO_STATES;  // logits memo rows (grids up to 11 x 11)
 
+// DPT_DR_EMB_GLOBAL: the token embedding (10 x 32 floats, read by the episode prologue and the table-free
+// kernels' block-0 re-embedding) from global memory instead of the LDS parameter block (1.25 KB less LDS
+// per workgroup)
+#ifndef DPT_DR_EMB_GLOBAL
+#define DPT_DR_EMB_GLOBAL 0
+#endif
 struct PTop {
     int lnf_g, lnf_b, head_w, head_b, emb_b, wpe0, emb_w, total;
     __host__ __device__ static PTop make(int L) {
@@ -81,7 +87,7 @@ struct PTop {
         t.head_b = o; o += 8;
         t.emb_b = o; o += kE;
         t.wpe0 = o; o += kE;
-        t.emb_w = o; o += kDrF * kE;
+        t.emb_w = o; o += DPT_DR_EMB_GLOBAL ? 0 : kDrF * kE;
         t.total = o;
         return t;
     }
@@ -241,8 +247,8 @@ __device__ inline void l0_cproj(const float* W, const FragSrc3& f3, float (&o)[2
 // the query [state, 0...] at position 0, context transitions after it, zeros
 // past the window.
 template <class Smem>
-__device__ inline void embed_block(const Smem& S, const float* P, const PTop& pt, const float* wpe, int qb, int T,
-                                   float (&x)[8]) {
+__device__ inline void embed_block(const Smem& S, const float* P, const PTop& pt, const float* embw, const float* wpe,
+                                   int qb, int T, float (&x)[8]) {
     const int lane = lane_id(), g = lane >> 4, tok = qb * 16 + (lane & 15);
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = 0.f;
@@ -257,7 +263,7 @@ __device__ inline void embed_block(const Smem& S, const float* P, const PTop& pt
         floatx4 acc = ld4(P + pt.emb_b + d0);
 #pragma unroll
         for (int f = 0; f < 6; ++f) {
-            const floatx4 w = ld4(P + pt.emb_w + rows[f] * kE + d0);
+            const floatx4 w = ld4(embw + rows[f] * kE + d0);
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[r] = fmaf(fv[f], w[r], acc[r]);
         }
@@ -527,6 +533,9 @@ __device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
 #ifndef DPT_DR_SEQ_BLOCKS
 #define DPT_DR_SEQ_BLOCKS 0
 #endif
+#ifndef DPT_DR_SEQ4
+#define DPT_DR_SEQ4 0
+#endif
 // one phase over the wave's blocks inside the step: specialised on NBC when it is known at compile
 // time (no-op for 0), else dispatched on the run-time count (DPT_BLOCKS)
 // With kSeqBlocks (DPT_DR_SEQ_BLOCKS = 1; the 8- and 16-wave geometries, 128 VGPRs per wave) a
@@ -563,7 +572,7 @@ template <bool kWs, int NW, bool kTab = kWs>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? (kWs && DPT_DR_WG3 ? DPT_DR_WG3_N : 2) : (NW == 8 && kWs && DPT_DR_NW8_2 ? 4 : 1))
 rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     static_assert(kWs || !kTab, "the state table lives in the workspace");
-    constexpr bool kSeqBlocks = DPT_DR_SEQ_BLOCKS && NW >= 8;  // DR_BLOCKS
+    constexpr bool kSeqBlocks = (DPT_DR_SEQ_BLOCKS && NW >= 8) || (DPT_DR_SEQ4 && NW == 4);  // DR_BLOCKS
     // with kSeqBlocks the last layer's fp32 tail weights load after the partials' barrier
     constexpr bool kTailLate = kSeqBlocks;
     __shared__ DrSmem<kWs, NW> S;
@@ -593,7 +602,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
         uint4* vs = reinterpret_cast<uint4*>(&S.kv.VT[0][0][0]);
         for (int i = tid; i < (int)(sizeof(S.kv.VT) / 16); i += blockDim.x) vs[i] = uint4{0u, 0u, 0u, 0u};
     }
-    for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
+    if (!DPT_DR_EMB_GLOBAL)
+        for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
+    const float* embw = DPT_DR_EMB_GLOBAL ? M.emb_w : P + pt.emb_w;
 #if !DPT_DR_NO_DIAG_BIAS
     diag_bias_init(S.diag_bias, tid, blockDim.x);
     const float* diag_bias = S.diag_bias;
@@ -653,7 +664,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             float x[2][8], xn[2][8], q[2][8];
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                if (j < NBR) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
+                if (j < NBR) embed_block(S, P, pt, embw, M.wpe, qb[j], T, x[j]);
             DR_BLOCKS((ln_n<NB, J0>(x, xn, P + PL::ln1_g, P + PL::ln1_b), u_proj_kv3_n<NB, J0>(P, split0, xn, q, S.kv, qb, M)));
             if constexpr (kWs) {
 #pragma unroll
@@ -815,14 +826,14 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                                                        : l0_cache<NW>(p, task, 0, qb[j]),
                                     x[j]);
                         } else {
-                            if (qb[j] == 0) embed_block(S, P, pt, M.wpe, 0, T, x[j]);
+                            if (qb[j] == 0) embed_block(S, P, pt, embw, M.wpe, 0, T, x[j]);
                             else ws_load(l0_cache<NW>(p, task, 0, qb[j]), x[j]);
                         }
                     }
                 } else {
     #pragma unroll
                     for (int j = 0; j < 2; ++j)
-                        if (j < NBR) embed_block(S, P, pt, M.wpe, qb[j], T, x[j]);
+                        if (j < NBR) embed_block(S, P, pt, embw, M.wpe, qb[j], T, x[j]);
                 }
 
                 // ---- layer 0: queries of the window (token 0's is never used: it has no
