@@ -536,6 +536,9 @@ __device__ inline int assign_blocks(int wave, int nqb, int (&qb)[2]) {
 #ifndef DPT_DR_SEQ4
 #define DPT_DR_SEQ4 0
 #endif
+#ifndef DPT_DR_HIT_WAVE
+#define DPT_DR_HIT_WAVE 1
+#endif
 // one phase over the wave's blocks inside the step: specialised on NBC when it is known at compile
 // time (no-op for 0), else dispatched on the run-time count (DPT_BLOCKS)
 // With kSeqBlocks (DPT_DR_SEQ_BLOCKS = 1; the 8- and 16-wave geometries, 128 VGPRs per wave) a
@@ -760,7 +763,75 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
             }
         };
         for (int t = 0; t < p.horizon; ++t) {
-            if (p.memo) {
+            if (DPT_DR_HIT_WAVE && p.memo && p.sample) {
+                // the tail wave runs consecutive steps whose state was already queried this episode
+                // (a memo hit needs no forward) as one wave-uniform chain: lane k < 5 reads the row's
+                // cdf value q_k (and lanes 6..10 its logits) in one LDS round trip, the five compares
+                // of select_fast are one ballot, and the state, action, env step and return are
+                // wave-uniform (scalar) values -- instead of thread 0 alone walking the row, the five
+                // compares and the margin tests one dependent instruction after another.  The same
+                // comparisons in fp32 and the same fp64 fallback (cdf_fixed within 2^-15 of an edge):
+                // bit-identical to finish_step.  The other waves wait at one barrier.
+                if (wave == kTailWave) {
+                    DPT_TAIL_PRIO(3);
+                    const int lane = lane_id();
+                    int tt = t;
+                    int cx = __builtin_amdgcn_readfirstlane(cur_x), cy = __builtin_amdgcn_readfirstlane(cur_y);
+                    int cret = __builtin_amdgcn_readfirstlane(cur_ret);
+                    while (tt < p.horizon) {
+                        const int sidx = cx * p.dim + cy;
+                        const float rv = lane < S.kMemoRow ? S.memo[sidx][lane] : 0.0f;
+                        const double u = S.u_ep[tt];
+                        const float q0 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rv)));
+                        if (!(q0 >= 0.0f)) break;  // no stored row: this state needs a forward
+                        const float uf = (float)u;
+                        const unsigned long long le = __builtin_amdgcn_ballot_w64(lane < kDrA && rv <= uf);
+                        const unsigned long long unsafe =
+                            __builtin_amdgcn_ballot_w64(lane < kDrA && !(__builtin_fabsf(rv - uf) > kCdfMargin));
+                        int a = __builtin_popcountll(le);
+                        a = a < kDrA ? a : kDrA - 1;
+                        const int step = ep * p.horizon + tt;
+                        if (unsafe) {  // within 2^-15 of an edge (or a NaN logit): the exact fp64 cdf
+                            float lg[kDrA];
+#pragma unroll
+                            for (int k = 0; k < kDrA; ++k)
+                                lg[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, rv), S.kMemoLg + k));
+                            double qe[kDrA];
+                            cdf_fixed<kDrA>(lg, p.temp, qe);
+                            a = __builtin_amdgcn_readfirstlane(select_from_cdf<kDrA>(qe, u));
+                        }
+                        const int ea = (perm_bits >> (3 * a)) & 7;
+                        int nx = cx + (ea == 0) - (ea == 1);
+                        int ny = cy + (ea == 2) - (ea == 3);
+                        nx = min(max(nx, 0), p.dim - 1);
+                        ny = min(max(ny, 0), p.dim - 1);
+                        const int r = (nx == goal_x && ny == goal_y) ? 1 : 0;
+                        if (lane == 0) {
+                            S.cur[tt] = pack_tr(cx, cy, a, nx, ny, r);
+                            if (p.actions_out) p.actions_out[(size_t)task * steps_total + step] = a;
+                        }
+                        if (p.logits_out && lane >= S.kMemoLg && lane < S.kMemoLg + kDrA)
+                            p.logits_out[((size_t)step * p.N + task) * kDrA + (lane - S.kMemoLg)] = rv;
+                        cx = nx;
+                        cy = ny;
+                        cret += r;
+                        ++tt;
+                    }
+                    cur_x = cx;
+                    cur_y = cy;
+                    cur_ret = cret;
+                    if (lane == 0) {
+                        S.sx = cx;
+                        S.sy = cy;
+                        S.tnext = tt;
+                    }
+                    DPT_TAIL_PRIO(0);
+                }
+                bar_lds();
+                DR_STAMP(2 * L + 4);
+                t = S.tnext;
+                if (t >= p.horizon) break;
+            } else if (p.memo) {
                 // thread 0 runs consecutive steps whose state was already queried this
                 // episode (a memo hit needs no forward); the other threads wait at one
                 // barrier for the first state that needs one

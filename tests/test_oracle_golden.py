@@ -231,6 +231,31 @@ def test_c_darkroom_oracle_matches_reference(tag):
     assert np.array_equal(outs[0]["actions"], outs[1]["actions"])
 
 
+@pytest.mark.parametrize("dim,R,horizon", [(10, 2, 30), (12, 1, 37), (11, 3, 13)])
+def test_c_darkroom_oracle_equals_numpy_oracle(dim, R, horizon):
+    """The vectorised float64 C DarkRoom forward (phase by phase over the tokens, 4-row register
+    blocks, transposed keys padded to 16, libmvec exp) against the plain numpy float64 restatement
+    (oracle/dpt_oracle.py darkroom_online_rollout) at windows that are not multiples of 4 or 16, grids
+    over 10 x 10 and several context episodes: logits within 1e-6 (float32-rounded float64 logits), the
+    same actions and returns."""
+    import torch
+    from oracle import c_oracle
+    import dpt_hip
+    fw, W = weights("darkroom")
+    sd = {k[2:]: torch.from_numpy(v) for k, v in fw.items() if k.startswith("w/")}
+    blob = dpt_hip.pack_weights(sd, 4).numpy()
+    rs = np.random.RandomState(dim * 10 + R)
+    N, Heps = 5, R + 2
+    goals = rs.randint(0, dim, (N, 2))
+    u = rs.uniform(size=(Heps, horizon, N))
+    ref = O.darkroom_online_rollout(W, goals, Heps, R * horizon, horizon, u, True, dim=dim)
+    got = c_oracle.darkroom_rollout(blob, 4, 404, goals, Heps, horizon, R, u.reshape(Heps * horizon, N), True,
+                                    dim=dim, threads=2, want_logits=True)
+    assert np.abs(got["logits"] - ref["logits"]).max() <= 1e-6
+    assert np.array_equal(got["actions"], ref["actions"])
+    assert np.array_equal(got["returns"], ref["returns"])
+
+
 def _bandit_cases():
     """(fixture, weights, means, H, var, u, g, sample, ref actions, ref cum_means, ref rewards, ref logits)
     of every recorded reference bandit rollout (evals/eval_bandit.py:56-103 with the DPT controller)."""
