@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DPT_HIP_LIB: another build's file name in this directory (A/B runs of kernel variants)
 LIB_PATH = os.path.join(_HERE, os.environ.get("DPT_HIP_LIB", "libdpt_hip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 DPT_OK = 0
 DPT_EINVAL = -1

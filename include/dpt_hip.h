@@ -35,7 +35,9 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 6
+/* 7 (round 6): dpt_policy_workspace_numel returns 0 and dpt_policy_rollout_args.workspace may be
+ * NULL (each task's context lives in LDS); DPT_TUNE_POLICY_WAVE accepts only 1 */
+#define DPT_ABI_VERSION 7
 
 /* error codes (mapped to the reference's Python exceptions by dpt_hip/_lib.py) */
 #define DPT_OK 0
