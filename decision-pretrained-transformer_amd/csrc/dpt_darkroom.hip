@@ -112,9 +112,6 @@ struct DrGeom {
 #ifndef DPT_DR_NW8_2
 #define DPT_DR_NW8_2 1
 #endif
-#ifndef DPT_DR_NO_DIAG_BIAS
-#define DPT_DR_NO_DIAG_BIAS 0
-#endif
 #ifndef DPT_DR_WG3_N
 #define DPT_DR_WG3_N 3
 #endif
@@ -150,9 +147,7 @@ struct alignas(16) DrSmem {
     static_assert(kMemoLg >= kDrA && kMemoLg + kDrA <= kMemoRow, "memo row layout");
     alignas(16) float memo[kMemoStates][kMemoRow];
     double u_ep[kFwdT];                // this episode's selection uniforms, one per step
-#if !DPT_DR_NO_DIAG_BIAS
-    alignas(16) float diag_bias[64 * 4];  // the diagonal score tile's causal mask (diag_bias_init)
-#endif
+    alignas(16) float diag_bias[kDiagBiasFloats];  // the masked score tiles' additive rows (diag_bias_init)
     int sx, sy, nfwd, tnext;
 };
 
@@ -604,16 +599,16 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
     if constexpr (kSplitV) {  // finite values in tiles no episode has written yet (attend)
         uint4* vs = reinterpret_cast<uint4*>(&S.kv.VT[0][0][0]);
         for (int i = tid; i < (int)(sizeof(S.kv.VT) / 16); i += blockDim.x) vs[i] = uint4{0u, 0u, 0u, 0u};
+        if constexpr (decltype(S.kv)::kKS) {  // the key tiles too: attend scores the tile past the diagonal
+            uint4* ks = reinterpret_cast<uint4*>(&S.kv.KS[0][0][0]);
+            for (int i = tid; i < (int)(sizeof(S.kv.KS) / 16); i += blockDim.x) ks[i] = uint4{0u, 0u, 0u, 0u};
+        }
     }
     if (!DPT_DR_EMB_GLOBAL)
         for (int i = tid; i < kDrF * kE; i += blockDim.x) P[pt.emb_w + i] = M.emb_w[i];
     const float* embw = DPT_DR_EMB_GLOBAL ? M.emb_w : P + pt.emb_w;
-#if !DPT_DR_NO_DIAG_BIAS
     diag_bias_init(S.diag_bias, tid, blockDim.x);
     const float* diag_bias = S.diag_bias;
-#else
-    const float* diag_bias = nullptr;
-#endif
 
     // the task's goal and action permutation, once (wave-uniform: scalar registers), not
     // reloaded from memory on thread 0's serial select chain every step
@@ -915,8 +910,7 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                         if constexpr (kWs) {
                             if (own0) ln_n<1>(x, xn, P + PL::ln1_g, P + PL::ln1_b);
                         } else {
-                            DR_BLOCKS((ln_n<NB, J0>(x, xn, P + PL::ln1_g, P + PL::ln1_b),
-                                           u_proj3_n<NB, J0>(P, split0, xn, q, M)));
+                            DR_BLOCKS(ln_n<NB, J0>(x, xn, P + PL::ln1_g, P + PL::ln1_b));
                         }
                         if (own0) {  // block 0: key/value (= y) of the query token (the merge below reads them)
                             const int lane = lane_id();
@@ -930,6 +924,9 @@ rollout_darkroom_kernel(ModelView M, DarkroomParams p) {
                                 }
                             }
                         }
+                        // the queries after the store above: no branch between their MFMAs and the
+                        // first reads of q (the wait states stay in one block: attend's note)
+                        if constexpr (!kWs) DR_BLOCKS(u_proj3_n<NB, J0>(P, split0, xn, q, M));
                         bar_lds();
                     }
                     DR_STAMP(0);

@@ -598,7 +598,8 @@ __device__ inline void u_proj_kv3_n(const float* W, const FragSrc3& f3, const fl
 // scores times log2(e) (folded into the scale), so each probability is one v_exp_f32.  o / l is
 // the attention output at the scale of the c_proj product's B operand (attn_proj3_ol).
 // kReduceL = false (split-value form): lsum is returned as this lane's partial, for a caller that
-// reduces two blocks' columns at once (sum_cols2)
+// reduces two blocks' columns at once (sum_cols2).  The split-value form needs diag_bias (the three
+// additive rows of diag_bias_init in LDS).
 template <class KV, bool kReduceL = true>
 __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_lo, float scale, float& m,
                               float& lsum, float (&o)[8], const ModelView& M, const float* diag_bias = nullptr) {
@@ -645,35 +646,28 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int kt = kb + h;
-                if (decltype(masked)::value && kt > qb) {  // wave-uniform
+                if constexpr (decltype(masked)::value) {
+                    // Branch-free masked tile: the score product, then one additive row per tile
+                    // (diag_bias_init: the causal 0 / -inf on the diagonal tile, zeros below it, -inf
+                    // past it; the row is wave-uniform) and the key_lo select, all in the block of the
+                    // MFMA.  A branch between an MFMA and the VALU reading its result leaves the wait
+                    // states to hipcc's hazard recognizer across blocks, which (ROCm 7.2) can count
+                    // too few there (scripts/isa_hazard_cfg.py).  Past the diagonal the keys are
+                    // finite (zeroed at launch), so score + -inf = -inf, as the skipped tile had;
+                    // below it score + 0 (bit-identical softmax).
+                    const int row = kt < qb ? 1 : (kt == qb ? 0 : 2);
+                    const floatx4 b = *reinterpret_cast<const floatx4*>(diag_bias + 256 * row + 4 * lane);
+                    const floatx4 sc = mfma_x3(key_split(S, kt, lane), qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) sv[4 * h + r] = -INFINITY;
+                    for (int r = 0; r < 4; ++r) {
+                        sv[4 * h + r] = sc[r] + b[r];
+                        if (key_lo > 0 && kt * 16 + 4 * g + r < key_lo) sv[4 * h + r] = -INFINITY;
+                    }
                     continue;
                 }
                 const floatx4 sc = mfma_x3(key_split(S, kt, lane), qs, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
                 for (int r = 0; r < 4; ++r) sv[4 * h + r] = sc[r];
-                if constexpr (decltype(masked)::value) {
-                    if (diag_bias) {
-                        // the causal mask of the diagonal tile as an additive 0 / -inf per (lane, r)
-                        // (diag_bias_init): one LDS read and four adds instead of two compares, a
-                        // mask merge and a select per score (-0.9 % at config 3, bit-identical)
-                        if (kt == qb) {
-                            const floatx4 b = *reinterpret_cast<const floatx4*>(diag_bias + 4 * lane);
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) sv[4 * h + r] += b[r];
-                        }
-                        if (key_lo > 0) {
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                if (kt * 16 + 4 * g + r < key_lo) sv[4 * h + r] = -INFINITY;
-                        }
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            if ((kt == qb && 4 * g + r > c) || kt * 16 + 4 * g + r < key_lo) sv[4 * h + r] = -INFINITY;
-                    }
-                }
             }
             const float mt = vmax8(sv);
             if (__builtin_amdgcn_ballot_w64(mt > thr)) {  // wave-uniform
@@ -780,12 +774,14 @@ __device__ inline void attend(const KV& S, const float (&q)[8], int qb, int key_
     }
 }
 
-// The diagonal score tile's causal mask as additive terms: element r of lane (g, c) is key 4g + r
-// of the tile against query c, masked (-inf) when 4g + r > c.  64 x 4 floats in LDS.
+// The masked score tiles' additive terms, three rows of 64 x 4 floats in LDS: row 0 the diagonal
+// tile's causal mask (element r of lane (g, c) is key 4g + r of the tile against query c, -inf when
+// 4g + r > c), row 1 zeros (a tile below the diagonal), row 2 -inf (a tile past it).
+constexpr int kDiagBiasFloats = 3 * 64 * 4;
 __device__ inline void diag_bias_init(float* b, int tid, int nthreads) {
-    for (int i = tid; i < 64 * 4; i += nthreads) {
-        const int lane = i >> 2, r = i & 3;
-        b[i] = 4 * (lane >> 4) + r > (lane & 15) ? -INFINITY : 0.0f;
+    for (int i = tid; i < kDiagBiasFloats; i += nthreads) {
+        const int row = i >> 8, lane = (i >> 2) & 63, r = i & 3;
+        b[i] = row == 1 ? 0.0f : (row == 2 || 4 * (lane >> 4) + r > (lane & 15)) ? -INFINITY : 0.0f;
     }
 }
 
@@ -834,10 +830,12 @@ __device__ inline void load_layer_params(float* P, const ModelView& M, int tid, 
         if ((nb) == 2) {          \
             constexpr int NB = 2; \
             constexpr int J0 = 0; \
+            (void)J0;             \
             __VA_ARGS__;          \
         } else if ((nb) == 1) {   \
             constexpr int NB = 1; \
             constexpr int J0 = 0; \
+            (void)J0;             \
             __VA_ARGS__;          \
         }                         \
     } while (0)

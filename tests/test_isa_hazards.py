@@ -1,0 +1,52 @@
+"""The DarkRoom and prefill kernels' machine code keeps the MFMA wait states on every control-flow path.
+
+hipcc's hazard recognizer (ROCm 7.2, gfx950) sets the wait states between a v_mfma and the VALU /
+LDS instructions that read or overwrite its registers; across basic blocks it can count too few
+(a consumer reached through a taken branch 2-7 issue slots after the MFMA, where straight-line code
+keeps 8).  Such a read returns the register's old contents or not, depending on timing: the
+symptom is a nondeterministic wrong result (a first-pair peel in attend gave NaN logits through one
+such path).  scripts/isa_hazard_cfg.py walks every path of every kernel and compares the distances
+with the smallest ones the compiler keeps in straight-line code; the sources are written so that no
+path comes closer (attend's branch-free masked tiles, the layer-0 query projection after the token-0
+store).  CPU only: hipcc -S for gfx950."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "decision-pretrained-transformer_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+@pytest.mark.parametrize("src", ["dpt_darkroom.hip", "dpt_prefill.hip", "dpt_decode.hip"])
+def test_no_short_mfma_hazard_paths(src, tmp_path):
+    import isa_hazard_cfg
+    out = tmp_path / (src + ".s")
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-slp-vectorize",
+                    "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S", os.path.join(CSRC, src),
+                    "-o", str(out)], check=True, capture_output=True)
+    assert isa_hazard_cfg.scan_all([str(out)]) == 0
+
+
+def test_scanner_finds_a_short_path(tmp_path):
+    """the scanner itself: an MFMA result read 2 slots later through a taken branch is reported"""
+    import isa_hazard_cfg
+    s = tmp_path / "k.s"
+    s.write_text("""_Z1kv:
+\tv_mfma_f32_16x16x32_f16 v[6:9], v[2:5], v[10:13], 0
+\ts_nop 7
+\tv_add_f32_e32 v20, v6, v7
+\tv_mfma_f32_16x16x32_f16 v[6:9], v[2:5], v[10:13], 0
+\ts_cbranch_vccnz .LBB0_2
+\ts_nop 7
+\tv_mov_b32_e32 v8, 0
+.LBB0_2:
+\tv_add_f32_e32 v21, v8, v9
+\ts_endpgm
+.Lfunc_end0:
+""")
+    assert isa_hazard_cfg.scan_all([str(s)]) == 1
