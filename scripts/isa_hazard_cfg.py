@@ -7,8 +7,10 @@ N + 1, every other instruction 1) along any path, and the places where a pair co
 the smallest distance the same pair has in straight-line code (where the compiler's own hazard
 recognizer sets the wait states) -- a cross-block path the recognizer may have missed.  Edges taken
 only with EXEC = 0 (s_cbranch_execz taken, s_cbranch_execnz not taken) are left out.
+--all-producers adds VALU producers with the gfx950 rules of vector_rule() and scans every function.
 
-    python scripts/isa_hazard_cfg.py kernel.s [max_slots]
+    python scripts/isa_hazard_cfg.py kernel.s [max_slots]     (one function, per-pair report)
+    python scripts/isa_hazard_cfg.py --all[-producers] a.s b.s  (every function; exit 1 on a short pair)
 """
 import re
 import sys
@@ -91,6 +93,9 @@ def dst_src(op, args):
     return w, rd, set()
 
 
+ALL_PRODUCERS = False  # --all-producers: VALU / permlane producers too, not only MFMA
+
+
 def main(path, max_slots=24):
     ins, labels = parse(path)
     best = pairs(ins, labels, max_slots)
@@ -148,6 +153,14 @@ def pairs(ins, labels, max_slots):
             seen[key] = d
             jw, jr, jc = info[j]
             jop = ins[j][0]
+            if ALL_PRODUCERS and classify(jop) in ("valu", "permlane"):
+                # a vector producer: every read of what it wrote (VALU -> MFMA operand, -> permlane,
+                # transcendental -> use, ...); the straight-line minima tell which pairs need waits
+                for r in open_regs & jw:
+                    if want[r] in ("RAW", "RAW_C"):
+                        k = (j, i, want[r])
+                        if k not in best or d < best[k][0]:
+                            best[k] = (d, st)
             if classify(jop) == "mfma":
                 hit = open_regs & jw
                 for r in hit:
@@ -209,6 +222,23 @@ def split_functions(path):
     return out
 
 
+TRANS = ("v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_", "v_sin_", "v_cos_")
+
+
+def vector_rule(prod, cons):
+    """wait states after a VALU write (the gfx950 rules hipcc applies; the straight-line code of this
+    library keeps each of them): 2 before an MFMA or a v_permlane reads the register, 1 before
+    v_readlane / v_readfirstlane reads it, 1 after a transcendental before any VALU use"""
+    cc = classify(cons)
+    if cc in ("mfma", "permlane"):
+        return 2
+    if cc == "readlane":
+        return 1
+    if prod.startswith(TRANS) and cc == "valu":
+        return 1
+    return 0
+
+
 def scan_all(paths, max_slots=24):
     """every function of every file: the MFMA / consumer pairs that some path brings closer than the
     smallest distance the compiler keeps for the same (MFMA opcode, hazard, consumer class) in
@@ -217,7 +247,7 @@ def scan_all(paths, max_slots=24):
     funcs = []
     for path in paths:
         for name, text in split_functions(path):
-            if "v_mfma" not in text:
+            if "v_mfma" not in text and not ALL_PRODUCERS:
                 continue
             with tempfile.NamedTemporaryFile("w", suffix=".s", delete=False) as f:
                 f.write(text)
@@ -237,9 +267,12 @@ def scan_all(paths, max_slots=24):
         hits = []
         for (j, i, kind), (d, st) in rows.items():
             k = (ins[j][0], kind, classify(ins[i][0]))
-            if kind == "RAW_C" or classify(ins[i][0]) == "mfma":
-                continue
-            need = rule.get(k, rule.get((ins[j][0], kind, "valu"), 0))
+            if classify(ins[j][0]) == "mfma" and (kind == "RAW_C" or classify(ins[i][0]) == "mfma"):
+                continue  # MFMA -> MFMA: the matrix core's own dependency checks
+            if classify(ins[j][0]) == "mfma":
+                need = rule.get(k, rule.get((ins[j][0], kind, "valu"), 0))
+            else:
+                need = vector_rule(ins[j][0], ins[i][0])
             if d < need:
                 hits.append((d, need, kind, j, i))
         print(f"{path}: {name[:100]}: {len(hits)} short pairs")
@@ -250,6 +283,9 @@ def scan_all(paths, max_slots=24):
 
 
 if __name__ == "__main__":
+    if sys.argv[1] == "--all-producers":
+        ALL_PRODUCERS = True
+        sys.argv[1] = "--all"
     if sys.argv[1] == "--all":
         sys.exit(1 if scan_all(sys.argv[2:]) else 0)
     main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 24)

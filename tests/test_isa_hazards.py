@@ -8,7 +8,8 @@ symptom is a nondeterministic wrong result (a first-pair peel in attend gave NaN
 such path).  scripts/isa_hazard_cfg.py walks every path of every kernel and compares the distances
 with the smallest ones the compiler keeps in straight-line code; the sources are written so that no
 path comes closer (attend's branch-free masked tiles, the layer-0 query projection after the token-0
-store).  CPU only: hipcc -S for gfx950."""
+store).  The scan also applies the VALU rules (2 wait states before an MFMA or v_permlane reads a
+VALU result, 1 before v_readlane, 1 after a transcendental).  CPU only: hipcc -S for gfx950."""
 import os
 import subprocess
 import sys
@@ -29,6 +30,7 @@ def test_no_short_mfma_hazard_paths(src, tmp_path):
     subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-slp-vectorize",
                     "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S", os.path.join(CSRC, src),
                     "-o", str(out)], check=True, capture_output=True)
+    isa_hazard_cfg.ALL_PRODUCERS = True  # the VALU rules too (-> MFMA / permlane / readlane, transcendental)
     assert isa_hazard_cfg.scan_all([str(out)]) == 0
 
 
@@ -49,4 +51,21 @@ def test_scanner_finds_a_short_path(tmp_path):
 \ts_endpgm
 .Lfunc_end0:
 """)
+    isa_hazard_cfg.ALL_PRODUCERS = False
     assert isa_hazard_cfg.scan_all([str(s)]) == 1
+    # a VALU write read by a cross-lane permute 1 slot later on the branch path, a transcendental's
+    # result read at once
+    v = tmp_path / "v.s"
+    v.write_text("""_Z1vv:
+\tv_add_f32_e32 v2, v3, v4
+\ts_cbranch_vccnz .LBB0_2
+\ts_nop 1
+.LBB0_2:
+\tv_permlane32_swap_b32_e32 v2, v5
+\tv_exp_f32_e32 v7, v8
+\tv_add_f32_e32 v9, v7, v7
+\ts_endpgm
+.Lfunc_end0:
+""")
+    isa_hazard_cfg.ALL_PRODUCERS = True
+    assert isa_hazard_cfg.scan_all([str(v)]) == 2
