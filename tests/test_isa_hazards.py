@@ -1,4 +1,4 @@
-"""The DarkRoom and prefill kernels' machine code keeps the MFMA wait states on every control-flow path.
+"""Every kernel's machine code keeps the MFMA (and VALU) wait states on every control-flow path.
 
 hipcc's hazard recognizer (ROCm 7.2, gfx950) sets the wait states between a v_mfma and the VALU /
 LDS instructions that read or overwrite its registers; across basic blocks it can count too few
@@ -23,7 +23,8 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
-@pytest.mark.parametrize("src", ["dpt_darkroom.hip", "dpt_prefill.hip", "dpt_decode.hip"])
+@pytest.mark.parametrize("src", ["dpt_darkroom.hip", "dpt_prefill.hip", "dpt_decode.hip", "dpt_train.hip",
+                                 "dpt_policies.hip", "dpt_env.hip", "dpt_stats.hip", "dpt_abi.hip"])
 def test_no_short_mfma_hazard_paths(src, tmp_path):
     import isa_hazard_cfg
     out = tmp_path / (src + ".s")
