@@ -6,6 +6,7 @@ near-tie draw; logits within 1e-5 at every compared step; per-episode returns ex
 oracle runs in chunks of 512 tasks with a progress line each.  Prints one JSON line per case.
 
     python scripts/dr_full_population.py > gpurun_out/dr_full_population.jsonl
+    python scripts/dr_full_population.py --long   (windows 201 / 301 and the workspace-free dim 12)
 """
 import json
 import os
@@ -27,12 +28,12 @@ LOGIT_TOL = 1e-5
 CHUNK = 512
 
 
-def case(label, N, seed, ctr, first_task, goals):
-    Heps, horizon, L = 40, 100, 4
+def case(label, N, seed, ctr, first_task, goals, R=1, dim=10, Heps=40):
+    horizon, L = 100, 4
     steps = Heps * horizon
-    sd, _ = bench.synthetic_state_dict(L, 2, 5, horizon)
-    m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + horizon))
-    out = m.rollout_darkroom(goals, Heps, horizon, 1, seed=seed, counter=ctr, first_task=first_task,
+    sd, _ = bench.synthetic_state_dict(L, 2, 5, R * horizon)
+    m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + R * horizon))
+    out = m.rollout_darkroom(goals, Heps, horizon, R, dim=dim, seed=seed, counter=ctr, first_task=first_task,
                              want_actions=True, want_logits=True)
     lg_all = out["logits"].cpu().numpy()
     acts_all = out["actions"].cpu().numpy()
@@ -43,8 +44,8 @@ def case(label, N, seed, ctr, first_task, goals):
         tasks = np.arange(lo, min(N, lo + CHUNK))
         u = np.stack([philox_np.uniform(seed, ctr + k, first_task + tasks, dpt_hip.STREAM_SELECT)
                       for k in range(steps)])
-        ref = c_oracle.darkroom_rollout(blob, L, 4 * (1 + horizon), goals[tasks], Heps, horizon, 1, u, True,
-                                        threads=bench.host_cpus()[0], want_logits=True)
+        ref = c_oracle.darkroom_rollout(blob, L, 4 * (1 + R * horizon), goals[tasks], Heps, horizon, R, u, True,
+                                        dim=dim, threads=bench.host_cpus()[0], want_logits=True)
         n = compared_steps(acts_all[tasks], ref["actions"], ref["margin"])
         for j, t in enumerate(tasks):
             k = min(n[j] + 1, steps)
@@ -54,7 +55,7 @@ def case(label, N, seed, ctr, first_task, goals):
         n_all.append(n)
         print(f"{label}: tasks {lo}..{tasks[-1]} done, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
     n = np.concatenate(n_all)
-    res = {"case": label, "tasks": int(N), "steps_per_task": steps,
+    res = {"case": label, "tasks": int(N), "steps_per_task": steps, "window": 1 + R * horizon, "dim": dim,
            "task_steps_compared_frac": float(n.sum()) / (N * steps),
            "tasks_identical_all_steps_frac": float((n == steps).mean()),
            "tasks_with_a_near_tie_flip": int((n < steps).sum()),
@@ -66,8 +67,16 @@ def case(label, N, seed, ctr, first_task, goals):
 
 
 def main():
-    ok = case("C3_all_4096", 4096, 99, 3, 0, darkroom_config(4096))
-    ok &= case("C5_shard0_all_8192", 8192, 1234, 0, 0, darkroom_config(65536)[:8192])
+    if "--long" in sys.argv:
+        # the reference's longer contexts (H = 200 / 300 with horizon 100: windows 201 / 301), and the
+        # workspace-free kernels (dim 12: 144 cells, no per-state table), on every task of smaller batches
+        goals12 = np.random.RandomState(5).randint(0, 12, (1024, 2))
+        ok = case("window201_all_1024", 1024, 7, 0, 0, darkroom_config(1024), R=2, Heps=20)
+        ok &= case("window301_all_512", 512, 8, 0, 0, darkroom_config(512), R=3, Heps=12)
+        ok &= case("dim12_window201_all_1024", 1024, 9, 0, 0, goals12, R=2, dim=12, Heps=20)
+    else:
+        ok = case("C3_all_4096", 4096, 99, 3, 0, darkroom_config(4096))
+        ok &= case("C5_shard0_all_8192", 8192, 1234, 0, 0, darkroom_config(65536)[:8192])
     sys.exit(0 if ok else 1)
 
 
