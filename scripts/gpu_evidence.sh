@@ -14,7 +14,7 @@ CSRC=decision-pretrained-transformer_amd/csrc
     echo "library_sha256 $(sha256sum $LIB | cut -d' ' -f1)"
     echo "library_built_from $(cat $LIB.srchash 2>/dev/null || echo missing)"
     now=$(cd $CSRC && cat dpt_abi.hip dpt_decode.hip dpt_env.hip dpt_policies.hip dpt_darkroom.hip dpt_prefill.hip \
-          dpt_stats.hip dpt_train.hip dpt_common.h dpt_mfma_fwd.h dpt_linucb.h ../../include/dpt_hip.h | sha256sum | cut -d' ' -f1)
+          dpt_stats.hip dpt_train.hip dpt_common.h dpt_mfma_fwd.h dpt_linucb.h ../../include/dpt_hip.h Makefile | sha256sum | cut -d' ' -f1)
     echo "pushed_sources $now"
     if [ "$now" = "$(cat $LIB.srchash 2>/dev/null)" ]; then echo "library matches the pushed sources: yes"
     else echo "library matches the pushed sources: NO"; fi

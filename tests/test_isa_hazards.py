@@ -22,6 +22,15 @@ HIPCC = "/opt/rocm/bin/hipcc"
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 
+def file_flags(src):
+    """the Makefile's per-file code-generation flags (FLAGS_<name> := ...) for this source"""
+    name = src.rsplit(".", 1)[0]
+    for line in open(os.path.join(CSRC, "Makefile")):
+        if line.startswith(f"FLAGS_{name} :="):
+            return line.split(":=", 1)[1].split()
+    return []
+
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
 @pytest.mark.parametrize("src", ["dpt_darkroom.hip", "dpt_prefill.hip", "dpt_decode.hip", "dpt_train.hip",
                                  "dpt_policies.hip", "dpt_env.hip", "dpt_stats.hip", "dpt_abi.hip"])
@@ -29,8 +38,8 @@ def test_no_short_mfma_hazard_paths(src, tmp_path):
     import isa_hazard_cfg
     out = tmp_path / (src + ".s")
     subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-slp-vectorize",
-                    "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S", os.path.join(CSRC, src),
-                    "-o", str(out)], check=True, capture_output=True)
+                    "-I" + os.path.join(ROOT, "include"), *file_flags(src), "--cuda-device-only", "-S",
+                    os.path.join(CSRC, src), "-o", str(out)], check=True, capture_output=True)
     isa_hazard_cfg.ALL_PRODUCERS = True  # the VALU rules too (-> MFMA / permlane / readlane, transcendental)
     assert isa_hazard_cfg.scan_all([str(out)]) == 0
 
