@@ -6,7 +6,8 @@ near-tie draw; logits within 1e-5 at every compared step; per-episode returns ex
 oracle runs in chunks of 512 tasks with a progress line each.  Prints one JSON line per case.
 
     python scripts/dr_full_population.py > gpurun_out/dr_full_population.jsonl
-    python scripts/dr_full_population.py --long   (windows 201 / 301 and the workspace-free dim 12)
+    python scripts/dr_full_population.py --long       (windows 201 / 301 and the workspace-free dim 12)
+    python scripts/dr_full_population.py --variants   (config 3 greedy, and with permuted actions)
 """
 import json
 import os
@@ -28,13 +29,13 @@ LOGIT_TOL = 1e-5
 CHUNK = 512
 
 
-def case(label, N, seed, ctr, first_task, goals, R=1, dim=10, Heps=40):
+def case(label, N, seed, ctr, first_task, goals, R=1, dim=10, Heps=40, sample=True, perms=None):
     horizon, L = 100, 4
     steps = Heps * horizon
     sd, _ = bench.synthetic_state_dict(L, 2, 5, R * horizon)
     m = dpt_hip.DeviceModel(sd, L, 2, 5, 4 * (1 + R * horizon))
-    out = m.rollout_darkroom(goals, Heps, horizon, R, dim=dim, seed=seed, counter=ctr, first_task=first_task,
-                             want_actions=True, want_logits=True)
+    out = m.rollout_darkroom(goals, Heps, horizon, R, dim=dim, perms=perms, sample=sample, seed=seed, counter=ctr,
+                             first_task=first_task, want_actions=True, want_logits=True)
     lg_all = out["logits"].cpu().numpy()
     acts_all = out["actions"].cpu().numpy()
     rets_all = out["returns"].cpu().numpy()
@@ -43,9 +44,10 @@ def case(label, N, seed, ctr, first_task, goals, R=1, dim=10, Heps=40):
     for lo in range(0, N, CHUNK):
         tasks = np.arange(lo, min(N, lo + CHUNK))
         u = np.stack([philox_np.uniform(seed, ctr + k, first_task + tasks, dpt_hip.STREAM_SELECT)
-                      for k in range(steps)])
-        ref = c_oracle.darkroom_rollout(blob, L, 4 * (1 + R * horizon), goals[tasks], Heps, horizon, R, u, True,
-                                        dim=dim, threads=bench.host_cpus()[0], want_logits=True)
+                      for k in range(steps)]) if sample else None
+        ref = c_oracle.darkroom_rollout(blob, L, 4 * (1 + R * horizon), goals[tasks], Heps, horizon, R, u, sample,
+                                        perms=None if perms is None else perms[tasks], dim=dim,
+                                        threads=bench.host_cpus()[0], want_logits=True)
         n = compared_steps(acts_all[tasks], ref["actions"], ref["margin"])
         for j, t in enumerate(tasks):
             k = min(n[j] + 1, steps)
@@ -67,7 +69,14 @@ def case(label, N, seed, ctr, first_task, goals, R=1, dim=10, Heps=40):
 
 
 def main():
-    if "--long" in sys.argv:
+    if "--variants" in sys.argv:
+        # config 3's population greedy (argmax: no draw, so every step must agree) and with a random
+        # action permutation per task (the reference's permuted DarkRoom), sampled
+        from oracle import dpt_oracle
+        perms = dpt_oracle.perm_table()[np.random.RandomState(6).randint(0, 120, 4096)].astype(np.int32)
+        ok = case("C3_greedy_all_4096", 4096, 0, 0, 0, darkroom_config(4096), sample=False)
+        ok &= case("C3_permuted_all_4096", 4096, 11, 0, 0, darkroom_config(4096), perms=perms)
+    elif "--long" in sys.argv:
         # the reference's longer contexts (H = 200 / 300 with horizon 100: windows 201 / 301), and the
         # workspace-free kernels (dim 12: 144 cells, no per-state table), on every task of smaller batches
         goals12 = np.random.RandomState(5).randint(0, 12, (1024, 2))
