@@ -8,6 +8,7 @@ oracle runs in chunks of 512 tasks with a progress line each.  Prints one JSON l
     python scripts/dr_full_population.py > gpurun_out/dr_full_population.jsonl
     python scripts/dr_full_population.py --long       (windows 201 / 301 and the workspace-free dim 12)
     python scripts/dr_full_population.py --variants   (config 3 greedy, and with permuted actions)
+    python scripts/dr_full_population.py --lastshard  (config 5's last shard)
 """
 import json
 import os
@@ -69,7 +70,9 @@ def case(label, N, seed, ctr, first_task, goals, R=1, dim=10, Heps=40, sample=Tr
 
 
 def main():
-    if "--variants" in sys.argv:
+    if "--lastshard" in sys.argv:  # config 5's last rank (global tasks 57344..65535)
+        ok = case("C5_shard7_all_8192", 8192, 1234, 0, 57344, darkroom_config(65536)[57344:])
+    elif "--variants" in sys.argv:
         # config 3's population greedy (argmax: no draw, so every step must agree) and with a random
         # action permutation per task (the reference's permuted DarkRoom), sampled
         from oracle import dpt_oracle
